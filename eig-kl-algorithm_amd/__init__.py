@@ -1,0 +1,386 @@
+"""eig-kl-algorithm_amd — Python mirror of the MI355X EIG+KL bipartitioner.
+
+A thin ctypes layer over ``build/libeigkl_hip.so`` (C-ABI: include/eigkl.h).
+It mirrors the reference's surface (yhinai/EIG-KL-Algorithm):
+
+* ``cEIG(path)``, ``cKL(path, EIG=False)``, ``gKL(...)``, ``gKL2(...)`` run the
+  drop-in tools in-process with the reference's argv/CWD semantics
+  (cEIG.cpp:138-237, cKL.cpp:424-468, gKL.cu:672-713, gKL2.cu:989-1033);
+* ``Hypergraph`` (read / generate / clique expansions), ``Context`` (SpMV seam,
+  Lanczos Fiedler solver, KL swap loop) expose the hot path piecewise.
+
+There is no CPU fallback: importing fails loudly when the HIP library has not
+been built, and GPU calls raise ``EKError`` when no gfx950 device is usable.
+The directory name is not a Python identifier; load it with
+``importlib`` (see ``load()`` in tests/conftest.py or __graft_entry__.py).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libeigkl_hip.so")
+BIN_DIR = os.path.join(HERE, "build", "bin")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is not built: run `make -C {HERE}` "
+                      "(the HIP path has no CPU fallback)")
+
+_lib = ctypes.CDLL(LIB_PATH)
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+
+EK_OK, EK_EINVAL, EK_EIO, EK_EHIP, EK_ENOMEM, EK_ENOCONV, EK_ESTATE, EK_ECOMM = 0, -1, -2, -3, -4, -5, -6, -7
+
+SWAP_DTYPE = np.dtype([("iter", "<u4"), ("node_left", "<u4"), ("node_right", "<u4"),
+                       ("max_gain", "<f4"), ("min_gain", "<f4"), ("gain", "<f4"),
+                       ("cut", "<f4"), ("pad", "<u4")])
+
+
+class LanczosOpts(ctypes.Structure):
+    _fields_ = [("ncv", _I32), ("maxit", _I32), ("tol", ctypes.c_double), ("deflate", _I32),
+                ("time_spmv", _I32)]
+
+
+class LanczosStats(ctypes.Structure):
+    _fields_ = [("restarts", _I32), ("matvecs", _I32), ("converged", _I32), ("residual", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double), ("spmv_timed", _I32),
+                ("comm_ms", ctypes.c_double)]
+
+
+class KLResult(ctypes.Structure):
+    _fields_ = [("iterations", _I64), ("initial_cut", ctypes.c_float), ("best_cut", ctypes.c_float),
+                ("final_cut", ctypes.c_float), ("best_iter", _I64), ("net_cut_initial", _I64),
+                ("net_cut_best", _I64), ("net_cut_final", _I64), ("loop_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double)]
+
+
+def _sig(name, res, *args):
+    fn = getattr(_lib, name)
+    fn.restype = res
+    fn.argtypes = list(args)
+    return fn
+
+
+_sig("ek_last_error", ctypes.c_char_p)
+_sig("ek_version", ctypes.c_char_p)
+_sig("ek_hgr_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_P))
+_sig("ek_hgr_generate", ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.POINTER(_P))
+_sig("ek_hgr_from_pins", ctypes.c_int, _I64, _I64, _P, _P, ctypes.POINTER(_P))
+_sig("ek_hgr_write", ctypes.c_int, _P, ctypes.c_char_p)
+_sig("ek_hgr_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
+_sig("ek_hgr_copy_pins", ctypes.c_int, _P, _P, _P)
+_sig("ek_hgr_free", None, _P)
+_sig("ek_laplacian_build", ctypes.c_int, _P, ctypes.POINTER(_P))
+_sig("ek_kl_graph_build", ctypes.c_int, _P, ctypes.POINTER(_P))
+_sig("ek_csr_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I32))
+_sig("ek_csr_copy", ctypes.c_int, _P, _P, _P, _P, _P)
+_sig("ek_csr_free", None, _P)
+_sig("ek_shard_rows", ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I64),
+     ctypes.POINTER(_I64), ctypes.POINTER(_I64))
+_sig("ek_device_count", ctypes.c_int, ctypes.POINTER(ctypes.c_int))
+_sig("ek_init", ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P))
+_sig("ek_destroy", None, _P)
+_sig("ek_get_stream", ctypes.c_int, _P, ctypes.POINTER(_P))
+_sig("ek_comm_unique_id", ctypes.c_int, _P)
+_sig("ek_comm_init", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P)
+_sig("ek_spmv_setup", ctypes.c_int, _P, _I64, _I64, _I64, _P, _P, _P)
+_sig("ek_spmv", ctypes.c_int, _P, _P, _P, _P)
+_sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
+_sig("ek_spmv_bytes", _I64, _P)
+_sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
+_sig("ek_lanczos_fiedler", ctypes.c_int, _P, ctypes.POINTER(LanczosOpts), ctypes.POINTER(ctypes.c_double), _P,
+     ctypes.POINTER(LanczosStats))
+_sig("ek_median_split", ctypes.c_int, _I64, _P, ctypes.POINTER(ctypes.c_double), _P)
+_sig("ek_align_sign", ctypes.c_int, _I64, _P, _P)
+_sig("ek_eig_write", ctypes.c_int, ctypes.c_char_p, _I64, ctypes.c_double, ctypes.c_double, _P, _P)
+_sig("ek_eig_read", ctypes.c_int, ctypes.c_char_p, _I64, ctypes.POINTER(ctypes.c_double),
+     ctypes.POINTER(ctypes.c_double), _P, _P, _P, ctypes.POINTER(_I64), _P, ctypes.POINTER(_I64))
+_sig("ek_kl_graph_setup", ctypes.c_int, _P, _I64, _P, _P, _P)
+_sig("ek_kl_nets_setup", ctypes.c_int, _P, _I64, _P, _P)
+_sig("ek_kl_set_partition", ctypes.c_int, _P, _P, _I64, _P, _I64)
+_sig("ek_kl_run", ctypes.c_int, _P, _I32, _P, _I64, ctypes.POINTER(KLResult))
+_sig("ek_kl_sides", ctypes.c_int, _P, _I32, _P)
+_sig("ek_cli_main", ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p))
+
+lib = _lib
+
+
+class EKError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what}: {_lib.ek_last_error().decode(errors='replace')} (status {code})")
+        self.code = code
+
+
+def _chk(rc, what):
+    if rc != EK_OK:
+        raise EKError(rc, what)
+
+
+def _p(a):
+    return a.ctypes.data_as(_P) if a is not None else None
+
+
+def version():
+    return _lib.ek_version().decode()
+
+
+# ---------------------------------------------------------------------------
+# host side
+class CSR:
+    def __init__(self, rowptr, col, val, nfwd=None):
+        self.rowptr, self.col, self.val, self.nfwd = rowptr, col, val, nfwd
+
+    @property
+    def nrows(self):
+        return len(self.rowptr) - 1
+
+    @property
+    def nnz(self):
+        return len(self.col)
+
+
+def _take_csr(handle):
+    nr, nnz, vb = _I64(), _I64(), _I32()
+    _lib.ek_csr_dims(handle, ctypes.byref(nr), ctypes.byref(nnz), ctypes.byref(vb))
+    rowptr = np.empty(nr.value + 1, np.int32)
+    col = np.empty(nnz.value, np.int32)
+    val = np.empty(nnz.value, np.float64 if vb.value == 8 else np.float32)
+    nfwd = np.empty(nr.value, np.int32) if vb.value == 4 else None
+    _lib.ek_csr_copy(handle, _p(rowptr), _p(col), _p(val), _p(nfwd))
+    _lib.ek_csr_free(handle)
+    return CSR(rowptr, col, val, nfwd)
+
+
+class Hypergraph:
+    """A .hgr circuit (cKL.cpp:84-116 / cEIG.cpp:177-182 readers)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def read(cls, path):
+        h = _P()
+        _chk(_lib.ek_hgr_read(os.fsencode(path), ctypes.byref(h)), f"read {path}")
+        return cls(h)
+
+    @classmethod
+    def generate(cls, multiplier=1.0, seed=1):
+        """Seeded ISPD98-shaped synthetic circuit (circuit_generator.py:41-59)."""
+        h = _P()
+        _chk(_lib.ek_hgr_generate(float(multiplier), int(seed), ctypes.byref(h)), "generate")
+        return cls(h)
+
+    @classmethod
+    def from_pins(cls, nodes, net_ptr, pins):
+        net_ptr = np.ascontiguousarray(net_ptr, np.int64)
+        pins = np.ascontiguousarray(pins, np.int32)
+        h = _P()
+        _chk(_lib.ek_hgr_from_pins(len(net_ptr) - 1, int(nodes), _p(net_ptr), _p(pins), ctypes.byref(h)),
+             "from_pins")
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.ek_hgr_free(self._h)
+            self._h = None
+
+    def dims(self):
+        a, b, c = _I64(), _I64(), _I64()
+        _lib.ek_hgr_dims(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    @property
+    def nets(self):
+        return self.dims()[0]
+
+    @property
+    def nodes(self):
+        return self.dims()[1]
+
+    def pins(self):
+        nets, _, npins = self.dims()
+        net_ptr = np.empty(nets + 1, np.int64)
+        pins = np.empty(npins, np.int32)
+        _lib.ek_hgr_copy_pins(self._h, _p(net_ptr), _p(pins))
+        return net_ptr, pins
+
+    def write(self, path):
+        _chk(_lib.ek_hgr_write(self._h, os.fsencode(path)), f"write {path}")
+
+    def laplacian(self):
+        """fp64 clique Laplacian (cEIG.cpp:86-133)."""
+        c = _P()
+        _chk(_lib.ek_laplacian_build(self._h, ctypes.byref(c)), "laplacian")
+        return _take_csr(c)
+
+    def kl_graph(self):
+        """fp32 KL adjacency in cKL summation order (cKL.cpp:84-149, 225-251)."""
+        c = _P()
+        _chk(_lib.ek_kl_graph_build(self._h, ctypes.byref(c)), "kl_graph")
+        return _take_csr(c)
+
+
+def shard_rows(n, nranks, rank):
+    a, b, c = _I64(), _I64(), _I64()
+    _chk(_lib.ek_shard_rows(int(n), int(nranks), int(rank), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+         "shard_rows")
+    return a.value, b.value, c.value
+
+
+def median_split(v):
+    """cEIG.cpp:55-65, 218: median and bits = (median > v)."""
+    v = np.ascontiguousarray(v, np.float64)
+    med = ctypes.c_double()
+    bits = np.empty(len(v), np.uint8)
+    _chk(_lib.ek_median_split(len(v), _p(v), ctypes.byref(med), _p(bits)), "median_split")
+    return med.value, bits
+
+
+def eig_write(path, lam, median, bits, v):
+    bits = np.ascontiguousarray(bits, np.uint8)
+    v = np.ascontiguousarray(v, np.float64)
+    _chk(_lib.ek_eig_write(os.fsencode(path), len(v), float(lam), float(median), _p(bits), _p(v)), "eig_write")
+
+
+def eig_read(path, n):
+    """pre_saved_EIG file as cKL reads it (cKL.cpp:155-174)."""
+    lam, med = ctypes.c_double(), ctypes.c_double()
+    bits = np.zeros(n, np.uint8)
+    v = np.zeros(n, np.float64)
+    o0 = np.empty(n, np.int32)
+    o1 = np.empty(n, np.int32)
+    n0, n1 = _I64(), _I64()
+    _chk(_lib.ek_eig_read(os.fsencode(path), n, ctypes.byref(lam), ctypes.byref(med), _p(bits), _p(v), _p(o0),
+                          ctypes.byref(n0), _p(o1), ctypes.byref(n1)), f"eig_read {path}")
+    return lam.value, med.value, bits, v, o0[: n0.value].copy(), o1[: n1.value].copy()
+
+
+def device_count():
+    c = ctypes.c_int()
+    _lib.ek_device_count(ctypes.byref(c))
+    return c.value
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    _chk(_lib.ek_comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf.raw)
+
+
+# ---------------------------------------------------------------------------
+# GPU side
+class Context:
+    """One MI355X (gfx950) device: SpMV seam, Lanczos Fiedler solver, KL loop."""
+
+    def __init__(self, device=0):
+        self._c = _P()
+        _chk(_lib.ek_init(int(device), ctypes.byref(self._c)), "ek_init")
+        self.n = 0
+        self.nrows = 0
+
+    def close(self):
+        if getattr(self, "_c", None):
+            _lib.ek_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def stream(self):
+        s = _P()
+        _chk(_lib.ek_get_stream(self._c, ctypes.byref(s)), "stream")
+        return s.value
+
+    def comm_init(self, nranks, rank, uid):
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        _chk(_lib.ek_comm_init(self._c, int(nranks), int(rank), buf), "comm_init")
+
+    # SpMV seam (SparseSymMatProd::perform_op, cEIG.cpp:194)
+    def spmv_setup(self, n, row0, rowptr, col, val):
+        rowptr = np.ascontiguousarray(rowptr, np.int32)
+        col = np.ascontiguousarray(col, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        nrows = len(rowptr) - 1
+        _chk(_lib.ek_spmv_setup(self._c, int(n), int(row0), nrows, _p(rowptr), _p(col), _p(val)), "spmv_setup")
+        self.n, self.nrows = int(n), nrows
+
+    def spmv_host(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.empty(self.nrows, np.float64)
+        _chk(_lib.ek_spmv_host(self._c, _p(x), _p(y)), "spmv")
+        return y
+
+    def spmv_device(self, x_ptr, y_ptr, stream=None):
+        _chk(_lib.ek_spmv(self._c, x_ptr, y_ptr, stream), "spmv")
+
+    def spmv_bytes(self):
+        return _lib.ek_spmv_bytes(self._c)
+
+    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False):
+        """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207)."""
+        o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0)
+        st = LanczosStats()
+        lam = ctypes.c_double()
+        v = np.empty(self.n, np.float64)
+        _chk(_lib.ek_lanczos_fiedler(self._c, ctypes.byref(o), ctypes.byref(lam), _p(v), ctypes.byref(st)),
+             "lanczos_fiedler")
+        return lam.value, v, {k: getattr(st, k) for k, _ in LanczosStats._fields_}
+
+    # KL (cKL.cpp:288-406)
+    def kl_graph_setup(self, csr):
+        self.kl_n = csr.nrows
+        _chk(_lib.ek_kl_graph_setup(self._c, csr.nrows, _p(np.ascontiguousarray(csr.rowptr, np.int32)),
+                                    _p(np.ascontiguousarray(csr.col, np.int32)),
+                                    _p(np.ascontiguousarray(csr.val, np.float32))), "kl_graph_setup")
+
+    def kl_nets_setup(self, net_ptr, pins):
+        net_ptr = np.ascontiguousarray(net_ptr, np.int64)
+        pins = np.ascontiguousarray(pins, np.int32)
+        _chk(_lib.ek_kl_nets_setup(self._c, len(net_ptr) - 1, _p(net_ptr), _p(pins)), "kl_nets_setup")
+
+    def kl_set_partition(self, order0, order1):
+        self._o0 = np.ascontiguousarray(order0, np.int32)
+        self._o1 = np.ascontiguousarray(order1, np.int32)
+        _chk(_lib.ek_kl_set_partition(self._c, _p(self._o0), len(self._o0), _p(self._o1), len(self._o1)),
+             "kl_set_partition")
+
+    def kl_run(self, limit=-1, cap=None):
+        cap = min(len(self._o0), len(self._o1)) if cap is None else cap
+        log = np.zeros(max(cap, 1), SWAP_DTYPE)
+        r = KLResult()
+        _chk(_lib.ek_kl_run(self._c, int(limit), _p(log), cap, ctypes.byref(r)), "kl_run")
+        res = {k: getattr(r, k) for k, _ in KLResult._fields_}
+        return log[: min(r.iterations, cap)], res
+
+    def kl_sides(self, which):
+        out = np.empty(self.kl_n, np.uint8)
+        _chk(_lib.ek_kl_sides(self._c, int(which), _p(out)), "kl_sides")
+        return out
+
+
+# ---------------------------------------------------------------------------
+# drop-in tools, in-process (same argv / CWD semantics as the executables)
+def _cli(tool, *args):
+    argv = [tool.encode()] + [os.fsencode(str(a)) for a in args]
+    arr = (ctypes.c_char_p * len(argv))(*argv)
+    return _lib.ek_cli_main(tool.encode(), len(argv), arr)
+
+
+def cEIG(path, *flags):
+    return _cli("cEIG", path, *flags)
+
+
+def cKL(path, EIG=False, *flags):
+    return _cli("cKL", path, *(["-EIG"] if EIG else []), *flags)
+
+
+def gKL(path, EIG=False, *flags):
+    return _cli("gKL", path, *(["-EIG"] if EIG else []), *flags)
+
+
+def gKL2(path, EIG=False, *flags):
+    return _cli("gKL2", path, *(["-EIG"] if EIG else []), *flags)

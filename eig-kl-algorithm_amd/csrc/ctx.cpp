@@ -1,0 +1,745 @@
+// GPU context, SpMV seam, implicitly restarted Lanczos driver and KL driver
+// of libeigkl_hip.so (host code over the HIP runtime + RCCL).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <memory>
+
+#include "ek_internal.hpp"
+
+#define HIPCHK(call)                                                                                 \
+    do {                                                                                             \
+        const hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess) ek::fail(EK_EHIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                                       __FILE__, __LINE__);                                          \
+    } while (0)
+#define NCCLCHK(call)                                                                                 \
+    do {                                                                                              \
+        const ncclResult_t r_ = (call);                                                               \
+        if (r_ != ncclSuccess) ek::fail(EK_ECOMM, "%s failed: %s", #call, ncclGetErrorString(r_));    \
+    } while (0)
+
+namespace {
+
+// Owning device allocation.
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t b) {
+        if (b <= bytes && p) return;
+        reset();
+        HIPCHK(hipMalloc(&p, b ? b : 16));
+        bytes = b;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+template <class T>
+void upload(DBuf& d, const T* h, size_t n, hipStream_t s) {
+    d.ensure(n * sizeof(T));
+    if (n) HIPCHK(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct ek_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    // Laplacian rows owned by this context
+    int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
+    int block_nnz = 1024, nrb_spmv = 0;
+    DBuf rb, rowptr, col, val;
+    // Lanczos workspace
+    DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, Qd, scal;
+    // KL state
+    int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
+    DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gain, kl_order0, kl_order1, kl_pos,
+        kl_ckey0, kl_ckey1, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
+    bool kl_graph_ready = false, kl_part_ready = false;
+};
+
+namespace {
+
+void set_device(ek_ctx* c) { HIPCHK(hipSetDevice(c->device)); }
+
+ek_ctx* check_ctx(ek_ctx* c) {
+    if (!c) ek::fail(EK_EINVAL, "null ek_ctx");
+    set_device(c);
+    return c;
+}
+
+// In-place sum all-reduce of `count` doubles on the context stream.
+void allreduce(ek_ctx* c, double* p, size_t count) {
+    if (c->nranks > 1 && count) NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, c->comm, c->stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int ek_device_count(int* count) {
+    EK_TRY
+    int c = 0;
+    const hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    if (count) *count = c;
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_init(int device, ek_ctx** out) {
+    EK_TRY
+    if (!out) ek::fail(EK_EINVAL, "ek_init: null out");
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) ek::fail(EK_EHIP, "no HIP device available (no CPU fallback)");
+    if (device < 0 || device >= cnt) ek::fail(EK_EINVAL, "device %d out of range [0,%d)", device, cnt);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        ek::fail(EK_EHIP, "device %d is %s; this build targets gfx950 (MI355X)", device, prop.gcnArchName);
+    auto c = std::make_unique<ek_ctx>();
+    c->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+void ek_destroy(ek_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int ek_get_stream(ek_ctx* c, void** s) {
+    EK_TRY
+    check_ctx(c);
+    if (s) *s = c->stream;
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_comm_unique_id(void* id128) {
+    EK_TRY
+    if (!id128) ek::fail(EK_EINVAL, "null id buffer");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memcpy(id128, &id, sizeof id);
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_comm_init(ek_ctx* c, int nranks, int rank, const void* id128) {
+    EK_TRY
+    check_ctx(c);
+    if (nranks < 1 || rank < 0 || rank >= nranks || !id128) ek::fail(EK_EINVAL, "ek_comm_init: bad argument");
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    if (nranks > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, id128, sizeof id);
+        NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
+    }
+    return EK_OK;
+    EK_CATCH
+}
+
+// ---------------------------------------------------------------------------
+// SpMV seam (SparseSymMatProd::perform_op, cEIG.cpp:194)
+int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr, const int32_t* col,
+                  const double* val) {
+    EK_TRY
+    check_ctx(c);
+    if (n <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > n || !rowptr || (nrows && (!col || !val)))
+        ek::fail(EK_EINVAL, "ek_spmv_setup: bad argument");
+    if (rowptr[0] != 0) ek::fail(EK_EINVAL, "ek_spmv_setup: rowptr[0] must be 0 (local rows)");
+    const int64_t nnz = rowptr[nrows];
+    for (int64_t r = 0; r < nrows; ++r)
+        if (rowptr[r + 1] < rowptr[r]) ek::fail(EK_EINVAL, "ek_spmv_setup: rowptr not monotone");
+    for (int64_t p = 0; p < nnz; ++p)
+        if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup: column %d out of range", col[p]);
+    int64_t row0_expect = 0, nrows_expect = 0, nloc = 0;
+    ek_shard_rows(n, c->nranks, c->rank, &row0_expect, &nrows_expect, &nloc);
+    if (c->nranks > 1 && (row0 != row0_expect || nrows != nrows_expect))
+        ek::fail(EK_EINVAL, "ek_spmv_setup: rank %d must own rows [%lld,+%lld) (ek_shard_rows)", c->rank,
+                 (long long)row0_expect, (long long)nrows_expect);
+    c->n = n;
+    c->row0 = row0;
+    c->nrows = nrows;
+    c->nloc = c->nranks > 1 ? nloc : n;
+    c->nnz = nnz;
+    c->block_nnz = nnz < 512ll * 1024 ? 512 : 1024;
+    const auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
+    c->nrb_spmv = int(rbv.size()) - 1;
+    upload(c->rb, rbv.data(), rbv.size(), c->stream);
+    upload(c->rowptr, rowptr, size_t(nrows) + 1, c->stream);
+    upload(c->col, col, size_t(nnz), c->stream);
+    upload(c->val, val, size_t(nnz), c->stream);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_spmv before ek_spmv_setup");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                  c->val.as<double>(), x, y, nullptr, nullptr, nullptr, c->block_nnz);
+    HIPCHK(hipGetLastError());
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_host before ek_spmv_setup");
+    DBuf dx, dy;
+    upload(dx, x, size_t(c->n), c->stream);
+    dy.ensure(size_t(std::max<int64_t>(c->nrows, 1)) * 8);
+    ek::dev::spmv(c->stream, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                  c->val.as<double>(), dx.as<double>(), dy.as<double>(), nullptr, nullptr, nullptr, c->block_nnz);
+    HIPCHK(hipGetLastError());
+    if (c->nrows) HIPCHK(hipMemcpyAsync(y, dy.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return EK_OK;
+    EK_CATCH
+}
+
+int64_t ek_spmv_bytes(ek_ctx* c) {
+    if (!c) return 0;
+    return 12 * c->nnz + 4 * (c->nrows + 1) + 8 * c->n + 8 * c->nrows;
+}
+
+// ---------------------------------------------------------------------------
+// Lanczos (Spectra SymEigsSolver restated, cEIG.cpp:194-207)
+void ek_lanczos_default_opts(ek_lanczos_opts* o) {
+    if (!o) return;
+    o->ncv = 0;
+    o->maxit = 1000;
+    o->tol = 1e-10;
+    o->deflate = 1;
+    o->time_spmv = 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Spectra SymEigsBase::nev_adjusted
+int nev_adjusted(int nev, int ncv, int nconv, const std::vector<double>& est) {
+    const double eps = std::numeric_limits<double>::epsilon();
+    int nev_new = nev;
+    for (int i = nev; i < ncv; ++i)
+        if (std::fabs(est[size_t(i)]) < eps) ++nev_new;
+    nev_new += std::min(nconv, (ncv - nev_new) / 2);
+    if (nev_new == 1 && ncv >= 6) nev_new = ncv / 2;
+    else if (nev_new == 1 && ncv > 2) nev_new = 2;
+    if (nev_new > ncv - 1) nev_new = ncv - 1;
+    return nev_new;
+}
+
+struct Lanczos {
+    ek_ctx* c;
+    hipStream_t s;
+    int m, ldv, nrb, nub, has_u0, nreal;
+    double u0val;
+    bool time_spmv;
+    std::vector<hipEvent_t> ev;
+    double spmv_ms = 0.0;
+    int spmv_timed = 0, matvecs = 0;
+
+    double* V() { return c->V.as<double>(); }
+    double* col(int j) { return V() + size_t(j) * ldv; }
+
+    // x for the matvec: the full vector (gathered when sharded)
+    const double* gather_f() {
+        if (c->nranks == 1) return c->f.as<double>();
+        NCCLCHK(ncclAllGather(c->f.as<double>(), c->xfull.as<double>(), size_t(c->nloc), ncclDouble, c->comm, s));
+        return c->xfull.as<double>();
+    }
+
+    void reduce_scalar(double* dst) {  // dst = allreduce(sum npart[0:nub])
+        ek::dev::finalize_step(s, c->npart.as<double>(), nub, dst, nullptr, nullptr, -1, nullptr, nullptr);
+        allreduce(c, dst, 1);
+    }
+
+    // Lanczos steps i = k .. m-1 (Spectra Lanczos::factorize_from): CGS2
+    // against the basis (+ the deflated constant vector).
+    void factorize(int k) {
+        double* fn2 = c->fn2.as<double>();
+        for (int i = k; i < m; ++i) {
+            const double* x = gather_f();
+            const bool timed = time_spmv && size_t(2 * (i - k) + 1) < ev.size();
+            if (timed) HIPCHK(hipEventRecord(ev[size_t(2 * (i - k))], s));
+            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                          c->val.as<double>(), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i), c->block_nnz);
+            if (timed) HIPCHK(hipEventRecord(ev[size_t(2 * (i - k) + 1)], s));
+            ++matvecs;
+            const int nc = i + 1, tot = nc + has_u0;
+            ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), c->part.as<double>());
+            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot, c->h1.as<double>());
+            allreduce(c, c->h1.as<double>(), size_t(tot));
+            ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h1.as<double>(), c->w.as<double>(),
+                            c->f.as<double>(), nullptr);
+            ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
+            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot, c->h2.as<double>());
+            allreduce(c, c->h2.as<double>(), size_t(tot));
+            ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
+                            c->f.as<double>(), c->npart.as<double>());
+            ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + i + 1, c->h1.as<double>(),
+                                   c->h2.as<double>(), i, c->alpha.as<double>(), c->offd.as<double>());
+            allreduce(c, fn2 + i + 1, 1);
+        }
+        HIPCHK(hipGetLastError());
+    }
+
+    void collect_spmv_times(int k) {
+        if (!time_spmv) return;
+        HIPCHK(hipStreamSynchronize(s));
+        for (int i = k; i < m && size_t(2 * (i - k) + 1) < ev.size(); ++i) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, ev[size_t(2 * (i - k))], ev[size_t(2 * (i - k) + 1)]));
+            spmv_ms += ms;
+            ++spmv_timed;
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double* lambda_out, double* v_out,
+                                  ek_lanczos_stats* stats) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_lanczos_fiedler before ek_spmv_setup");
+    ek_lanczos_opts o;
+    ek_lanczos_default_opts(&o);
+    if (opts) o = *opts;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t n = c->n;
+    const bool deflate = o.deflate != 0;
+    const int nev = deflate ? 1 : 2;
+    int m = o.ncv > 0 ? o.ncv : int(std::min<int64_t>(100, n / 2));  // cEIG.cpp:195
+    m = int(std::min<int64_t>(m, n - (deflate ? 1 : 0)));
+    if (m > ek::dev::MAX_NCV) ek::fail(EK_EINVAL, "ncv %d exceeds %d", m, ek::dev::MAX_NCV);
+    if (m <= nev) ek::fail(EK_EINVAL, "graph too small for ncv=%d (n=%lld)", m, (long long)n);
+    const double tol = o.tol > 0 ? o.tol : 1e-10;
+    const int maxit = o.maxit > 0 ? o.maxit : 1000;
+    const double eps23 = std::pow(std::numeric_limits<double>::epsilon(), 2.0 / 3.0);
+    const bool trace = std::getenv("EK_LANCZOS_TRACE") != nullptr;
+
+    Lanczos L{};
+    L.c = c;
+    L.s = c->stream;
+    L.m = m;
+    L.ldv = int(round_up(std::max<int64_t>(c->nloc, 1), ek::dev::GT_ROWS));
+    L.nrb = L.ldv / ek::dev::GT_ROWS;
+    L.nub = L.ldv / ek::dev::UPD_ROWS;
+    L.has_u0 = deflate ? 1 : 0;
+    L.nreal = int(c->nrows);
+    L.u0val = 1.0 / std::sqrt(double(n));
+    L.time_spmv = o.time_spmv != 0;
+    hipStream_t s = c->stream;
+
+    const size_t ldv = size_t(L.ldv);
+    c->V.ensure(ldv * size_t(m + 1) * 8);
+    c->Vn.ensure(ldv * size_t(m + 1) * 8);
+    c->f.ensure(ldv * 8);
+    c->w.ensure(ldv * 8);
+    if (c->nranks > 1) c->xfull.ensure(size_t(c->nloc) * size_t(c->nranks) * 8);
+    c->part.ensure(size_t(m + 2) * size_t(L.nrb) * 8);
+    c->h1.ensure(size_t(m + 2) * 8);
+    c->h2.ensure(size_t(m + 2) * 8);
+    c->alpha.ensure(size_t(m + 1) * 8);
+    c->offd.ensure(size_t(m + 1) * 8);
+    c->fn2.ensure(size_t(m + 2) * 8);
+    c->npart.ensure(size_t(L.nub) * 8);
+    c->Qd.ensure(size_t(m) * size_t(m + 1) * 8);
+    c->scal.ensure(64);
+    HIPCHK(hipMemsetAsync(c->V.p, 0, c->V.bytes, s));  // padded rows must stay exactly 0
+    HIPCHK(hipMemsetAsync(c->Vn.p, 0, c->Vn.bytes, s));
+    HIPCHK(hipMemsetAsync(c->w.p, 0, c->w.bytes, s));
+    if (c->nranks > 1) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
+    if (L.time_spmv) {
+        L.ev.resize(size_t(2 * m));
+        for (auto& e : L.ev) HIPCHK(hipEventCreate(&e));
+    }
+    struct EvGuard {
+        std::vector<hipEvent_t>& ev;
+        ~EvGuard() {
+            for (auto e : ev) (void)hipEventDestroy(e);
+        }
+    } evguard{L.ev};
+
+    // start vector: Park-Miller LCG over GLOBAL indices (identical on every
+    // rank), values in [-0.5, 0.5) like Spectra's SimpleRandom; deflated.
+    {
+        std::vector<double> h(ldv, 0.0);
+        uint64_t st = 1;
+        for (int64_t g = 0; g < c->row0 + c->nrows; ++g) {
+            st = (st * 16807ull) % 2147483647ull;
+            if (g >= c->row0) h[size_t(g - c->row0)] = double(st) / 2147483647.0 - 0.5;
+        }
+        HIPCHK(hipMemcpyAsync(c->f.p, h.data(), ldv * 8, hipMemcpyHostToDevice, s));
+        double* sc = c->scal.as<double>();
+        if (deflate) {
+            ek::dev::sum_partial(s, L.ldv, c->f.as<double>(), L.nreal, c->npart.as<double>(), 0);
+            L.reduce_scalar(sc);
+            ek::dev::scale_sub_mean(s, L.ldv, c->f.as<double>(), L.nreal, sc, 1.0 / double(n));
+        }
+        ek::dev::sum_partial(s, L.ldv, c->f.as<double>(), L.nreal, c->npart.as<double>(), 1);
+        L.reduce_scalar(c->fn2.as<double>());
+    }
+
+    std::vector<double> d(size_t(m), 0.0), e(size_t(m), 0.0), theta(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
+    std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
+    int k = 0, restarts = 0, nconv = 0;
+    bool converged = false;
+    for (;;) {
+        L.factorize(k);
+        L.collect_spmv_times(k);
+        HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(offd_h.data(), c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(fn2_h.data(), c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int i = k; i < m; ++i) {
+            d[size_t(i)] = alpha_h[size_t(i)];
+            if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
+        }
+        if (!ek::tridiag_eig(m, d.data(), e.data(), theta.data(), zl.data(), nullptr))
+            ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
+        const double fnorm = std::sqrt(std::max(0.0, fn2_h[size_t(m)]));
+        if (!std::isfinite(fnorm)) ek::fail(EK_ENOCONV, "Lanczos breakdown (non-finite residual)");
+        nconv = 0;
+        for (int i = 0; i < nev; ++i) {  // Spectra num_converged
+            const double thresh = tol * std::max(eps23, std::fabs(theta[size_t(i)]));
+            if (std::fabs(zl[size_t(i)]) * fnorm < thresh) ++nconv;
+        }
+        if (trace)
+            std::fprintf(stderr, "[lanczos] restart %d k=%d theta0=%.15g est0=%.3e theta1=%.15g fnorm=%.3e\n", restarts,
+                         k, theta[0], std::fabs(zl[0]) * fnorm, theta[1], fnorm);
+        if (nconv >= nev) {
+            converged = true;
+            break;
+        }
+        if (++restarts >= maxit) break;
+        // implicit restart with the m-knew unwanted Ritz values as shifts
+        const int knew = nev_adjusted(nev, m, nconv, zl);
+        std::vector<double> Q(size_t(m) * m, 0.0), dd(d), ee(e);
+        for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
+        for (int i = knew; i < m; ++i) ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q.data());
+        const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
+        const double hk = ee[size_t(knew - 1)];                         // H(knew, knew-1)
+        HIPCHK(hipMemcpyAsync(c->Qd.p, Q.data(), size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
+        ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>());
+        ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
+                            c->npart.as<double>());
+        L.reduce_scalar(c->fn2.as<double>() + knew);
+        std::swap(c->V.p, c->Vn.p);
+        std::swap(c->V.bytes, c->Vn.bytes);
+        HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart
+        for (int i = 0; i < knew; ++i) d[size_t(i)] = dd[size_t(i)];
+        for (int i = 0; i + 1 < knew; ++i) e[size_t(i)] = ee[size_t(i)];
+        k = knew;
+    }
+    if (!converged)
+        ek::fail(EK_ENOCONV, "Eigenvalue computation failed: %d of %d Ritz pairs converged after %d restarts", nconv,
+                 nev, restarts);
+    // Ritz vector of the wanted value (ascending: [0] is the null pair unless deflated)
+    const int want = deflate ? 0 : 1;
+    std::vector<double> Z(size_t(m) * m);
+    ek::tridiag_eig(m, d.data(), e.data(), theta.data(), zl.data(), Z.data());
+    const double lambda = theta[size_t(want)];
+    HIPCHK(hipMemcpyAsync(c->Qd.p, Z.data() + size_t(want) * m, size_t(m) * 8, hipMemcpyHostToDevice, s));
+    double* xloc = c->Vn.as<double>();
+    ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), 1, xloc);
+    // full vector on every rank
+    std::vector<double> v(static_cast<size_t>(n));
+    double* xg = xloc;
+    if (c->nranks > 1) {
+        NCCLCHK(ncclAllGather(xloc, c->xfull.as<double>(), size_t(c->nloc), ncclDouble, c->comm, s));
+        xg = c->xfull.as<double>();
+    }
+    HIPCHK(hipMemcpyAsync(v.data(), xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
+    // residual ||L x - lambda x|| on the owned rows
+    ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                  c->val.as<double>(), xg, c->w.as<double>(), nullptr, nullptr, nullptr, c->block_nnz);
+    std::vector<double> y(size_t(std::max<int64_t>(c->nrows, 1)));
+    if (c->nrows) HIPCHK(hipMemcpyAsync(y.data(), c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    double r2 = 0.0, nx2 = 0.0;
+    for (int64_t i = 0; i < n; ++i) nx2 += v[size_t(i)] * v[size_t(i)];
+    const double inv = 1.0 / std::sqrt(nx2);
+    for (int64_t i = 0; i < c->nrows; ++i) {
+        const double t = (y[size_t(i)] - lambda * v[size_t(c->row0 + i)]) * inv;
+        r2 += t * t;
+    }
+    if (c->nranks > 1) {
+        double* sc = c->scal.as<double>();
+        HIPCHK(hipMemcpyAsync(sc, &r2, 8, hipMemcpyHostToDevice, s));
+        allreduce(c, sc, 1);
+        HIPCHK(hipMemcpyAsync(&r2, sc, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    // deterministic sign: the entry of largest magnitude (first on ties) is positive
+    size_t imax = 0;
+    for (size_t i = 1; i < v.size(); ++i)
+        if (std::fabs(v[i]) > std::fabs(v[imax])) imax = i;
+    const double sgn = v[imax] < 0 ? -inv : inv;
+    for (double& t : v) t *= sgn;
+    if (lambda_out) *lambda_out = lambda;
+    if (v_out) std::copy(v.begin(), v.end(), v_out);
+    if (stats) {
+        stats->restarts = restarts;
+        stats->matvecs = L.matvecs;
+        stats->converged = 1;
+        stats->residual = std::sqrt(r2);
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->spmv_ms = L.spmv_ms;
+        stats->spmv_timed = L.spmv_timed;
+        stats->comm_ms = 0.0;
+    }
+    return EK_OK;
+    EK_CATCH
+}
+
+// ---------------------------------------------------------------------------
+// KL driver (KL(), cKL.cpp:288-406)
+extern "C" {
+
+int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t* col, const float* w) {
+    EK_TRY
+    check_ctx(c);
+    if (n <= 0 || n > INT32_MAX || !rowptr || !col || !w) ek::fail(EK_EINVAL, "ek_kl_graph_setup: bad argument");
+    const int64_t nnz = rowptr[n];
+    for (int64_t r = 0; r < n; ++r)
+        if (rowptr[r + 1] < rowptr[r]) ek::fail(EK_EINVAL, "ek_kl_graph_setup: rowptr not monotone");
+    for (int64_t p = 0; p < nnz; ++p)
+        if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_kl_graph_setup: column out of range");
+    hipStream_t s = c->stream;
+    c->kl_n = n;
+    upload(c->kl_rowptr, rowptr, size_t(n) + 1, s);
+    upload(c->kl_col, col, size_t(nnz), s);
+    upload(c->kl_w, w, size_t(nnz), s);
+    c->kl_side.ensure(size_t(n));
+    c->kl_side_init.ensure(size_t(n));
+    c->kl_locked.ensure(size_t(n));
+    c->kl_gain.ensure(size_t(n) * 4);
+    c->kl_pos.ensure(size_t(n) * 4);
+    c->kl_sides_tmp.ensure(size_t(n));
+    c->kl_cutpart.ensure(size_t((n + 255) / 256) * 8);
+    c->kl_cut0.ensure(16);
+    c->kl_out.ensure(sizeof(ek::dev::KLOut));
+    c->kl_count.ensure(64);
+    HIPCHK(hipStreamSynchronize(s));
+    c->kl_graph_ready = true;
+    c->kl_part_ready = false;
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_kl_nets_setup(ek_ctx* c, int64_t nets, const int64_t* net_ptr, const int32_t* pins) {
+    EK_TRY
+    check_ctx(c);
+    if (nets < 0 || !net_ptr || (net_ptr[nets] > 0 && !pins)) ek::fail(EK_EINVAL, "ek_kl_nets_setup: bad argument");
+    c->kl_nets = nets;
+    upload(c->kl_netptr, net_ptr, size_t(nets) + 1, c->stream);
+    upload(c->kl_pins, pins, size_t(net_ptr[nets]), c->stream);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int32_t* order1, int64_t n1) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->kl_graph_ready) ek::fail(EK_ESTATE, "ek_kl_set_partition before ek_kl_graph_setup");
+    const int64_t n = c->kl_n;
+    if (n0 < 0 || n1 < 0 || n0 + n1 != n || (n0 && !order0) || (n1 && !order1))
+        ek::fail(EK_EINVAL, "ek_kl_set_partition: the two lists must cover all %lld nodes", (long long)n);
+    std::vector<uint8_t> side(size_t(n), 2);
+    std::vector<int32_t> pos(size_t(n), -1);
+    for (int64_t i = 0; i < n0; ++i) {
+        const int32_t u = order0[i];
+        if (u < 0 || u >= n || side[size_t(u)] != 2) ek::fail(EK_EINVAL, "ek_kl_set_partition: bad/duplicate node %d", u);
+        side[size_t(u)] = 0;
+        pos[size_t(u)] = int32_t(i);
+    }
+    for (int64_t i = 0; i < n1; ++i) {
+        const int32_t u = order1[i];
+        if (u < 0 || u >= n || side[size_t(u)] != 2) ek::fail(EK_EINVAL, "ek_kl_set_partition: bad/duplicate node %d", u);
+        side[size_t(u)] = 1;
+        pos[size_t(u)] = int32_t(i);
+    }
+    hipStream_t s = c->stream;
+    c->kl_n0 = n0;
+    c->kl_n1 = n1;
+    upload(c->kl_order0, order0, size_t(n0), s);
+    upload(c->kl_order1, order1, size_t(n1), s);
+    upload(c->kl_side_init, side.data(), size_t(n), s);
+    upload(c->kl_pos, pos.data(), size_t(n), s);
+    c->kl_ckey0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
+    c->kl_ckey1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
+    c->kl_log.ensure(size_t(std::max<int64_t>(1, std::min(n0, n1))) * sizeof(ek_swap));
+    HIPCHK(hipStreamSynchronize(s));
+    c->kl_part_ready = true;
+    return EK_OK;
+    EK_CATCH
+}
+
+}  // extern "C"
+
+namespace {
+
+ek::dev::KLDev kl_dev(ek_ctx* c) {
+    ek::dev::KLDev d;
+    d.n = int(c->kl_n);
+    d.rowptr = c->kl_rowptr.as<int32_t>();
+    d.col = c->kl_col.as<int32_t>();
+    d.w = c->kl_w.as<float>();
+    d.side = c->kl_side.as<uint8_t>();
+    d.side_init = c->kl_side_init.as<uint8_t>();
+    d.locked = c->kl_locked.as<uint8_t>();
+    d.gain = c->kl_gain.as<float>();
+    d.order0 = c->kl_order0.as<int32_t>();
+    d.order1 = c->kl_order1.as<int32_t>();
+    d.pos = c->kl_pos.as<int32_t>();
+    d.n0 = int(c->kl_n0);
+    d.n1 = int(c->kl_n1);
+    d.nck0 = int((c->kl_n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK);
+    d.nck1 = int((c->kl_n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK);
+    d.ckey0 = c->kl_ckey0.as<unsigned long long>();
+    d.ckey1 = c->kl_ckey1.as<unsigned long long>();
+    d.cut_part = c->kl_cutpart.as<double>();
+    d.cut0 = c->kl_cut0.as<float>();
+    return d;
+}
+
+int64_t net_cut_of(ek_ctx* c, const uint8_t* side_dev, unsigned long long* cnt_dev, hipStream_t s) {
+    if (!c->kl_nets) return -1;
+    HIPCHK(hipMemsetAsync(cnt_dev, 0, 8, s));
+    ek::dev::net_cut(s, c->kl_nets, c->kl_netptr.as<int64_t>(), c->kl_pins.as<int32_t>(), side_dev, cnt_dev);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap, ek_kl_result* res) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->kl_graph_ready || !c->kl_part_ready) ek::fail(EK_ESTATE, "ek_kl_run before graph/partition setup");
+    hipStream_t s = c->stream;
+    const int64_t n = c->kl_n;
+    const int lim = limit >= 0 ? limit : int(std::log2(double(n))) + 5;  // cKL.cpp:303
+    const auto d = kl_dev(c);
+    hipEvent_t e0, e1, e2;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventCreate(&e2));
+    struct G {
+        hipEvent_t a, b, c;
+        ~G() {
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+            (void)hipEventDestroy(c);
+        }
+    } guard{e0, e1, e2};
+    const long long dcap = std::max<int64_t>(1, std::min(c->kl_n0, c->kl_n1));
+    auto* out = c->kl_out.as<ek::dev::KLOut>();
+    HIPCHK(hipEventRecord(e0, s));
+    HIPCHK(hipMemcpyAsync(c->kl_side.p, c->kl_side_init.p, size_t(n), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(c->kl_locked.p, 0, size_t(n), s));
+    ek::dev::kl_prepare(s, d);
+    HIPCHK(hipEventRecord(e1, s));
+    ek::dev::kl_loop(s, d, lim, c->kl_log.as<ek_swap>(), dcap, out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e2, s));
+    // integer net cuts: initial, best prefix, final
+    auto* cnt = c->kl_count.as<unsigned long long>();
+    const bool nets = c->kl_nets > 0;
+    if (nets) {
+        net_cut_of(c, c->kl_side_init.as<uint8_t>(), cnt + 0, s);
+        net_cut_of(c, c->kl_side.as<uint8_t>(), cnt + 2, s);
+        ek::dev::kl_replay(s, int(n), c->kl_side_init.as<uint8_t>(), c->kl_log.as<ek_swap>(), &out->best_iter, dcap,
+                           c->kl_sides_tmp.as<uint8_t>());
+        net_cut_of(c, c->kl_sides_tmp.as<uint8_t>(), cnt + 1, s);
+    }
+    ek::dev::KLOut ho{};
+    unsigned long long hc[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(&ho, out, sizeof ho, hipMemcpyDeviceToHost, s));
+    if (nets) HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (log_out && cap > 0) {
+        const int64_t k = std::min<int64_t>(cap, ho.iterations);
+        if (k) HIPCHK(hipMemcpy(log_out, c->kl_log.p, size_t(k) * sizeof(ek_swap), hipMemcpyDeviceToHost));
+    }
+    if (res) {
+        float loop_ms = 0.f, prep_ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&prep_ms, e0, e1));
+        HIPCHK(hipEventElapsedTime(&loop_ms, e1, e2));
+        res->iterations = ho.iterations;
+        res->initial_cut = ho.initial_cut;
+        res->best_cut = ho.best_cut;
+        res->final_cut = ho.final_cut;
+        res->best_iter = ho.best_iter;
+        res->net_cut_initial = nets ? int64_t(hc[0]) : -1;
+        res->net_cut_best = nets ? int64_t(hc[1]) : -1;
+        res->net_cut_final = nets ? int64_t(hc[2]) : -1;
+        res->loop_ms = loop_ms;
+        res->total_ms = double(loop_ms) + double(prep_ms);
+    }
+    return EK_OK;
+    EK_CATCH
+}
+
+extern "C" int ek_kl_sides(ek_ctx* c, int32_t which, uint8_t* sides_out) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->kl_part_ready || !sides_out) ek::fail(EK_ESTATE, "ek_kl_sides: nothing to report");
+    hipStream_t s = c->stream;
+    const int64_t n = c->kl_n;
+    const uint8_t* src = c->kl_side_init.as<uint8_t>();
+    if (which == 2) src = c->kl_side.as<uint8_t>();
+    if (which == 1) {
+        const long long dcap = std::max<int64_t>(1, std::min(c->kl_n0, c->kl_n1));
+        ek::dev::kl_replay(s, int(n), c->kl_side_init.as<uint8_t>(), c->kl_log.as<ek_swap>(),
+                           &c->kl_out.as<ek::dev::KLOut>()->best_iter, dcap, c->kl_sides_tmp.as<uint8_t>());
+        src = c->kl_sides_tmp.as<uint8_t>();
+    }
+    HIPCHK(hipMemcpyAsync(sides_out, src, size_t(n), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return EK_OK;
+    EK_CATCH
+}

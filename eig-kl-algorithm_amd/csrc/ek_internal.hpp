@@ -1,0 +1,165 @@
+// Internal declarations shared by the host (.cpp) and device (.hip) units of
+// libeigkl_hip.so.  Public surface: include/eigkl.h.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/eigkl.h"
+
+// ---------------------------------------------------------------------------
+// error plumbing: every C-ABI entry returns a status and sets a thread-local
+// message; nothing calls exit().
+namespace ek {
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+struct Error {
+    int code;
+};
+[[noreturn]] void fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int guard_exceptions();  // maps the in-flight exception to a status (call from catch(...))
+
+// bounded host parallelism (std::thread); EK_THREADS or OMP_NUM_THREADS caps it
+int host_threads();
+template <class F>
+void parallel_for(int64_t n, F&& fn);  // fn(begin, end)
+}  // namespace ek
+
+#define EK_TRY try {
+#define EK_CATCH \
+    }            \
+    catch (...) { return ek::guard_exceptions(); }
+
+// ---------------------------------------------------------------------------
+// host objects
+struct ek_hgr {
+    int64_t nets = 0, nodes = 0;
+    std::vector<int64_t> net_ptr;  // nets + 1
+    std::vector<int32_t> pins;     // 0-based
+};
+
+struct ek_csr {
+    int64_t nrows = 0;
+    int32_t value_bytes = 8;
+    std::vector<int32_t> rowptr, col, nfwd;
+    std::vector<double> val64;
+    std::vector<float> val32;
+};
+
+namespace ek {
+// graph_build.cpp
+void build_laplacian(const ek_hgr& h, ek_csr& out);
+void build_kl_graph(const ek_hgr& h, ek_csr& out);
+// libstdc++ unordered_map<uint32_t,...> iteration order for keys inserted
+// (first insertion) in the given order; writes the iteration order to out.
+void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch);
+uint64_t hashtable_next_buckets(uint64_t cur);  // bucket count after the rehash that follows `cur`
+
+// host_linalg.cpp — small dense/tridiagonal kernels for the IRL driver
+// eigenvalues (ascending) of the symmetric tridiagonal (d, e), e[i] = T(i+1,i);
+// zlast[j] = last component of eigenvector j; full Z (m x m col-major) if Z != null.
+bool tridiag_eig(int m, const double* d, const double* e, double* evals, double* zlast, double* Z);
+// one implicit symmetric QR step with shift mu on (d, e); accumulates Q (m x m col-major) <- Q G
+void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q);
+}  // namespace ek
+
+// ---------------------------------------------------------------------------
+// device-side launchers (kernels_*.hip).  All asynchronous on `stream`.
+typedef struct ihipStream_t* hipStream_t;
+
+namespace ek {
+namespace dev {
+
+// kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
+constexpr int SPMV_THREADS = 256;
+std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int block_nnz);
+// y[r] = scale * sum_c L[r,c] x[c]; scale = 1/sqrt(*fn2) when fn2 != null else 1.
+// If vcol != null also writes vcol[r] = f[r] * scale (Lanczos basis column).
+void spmv(hipStream_t s, int nblocks, const int32_t* rb, const int32_t* rowptr, const int32_t* col,
+          const double* val, const double* x, double* y, const double* fn2, const double* f, double* vcol,
+          int block_nnz);
+
+// kernels_lanczos.hip
+constexpr int GT_ROWS = 1024;  // rows per gemv-T block; ldv is a multiple of this
+constexpr int GT_COLS = 8;     // basis columns per gemv-T block
+constexpr int UPD_ROWS = 512;  // rows per update block
+constexpr int MAX_NCV = 128;
+// part[j*nrb + b] = sum_{rows of block b} V[row, j] * w[row]; column `ncols` is
+// the implicit deflation vector u0 (value u0val on rows < nreal) if has_u0.
+void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val,
+           int nreal, const double* w, double* part);
+// h[j] = sum_b part[j*nrb + b]  for j < ncols_total
+void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
+// dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
+void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
+            const double* h, const double* src, double* dst, double* npart);
+// fn2_out[0] = sum(npart[0:nb]); if step >= 0: alpha[step] = h1[step]+h2[step],
+// offd[step] = h1[step-1]+h2[step-1]
+void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1,
+                   const double* h2, int step, double* alpha, double* offd);
+// out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device)
+void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out);
+// f = f*sigma + x*hk ; per-block sum of f^2 -> npart
+void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart);
+// x = x / sqrt(*n2) ... and deflate helpers
+void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* mean_sum, double inv_n);
+void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares);
+
+// kernels_kl.hip
+constexpr int KL_LOOP_THREADS = 1024;
+constexpr int KL_CHUNK = 256;
+struct KLDev {
+    int n = 0;
+    const int32_t* rowptr = nullptr;
+    const int32_t* col = nullptr;
+    const float* w = nullptr;
+    uint8_t* side = nullptr;        // current split (0/1)
+    const uint8_t* side_init = nullptr;
+    uint8_t* locked = nullptr;      // erased from remain[]
+    float* gain = nullptr;
+    const int32_t* order0 = nullptr;  // remain[0] positions -> node
+    const int32_t* order1 = nullptr;
+    const int32_t* pos = nullptr;     // node -> position in its list
+    int n0 = 0, n1 = 0, nck0 = 0, nck1 = 0;
+    unsigned long long* ckey0 = nullptr;  // per-chunk best (gain, first position) keys
+    unsigned long long* ckey1 = nullptr;
+    double* cut_part = nullptr;
+    float* cut0 = nullptr;
+};
+struct KLOut {
+    long long iterations;
+    long long best_iter;
+    float initial_cut, best_cut, final_cut;
+    unsigned int status;
+};
+void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk keys
+void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out);
+// sides_out = side_init with the first `count` swaps of `log` applied (count on device: *best or *iters)
+void kl_replay(hipStream_t s, int n, const uint8_t* side_init, const ek_swap* log, const long long* count,
+               long long cap, uint8_t* sides_out);
+void net_cut(hipStream_t s, int64_t nets, const int64_t* net_ptr, const int32_t* pins, const uint8_t* side,
+             unsigned long long* count);
+
+}  // namespace dev
+}  // namespace ek
+
+// ---------------------------------------------------------------------------
+// parallel_for implementation
+#include <algorithm>
+#include <thread>
+template <class F>
+void ek::parallel_for(int64_t n, F&& fn) {
+    const int64_t T = std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 4096));
+    if (T <= 1) {
+        fn(int64_t(0), n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t b = n * t / T, e = n * (t + 1) / T;
+        th.emplace_back([&fn, b, e] { fn(b, e); });
+    }
+    for (auto& x : th) x.join();
+}

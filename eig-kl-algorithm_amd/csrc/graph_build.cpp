@@ -1,0 +1,387 @@
+// Clique expansions of the hypergraph (host side):
+//   * fp64 Laplacian, restating initializeMatrix (cEIG.cpp:86-133);
+//   * fp32 KL adjacency in cKL summation order, restating
+//     InitializeSparsMatrix (cKL.cpp:84-149) + the iteration order of its
+//     std::unordered_map<uint32_t,float> rows, emulated
+//     here so the product does not depend on the host's libstdc++.
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <numeric>
+
+#include "ek_internal.hpp"
+
+namespace ek {
+
+// ---------------------------------------------------------------------------
+// libstdc++ (GCC 11) _Hashtable<uint32_t, ...> with _Prime_rehash_policy,
+// max_load_factor 1, std::hash<uint32_t> = identity, bucket = key % B.
+//
+// Bucket counts a default-constructed map passes through; the first insert
+// rehashes to 13 (_M_next_bkt(12) via the small-size table), after that a
+// rehash to the smallest listed prime >= 2B happens when the element count
+// reaches B.  Checked against the live libstdc++ by
+// tests/test_host_logic.py::test_bucket_growth_matches_libstdcxx.
+static const uint64_t kBucketSeq[] = {13,     29,     59,      127,     257,     541,     1109,
+                                      2357,   5087,   10273,   20753,   42043,   85229,   172933,
+                                      351061, 712697, 1447153, 2938679, 5967347, 12117689};
+
+uint64_t hashtable_next_buckets(uint64_t cur) {
+    for (uint64_t b : kBucketSeq)
+        if (b > cur) return b;
+    fail(EK_EINVAL, "hash-order emulation: row exceeds %llu keys", (unsigned long long)cur);
+}
+
+// Emulates insertion of `cnt` distinct keys (first-insertion order) and
+// writes the resulting begin()->end() iteration order.
+//   insert (_M_insert_bucket_begin): non-empty bucket -> after the bucket's
+//     "before" node; empty bucket -> list front, the old front's bucket now
+//     points at the new node, this bucket points at before-begin;
+//   rehash (_M_rehash_aux, unique keys): walk the old list in order; a node
+//     whose new bucket is empty goes to the front (and the previous front's
+//     bucket is re-pointed at it); otherwise after its bucket's before node.
+void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch) {
+    constexpr int32_t NIL = -1, BB = -2, EMPTY = -3;
+    if (cnt == 0) return;
+    scratch.resize(size_t(cnt));
+    int32_t* next = scratch.data();
+    std::vector<int32_t> bucket(1, EMPTY);
+    uint64_t B = 1, next_resize = 0, count = 0;
+    int32_t head = NIL;
+    auto rehash = [&](uint64_t nb) {
+        std::vector<int32_t> nbk(nb, EMPTY);
+        int32_t p = head;
+        head = NIL;
+        uint64_t bbegin = 0;
+        while (p != NIL) {
+            const int32_t nx = next[p];
+            const uint64_t b = keys[p] % nb;
+            if (nbk[b] == EMPTY) {
+                next[p] = head;
+                head = p;
+                nbk[b] = BB;
+                if (next[p] != NIL) nbk[bbegin] = p;
+                bbegin = b;
+            } else if (nbk[b] == BB) {
+                next[p] = head;
+                head = p;
+            } else {
+                next[p] = next[nbk[b]];
+                next[nbk[b]] = p;
+            }
+            p = nx;
+        }
+        bucket.swap(nbk);
+        B = nb;
+    };
+    for (int64_t i = 0; i < cnt; ++i) {
+        // _M_need_rehash(B, count, 1)
+        if (count + 1 > next_resize) {
+            const double min_bkts = double(std::max<uint64_t>(count + 1, next_resize ? 0 : 11));
+            if (min_bkts >= double(B)) {
+                const uint64_t want = std::max<uint64_t>(uint64_t(std::floor(min_bkts)) + 1, B * 2);
+                uint64_t nb = want <= 13 ? 13 : 0;  // _M_next_bkt: small table gives 13 for 12..13
+                if (!nb)
+                    for (uint64_t b : kBucketSeq)
+                        if (b >= want) {
+                            nb = b;
+                            break;
+                        }
+                if (!nb) fail(EK_EINVAL, "hash-order emulation: row too large");
+                rehash(nb);
+                next_resize = nb;
+            } else {
+                next_resize = B;
+            }
+        }
+        const int32_t node = int32_t(i);
+        const uint64_t b = keys[i] % B;
+        if (bucket[b] == EMPTY) {
+            next[node] = head;
+            head = node;
+            if (next[node] != NIL) bucket[keys[next[node]] % B] = node;
+            bucket[b] = BB;
+        } else if (bucket[b] == BB) {
+            next[node] = head;
+            head = node;
+        } else {
+            next[node] = next[bucket[b]];
+            next[bucket[b]] = node;
+        }
+        ++count;
+    }
+    int64_t q = 0;
+    for (int32_t p = head; p != NIL; p = next[p]) out[q++] = keys[p];
+}
+
+// ---------------------------------------------------------------------------
+// cEIG.cpp:86-133.  Pairs (j<k) of every net contribute -2/|e| to (a,b) and
+// (b,a); duplicates are summed (in net order here; setFromTriplets' order is
+// thread-dependent in the reference); then diag = -(sum of row i in ascending
+// column order, including any (i,i) triplets from repeated pins).
+void build_laplacian(const ek_hgr& h, ek_csr& L) {
+    const int64_t n = h.nodes;
+    std::vector<int64_t> cnt(size_t(n) + 1, 0);
+    for (int64_t e = 0; e < h.nets; ++e) {
+        const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
+        if (k < 2) continue;
+        for (int64_t j = 0; j < k; ++j) cnt[size_t(h.pins[size_t(p0 + j)]) + 1] += k - 1;
+    }
+    for (int64_t i = 0; i < n; ++i) cnt[size_t(i) + 1] += cnt[size_t(i)];
+    std::vector<int32_t> tc(size_t(cnt[size_t(n)]));
+    std::vector<double> tv(size_t(cnt[size_t(n)]));
+    {
+        std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
+        for (int64_t e = 0; e < h.nets; ++e) {
+            const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
+            if (k < 2) continue;
+            const double wgt = 2.0 / double(k);
+            for (int64_t j = 0; j + 1 < k; ++j)
+                for (int64_t q = j + 1; q < k; ++q) {
+                    const int32_t a = h.pins[size_t(p0 + j)], b = h.pins[size_t(p0 + q)];
+                    tc[size_t(cur[size_t(a)])] = b;
+                    tv[size_t(cur[size_t(a)]++)] = -wgt;
+                    tc[size_t(cur[size_t(b)])] = a;
+                    tv[size_t(cur[size_t(b)]++)] = -wgt;
+                }
+        }
+    }
+    // per row: stable sort by column, sum duplicates in net order, diagonal
+    std::vector<int32_t> rlen(size_t(n), 0);
+    std::vector<std::vector<std::pair<int32_t, double>>> rows(static_cast<size_t>(n));
+    parallel_for(n, [&](int64_t lo, int64_t hi) {
+        std::vector<int64_t> idx;
+        for (int64_t r = lo; r < hi; ++r) {
+            const int64_t b = cnt[size_t(r)], e = cnt[size_t(r) + 1];
+            idx.resize(size_t(e - b));
+            std::iota(idx.begin(), idx.end(), b);
+            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return tc[size_t(x)] < tc[size_t(y)]; });
+            auto& row = rows[size_t(r)];
+            row.clear();
+            for (int64_t t : idx) {
+                if (!row.empty() && row.back().first == tc[size_t(t)]) row.back().second += tv[size_t(t)];
+                else row.push_back({tc[size_t(t)], tv[size_t(t)]});
+            }
+            double s = 0.0;
+            bool has_diag = false;
+            for (auto& [c, v] : row) {
+                s += v;
+                has_diag |= (c == r);
+            }
+            if (has_diag) {
+                for (auto& [c, v] : row)
+                    if (c == r) v = -s;
+            } else {
+                auto it = std::lower_bound(row.begin(), row.end(), std::make_pair(int32_t(r), -1e300));
+                row.insert(it, {int32_t(r), -s});
+            }
+            rlen[size_t(r)] = int32_t(row.size());
+        }
+    });
+    L.nrows = n;
+    L.value_bytes = 8;
+    L.rowptr.assign(size_t(n) + 1, 0);
+    for (int64_t r = 0; r < n; ++r) {
+        if (int64_t(L.rowptr[size_t(r)]) + rlen[size_t(r)] > INT32_MAX) fail(EK_EINVAL, "Laplacian nnz exceeds int32");
+        L.rowptr[size_t(r) + 1] = L.rowptr[size_t(r)] + rlen[size_t(r)];
+    }
+    L.col.resize(size_t(L.rowptr[size_t(n)]));
+    L.val64.resize(size_t(L.rowptr[size_t(n)]));
+    parallel_for(n, [&](int64_t lo, int64_t hi) {
+        for (int64_t r = lo; r < hi; ++r) {
+            int64_t p = L.rowptr[size_t(r)];
+            for (auto& [c, v] : rows[size_t(r)]) {
+                L.col[size_t(p)] = c;
+                L.val64[size_t(p++)] = v;
+            }
+            std::vector<std::pair<int32_t, double>>().swap(rows[size_t(r)]);
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
+// cKL.cpp:107-131 + connections() order (cKL.cpp:229-248).
+void build_kl_graph(const ek_hgr& h, ek_csr& G) {
+    const int64_t n = h.nodes;
+    // 1. upper-triangle pairs per row (min endpoint), in net order
+    std::vector<int64_t> cnt(size_t(n) + 1, 0);
+    for (int64_t e = 0; e < h.nets; ++e) {
+        const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
+        for (int64_t j = 0; j + 1 < k; ++j)
+            for (int64_t q = j + 1; q < k; ++q) {
+                const int32_t a = h.pins[size_t(p0 + j)], b = h.pins[size_t(p0 + q)];
+                cnt[size_t(std::min(a, b)) + 1]++;
+            }
+    }
+    for (int64_t i = 0; i < n; ++i) cnt[size_t(i) + 1] += cnt[size_t(i)];
+    std::vector<uint32_t> pk(size_t(cnt[size_t(n)]));
+    std::vector<float> pw(size_t(cnt[size_t(n)]));
+    {
+        std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
+        for (int64_t e = 0; e < h.nets; ++e) {
+            const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
+            if (k < 2) continue;
+            const float weight = 1.0f / float(k - 1);  // cKL.cpp:117
+            for (int64_t j = 0; j + 1 < k; ++j)
+                for (int64_t q = j + 1; q < k; ++q) {
+                    int32_t a = h.pins[size_t(p0 + j)], b = h.pins[size_t(p0 + q)];
+                    if (a > b) std::swap(a, b);
+                    pk[size_t(cur[size_t(a)])] = uint32_t(b);
+                    pw[size_t(cur[size_t(a)]++)] = weight;
+                }
+        }
+    }
+    // 2. per row: distinct keys in first-insertion order, fp32 sums in net order
+    //    (adjacencyList[a][b] += w), then the emulated map iteration order.
+    std::vector<int32_t> fcnt(size_t(n), 0);
+    std::vector<std::vector<std::pair<uint32_t, float>>> fwd(static_cast<size_t>(n));
+    std::atomic<bool> too_big{false};
+    parallel_for(n, [&](int64_t lo, int64_t hi) {
+        std::vector<int64_t> idx;
+        std::vector<std::pair<int64_t, std::pair<uint32_t, float>>> first;  // (first seq, (key, sum))
+        std::vector<uint32_t> keys, order;
+        std::vector<int32_t> scratch;
+        for (int64_t r = lo; r < hi; ++r) {
+            const int64_t b = cnt[size_t(r)], e = cnt[size_t(r) + 1];
+            if (b == e) continue;
+            idx.resize(size_t(e - b));
+            std::iota(idx.begin(), idx.end(), b);
+            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return pk[size_t(x)] < pk[size_t(y)]; });
+            first.clear();
+            for (size_t t = 0; t < idx.size();) {
+                const uint32_t key = pk[size_t(idx[t])];
+                float s = 0.0f;  // operator[] value-initialises to 0.0f, then += in net order
+                const int64_t seq0 = idx[t];
+                for (; t < idx.size() && pk[size_t(idx[t])] == key; ++t) s += pw[size_t(idx[t])];
+                first.push_back({seq0, {key, s}});
+            }
+            std::sort(first.begin(), first.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+            keys.resize(first.size());
+            for (size_t t = 0; t < first.size(); ++t) keys[t] = first[t].second.first;
+            order.resize(keys.size());
+            try {
+                hashtable_order(keys.data(), int64_t(keys.size()), order.data(), scratch);
+            } catch (const Error&) {
+                too_big = true;
+                continue;
+            }
+            // map key -> summed weight (keys are distinct): sort a copy by key
+            std::vector<std::pair<uint32_t, float>> bykey(first.size());
+            for (size_t t = 0; t < first.size(); ++t) bykey[t] = first[t].second;
+            std::sort(bykey.begin(), bykey.end());
+            auto& out = fwd[size_t(r)];
+            out.resize(order.size());
+            for (size_t t = 0; t < order.size(); ++t) {
+                auto it = std::lower_bound(bykey.begin(), bykey.end(), std::make_pair(order[t], -INFINITY));
+                out[t] = *it;
+            }
+            fcnt[size_t(r)] = int32_t(out.size());
+        }
+    });
+    if (too_big) fail(EK_EINVAL, "hash-order emulation: a row exceeds the bucket table");
+    std::vector<float>().swap(pw);
+    std::vector<uint32_t>().swap(pk);
+    // 3. backward lists: for rows i ascending, (i, w) appended to key k's list
+    std::vector<int64_t> bcnt(size_t(n) + 1, 0);
+    for (int64_t i = 0; i < n; ++i)
+        for (auto& [k, w] : fwd[size_t(i)])
+            if (int64_t(k) != i) bcnt[size_t(k) + 1]++;
+    for (int64_t i = 0; i < n; ++i) bcnt[size_t(i) + 1] += bcnt[size_t(i)];
+    G.nrows = n;
+    G.value_bytes = 4;
+    G.rowptr.assign(size_t(n) + 1, 0);
+    G.nfwd.assign(fcnt.begin(), fcnt.end());
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t len = int64_t(fcnt[size_t(r)]) + (bcnt[size_t(r) + 1] - bcnt[size_t(r)]);
+        if (int64_t(G.rowptr[size_t(r)]) + len > INT32_MAX) fail(EK_EINVAL, "KL graph nnz exceeds int32");
+        G.rowptr[size_t(r) + 1] = G.rowptr[size_t(r)] + int32_t(len);
+    }
+    G.col.resize(size_t(G.rowptr[size_t(n)]));
+    G.val32.resize(size_t(G.rowptr[size_t(n)]));
+    parallel_for(n, [&](int64_t lo, int64_t hi) {
+        for (int64_t r = lo; r < hi; ++r) {
+            int64_t p = G.rowptr[size_t(r)];
+            for (auto& [k, w] : fwd[size_t(r)]) {
+                G.col[size_t(p)] = int32_t(k);
+                G.val32[size_t(p++)] = w;
+            }
+        }
+    });
+    std::vector<int64_t> bcur(static_cast<size_t>(n));
+    for (int64_t r = 0; r < n; ++r) bcur[size_t(r)] = G.rowptr[size_t(r)] + fcnt[size_t(r)];
+    for (int64_t i = 0; i < n; ++i)
+        for (auto& [k, w] : fwd[size_t(i)])
+            if (int64_t(k) != i) {
+                G.col[size_t(bcur[k])] = int32_t(i);
+                G.val32[size_t(bcur[k]++)] = w;
+            }
+}
+
+}  // namespace ek
+
+extern "C" {
+
+int ek_laplacian_build(const ek_hgr* h, ek_csr** out) {
+    EK_TRY
+    if (!h || !out) ek::fail(EK_EINVAL, "ek_laplacian_build: null argument");
+    auto c = std::make_unique<ek_csr>();
+    ek::build_laplacian(*h, *c);
+    *out = c.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_kl_graph_build(const ek_hgr* h, ek_csr** out) {
+    EK_TRY
+    if (!h || !out) ek::fail(EK_EINVAL, "ek_kl_graph_build: null argument");
+    auto c = std::make_unique<ek_csr>();
+    ek::build_kl_graph(*h, *c);
+    *out = c.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_csr_dims(const ek_csr* c, int64_t* nrows, int64_t* nnz, int32_t* value_bytes) {
+    if (!c) {
+        ek::set_error("ek_csr_dims: null handle");
+        return EK_EINVAL;
+    }
+    if (nrows) *nrows = c->nrows;
+    if (nnz) *nnz = int64_t(c->col.size());
+    if (value_bytes) *value_bytes = c->value_bytes;
+    return EK_OK;
+}
+
+int ek_csr_copy(const ek_csr* c, int32_t* rowptr, int32_t* col, void* val, int32_t* nfwd) {
+    if (!c) {
+        ek::set_error("ek_csr_copy: null handle");
+        return EK_EINVAL;
+    }
+    if (rowptr) std::copy(c->rowptr.begin(), c->rowptr.end(), rowptr);
+    if (col) std::copy(c->col.begin(), c->col.end(), col);
+    if (val) {
+        if (c->value_bytes == 8) std::memcpy(val, c->val64.data(), c->val64.size() * 8);
+        else std::memcpy(val, c->val32.data(), c->val32.size() * 4);
+    }
+    if (nfwd && !c->nfwd.empty()) std::copy(c->nfwd.begin(), c->nfwd.end(), nfwd);
+    return EK_OK;
+}
+
+void ek_csr_free(ek_csr* c) { delete c; }
+
+int ek_shard_rows(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows, int64_t* nloc) {
+    if (n < 0 || nranks < 1 || rank < 0 || rank >= nranks) {
+        ek::set_error("ek_shard_rows: bad argument");
+        return EK_EINVAL;
+    }
+    int64_t blk = (n + nranks - 1) / nranks;
+    blk = (blk + 63) / 64 * 64;  // 512-byte aligned fp64 slices for the all-gather
+    const int64_t r0 = std::min<int64_t>(n, blk * rank);
+    if (row0) *row0 = r0;
+    if (nrows) *nrows = std::min<int64_t>(n, blk * (rank + 1)) - r0;
+    if (nloc) *nloc = blk;
+    return EK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,277 @@
+// .hgr ingest / write / seeded synthetic generator (host side).
+//
+// Reader semantics follow the reference readers (cKL.cpp:92-116,
+// cEIG.cpp:177-182,91-101): the header's first two integers are
+// `nets nodes`; then exactly `nets` lines are consumed, one net per line,
+// pins are 1-based unsigned integers separated by whitespace (a line ends the
+// net; extraction stops at the first non-numeric token, like `ss >> node`).
+// Missing lines give empty nets (getline failure).  Unlike the reference,
+// pin ids outside [1, nodes] are rejected (they are out-of-bounds writes
+// there) and the parse is two-pass and multi-threaded.
+#include <atomic>
+#include <cerrno>
+#include <memory>
+#include <cmath>
+#include <cstring>
+#include <random>
+
+#include "ek_internal.hpp"
+
+namespace {
+
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+
+// Parse unsigned integers on [p, end) (one line); calls emit(value).  Returns
+// false on overflow.  Stops at the first non-numeric token.
+template <class Emit>
+inline bool parse_line(const char* p, const char* end, Emit&& emit) {
+    while (p < end) {
+        while (p < end && is_space(*p)) ++p;
+        if (p >= end) break;
+        if (*p == '+') ++p;
+        if (p >= end || *p < '0' || *p > '9') break;
+        uint64_t v = 0;
+        while (p < end && *p >= '0' && *p <= '9') {
+            v = v * 10 + uint64_t(*p - '0');
+            if (v > 0xffffffffull) return false;
+            ++p;
+        }
+        emit(v);
+        if (p < end && !is_space(*p)) break;  // e.g. "12x": stream stops after 12
+    }
+    return true;
+}
+
+std::string slurp(const char* path) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) ek::fail(EK_EIO, "cannot open %s: %s", path, std::strerror(errno));
+    std::string buf;
+    std::fseek(f, 0, SEEK_END);
+    const long sz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    buf.resize(size_t(sz > 0 ? sz : 0));
+    const size_t got = sz > 0 ? std::fread(&buf[0], 1, size_t(sz), f) : 0;
+    std::fclose(f);
+    buf.resize(got);
+    return buf;
+}
+
+// xoshiro256** seeded by splitmix64: the generator's only RNG (seeded, unlike
+// circuit_generator.py's module-level `random`).
+struct Rng {
+    uint64_t s[4];
+    explicit Rng(uint64_t seed) {
+        for (auto& x : s) {
+            seed += 0x9e3779b97f4a7c15ull;
+            uint64_t z = seed;
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            x = z ^ (z >> 31);
+        }
+    }
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t next() {
+        const uint64_t r = rotl(s[1] * 5, 7) * 9;
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+    double uniform01() { return double(next() >> 11) * 0x1.0p-53; }
+    uint64_t below(uint64_t n) {  // unbiased (Lemire)
+        unsigned __int128 m = (unsigned __int128)next() * n;
+        uint64_t l = uint64_t(m);
+        if (l < n) {
+            const uint64_t t = (0 - n) % n;
+            while (l < t) {
+                m = (unsigned __int128)next() * n;
+                l = uint64_t(m);
+            }
+        }
+        return uint64_t(m >> 64);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int ek_hgr_read(const char* path, ek_hgr** out) {
+    EK_TRY
+    if (!path || !out) ek::fail(EK_EINVAL, "ek_hgr_read: null argument");
+    const std::string buf = slurp(path);
+    const char* b = buf.data();
+    const char* e = b + buf.size();
+    const char* nl = static_cast<const char*>(std::memchr(b, '\n', size_t(e - b)));
+    const char* hend = nl ? nl : e;
+    uint64_t hv[2] = {0, 0};
+    int nh = 0;
+    parse_line(b, hend, [&](uint64_t v) {
+        if (nh < 2) hv[nh] = v;
+        ++nh;
+    });
+    if (nh < 2) ek::fail(EK_EINVAL, "%s: header must be '<nets> <nodes>'", path);
+    auto h = std::make_unique<ek_hgr>();
+    h->nets = int64_t(hv[0]);
+    h->nodes = int64_t(hv[1]);
+    if (h->nodes > INT32_MAX || h->nets > INT32_MAX) ek::fail(EK_EINVAL, "%s: sizes exceed int32", path);
+    // line starts of the next `nets` lines
+    std::vector<const char*> ls(size_t(h->nets) + 1, e);
+    const char* p = nl ? nl + 1 : e;
+    for (int64_t i = 0; i < h->nets; ++i) {
+        ls[size_t(i)] = p;
+        if (p >= e) {  // getline failure: empty net
+            continue;
+        }
+        const char* q = static_cast<const char*>(std::memchr(p, '\n', size_t(e - p)));
+        p = q ? q + 1 : e;
+    }
+    auto line_end = [&](int64_t i) {
+        const char* s = ls[size_t(i)];
+        if (s >= e) return e;
+        const char* q = static_cast<const char*>(std::memchr(s, '\n', size_t(e - s)));
+        return q ? q : e;
+    };
+    std::vector<int64_t> cnt(size_t(h->nets) + 1, 0);
+    std::atomic<bool> bad{false};
+    ek::parallel_for(h->nets, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            int64_t c = 0;
+            if (!parse_line(ls[size_t(i)], line_end(i), [&](uint64_t) { ++c; })) bad = true;
+            cnt[size_t(i) + 1] = c;
+        }
+    });
+    if (bad) ek::fail(EK_EINVAL, "%s: pin id overflows uint32", path);
+    h->net_ptr.assign(size_t(h->nets) + 1, 0);
+    for (int64_t i = 0; i < h->nets; ++i) h->net_ptr[size_t(i) + 1] = h->net_ptr[size_t(i)] + cnt[size_t(i) + 1];
+    h->pins.resize(size_t(h->net_ptr.back()));
+    std::atomic<int64_t> bad_pin{-1};
+    ek::parallel_for(h->nets, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            int64_t q = h->net_ptr[size_t(i)];
+            parse_line(ls[size_t(i)], line_end(i), [&](uint64_t v) {
+                if (v < 1 || int64_t(v) > h->nodes) bad_pin = int64_t(v);
+                h->pins[size_t(q++)] = int32_t(v) - 1;
+            });
+        }
+    });
+    if (bad_pin.load() >= 0)
+        ek::fail(EK_EINVAL, "%s: pin id %lld outside [1, %lld]", path, (long long)bad_pin.load(),
+                 (long long)h->nodes);
+    *out = h.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_hgr_from_pins(int64_t nets, int64_t nodes, const int64_t* net_ptr, const int32_t* pins, ek_hgr** out) {
+    EK_TRY
+    if (!net_ptr || !out || nets < 0 || nodes < 0 || nodes > INT32_MAX) ek::fail(EK_EINVAL, "ek_hgr_from_pins: bad argument");
+    auto h = std::make_unique<ek_hgr>();
+    h->nets = nets;
+    h->nodes = nodes;
+    h->net_ptr.assign(net_ptr, net_ptr + nets + 1);
+    if (h->net_ptr[0] != 0) ek::fail(EK_EINVAL, "net_ptr[0] must be 0");
+    for (int64_t i = 0; i < nets; ++i)
+        if (h->net_ptr[size_t(i) + 1] < h->net_ptr[size_t(i)]) ek::fail(EK_EINVAL, "net_ptr not monotone");
+    h->pins.assign(pins, pins + h->net_ptr.back());
+    for (int32_t v : h->pins)
+        if (v < 0 || v >= nodes) ek::fail(EK_EINVAL, "pin %d outside [0, %lld)", v, (long long)nodes);
+    *out = h.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+// circuit_generator.py:41-59 restated with a seeded RNG: net size from the
+// cumulative table {2:84,3:2,4:6,5:2,6:4,8:2}/100 (r <= cumulative, as
+// _choose_net_size :22-30), then `size` distinct uniform nodes, sorted
+// (_select_nodes_for_net :32-39).
+int ek_hgr_generate(double multiplier, uint64_t seed, ek_hgr** out) {
+    EK_TRY
+    if (!out || !(multiplier > 0)) ek::fail(EK_EINVAL, "ek_hgr_generate: bad argument");
+    auto h = std::make_unique<ek_hgr>();
+    h->nodes = int64_t(std::floor(201920.0 * multiplier));
+    h->nets = int64_t(std::floor(210613.0 * multiplier));
+    if (h->nodes < 2 || h->nodes > INT32_MAX) ek::fail(EK_EINVAL, "ek_hgr_generate: bad size");
+    static const int sizes[6] = {2, 3, 4, 5, 6, 8};
+    static const int cum[6] = {84, 86, 92, 94, 98, 100};
+    Rng rng(seed);
+    h->net_ptr.reserve(size_t(h->nets) + 1);
+    h->pins.reserve(size_t(h->nets) * 3);
+    h->net_ptr.push_back(0);
+    int32_t pick[8];
+    for (int64_t e = 0; e < h->nets; ++e) {
+        const double r = rng.uniform01() * 100.0;
+        int k = 2;
+        for (int t = 0; t < 6; ++t)
+            if (r <= cum[t]) {
+                k = sizes[t];
+                break;
+            }
+        if (k > h->nodes) k = int(h->nodes);
+        for (int j = 0; j < k;) {
+            const int32_t v = int32_t(rng.below(uint64_t(h->nodes)));
+            bool dup = false;
+            for (int q = 0; q < j; ++q) dup |= pick[q] == v;
+            if (!dup) pick[j++] = v;
+        }
+        std::sort(pick, pick + k);
+        h->pins.insert(h->pins.end(), pick, pick + k);
+        h->net_ptr.push_back(int64_t(h->pins.size()));
+    }
+    *out = h.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_hgr_write(const ek_hgr* h, const char* path) {
+    EK_TRY
+    if (!h || !path) ek::fail(EK_EINVAL, "ek_hgr_write: null argument");
+    FILE* f = std::fopen(path, "w");
+    if (!f) ek::fail(EK_EIO, "cannot write %s: %s", path, std::strerror(errno));
+    std::string out;
+    out.reserve(size_t(h->pins.size()) * 8 + 64);
+    out += std::to_string(h->nets) + " " + std::to_string(h->nodes) + "\n";
+    char tmp[16];
+    for (int64_t e = 0; e < h->nets; ++e) {
+        for (int64_t p = h->net_ptr[size_t(e)]; p < h->net_ptr[size_t(e) + 1]; ++p) {
+            if (p != h->net_ptr[size_t(e)]) out += ' ';
+            const int len = snprintf(tmp, sizeof tmp, "%d", h->pins[size_t(p)] + 1);
+            out.append(tmp, size_t(len));
+        }
+        out += '\n';
+    }
+    const size_t wr = std::fwrite(out.data(), 1, out.size(), f);
+    std::fclose(f);
+    if (wr != out.size()) ek::fail(EK_EIO, "short write to %s", path);
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_hgr_dims(const ek_hgr* h, int64_t* nets, int64_t* nodes, int64_t* pins) {
+    if (!h) {
+        ek::set_error("ek_hgr_dims: null handle");
+        return EK_EINVAL;
+    }
+    if (nets) *nets = h->nets;
+    if (nodes) *nodes = h->nodes;
+    if (pins) *pins = int64_t(h->pins.size());
+    return EK_OK;
+}
+
+int ek_hgr_copy_pins(const ek_hgr* h, int64_t* net_ptr, int32_t* pins) {
+    if (!h) {
+        ek::set_error("ek_hgr_copy_pins: null handle");
+        return EK_EINVAL;
+    }
+    if (net_ptr) std::copy(h->net_ptr.begin(), h->net_ptr.end(), net_ptr);
+    if (pins) std::copy(h->pins.begin(), h->pins.end(), pins);
+    return EK_OK;
+}
+
+void ek_hgr_free(ek_hgr* h) { delete h; }
+
+}  // extern "C"

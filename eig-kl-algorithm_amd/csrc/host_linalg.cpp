@@ -1,0 +1,151 @@
+// Small host-side linear algebra for the implicitly restarted Lanczos driver
+// (the m x m projected problem, m = ncv <= 128).  The n-length work runs on
+// the GPU (kernels_lanczos.hip); these routines restate the two small dense
+// steps of Spectra's SymEigsSolver (the solver cEIG.cpp:195-198 calls):
+// TridiagEigen of the projected H and the shifted QR sweeps of its restart.
+#include <cfloat>
+#include <cmath>
+#include <numeric>
+
+#include "ek_internal.hpp"
+
+namespace ek {
+
+// Implicit QL with Wilkinson-type shifts on a symmetric tridiagonal matrix
+// (diagonal d, off-diagonal e[i] = T(i+1, i)).  Eigenvalues ascending in
+// evals; zlast[j] = last component of eigenvector j (the Ritz estimates need
+// only that row); the full eigenvector matrix (col-major) when Z != nullptr.
+bool tridiag_eig(int m, const double* d_in, const double* e_in, double* evals, double* zlast, double* Z) {
+    std::vector<double> d(d_in, d_in + m), e(size_t(m), 0.0), zl(size_t(m), 0.0);
+    for (int i = 0; i + 1 < m; ++i) e[size_t(i)] = e_in[i];
+    zl[size_t(m - 1)] = 1.0;
+    if (Z)
+        for (int j = 0; j < m; ++j)
+            for (int k = 0; k < m; ++k) Z[size_t(j) * m + k] = (j == k) ? 1.0 : 0.0;
+    for (int l = 0; l < m; ++l) {
+        int iter = 0;
+        for (;;) {
+            int mm = l;
+            for (; mm < m - 1; ++mm) {
+                const double dd = std::fabs(d[size_t(mm)]) + std::fabs(d[size_t(mm) + 1]);
+                if (std::fabs(e[size_t(mm)]) <= DBL_EPSILON * dd) break;
+            }
+            if (mm == l) break;
+            if (++iter > 64) return false;
+            double g = (d[size_t(l) + 1] - d[size_t(l)]) / (2.0 * e[size_t(l)]);
+            double r = std::hypot(g, 1.0);
+            g = d[size_t(mm)] - d[size_t(l)] + e[size_t(l)] / (g + std::copysign(r, g));
+            double s = 1.0, c = 1.0, p = 0.0;
+            bool early = false;
+            for (int i = mm - 1; i >= l; --i) {
+                const double f = s * e[size_t(i)], b = c * e[size_t(i)];
+                r = std::hypot(f, g);
+                e[size_t(i) + 1] = r;
+                if (r == 0.0) {  // underflow: split here and restart the sweep
+                    d[size_t(i) + 1] -= p;
+                    e[size_t(mm)] = 0.0;
+                    early = true;
+                    break;
+                }
+                s = f / r;
+                c = g / r;
+                g = d[size_t(i) + 1] - p;
+                r = (d[size_t(i)] - g) * s + 2.0 * c * b;
+                p = s * r;
+                d[size_t(i) + 1] = g + p;
+                g = c * r - b;
+                const double t = zl[size_t(i) + 1];
+                zl[size_t(i) + 1] = s * zl[size_t(i)] + c * t;
+                zl[size_t(i)] = c * zl[size_t(i)] - s * t;
+                if (Z) {
+                    double* zi = Z + size_t(i) * m;
+                    double* zj = Z + size_t(i + 1) * m;
+                    for (int k = 0; k < m; ++k) {
+                        const double tk = zj[k];
+                        zj[k] = s * zi[k] + c * tk;
+                        zi[k] = c * zi[k] - s * tk;
+                    }
+                }
+            }
+            if (early) continue;
+            d[size_t(l)] -= p;
+            e[size_t(l)] = g;
+            e[size_t(mm)] = 0.0;
+        }
+    }
+    std::vector<int> idx(static_cast<size_t>(m));
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return d[size_t(a)] < d[size_t(b)]; });
+    for (int j = 0; j < m; ++j) {
+        evals[j] = d[size_t(idx[size_t(j)])];
+        if (zlast) zlast[j] = zl[size_t(idx[size_t(j)])];
+    }
+    if (Z) {
+        std::vector<double> tmp(Z, Z + size_t(m) * m);
+        for (int j = 0; j < m; ++j)
+            std::copy(tmp.begin() + size_t(idx[size_t(j)]) * m, tmp.begin() + size_t(idx[size_t(j)] + 1) * m,
+                      Z + size_t(j) * m);
+    }
+    return true;
+}
+
+// One implicitly shifted symmetric QR step (bulge chase) with shift mu:
+// T <- G^T T G, Q <- Q G, where G = G_0 ... G_{m-2} is the orthogonal factor
+// of the QR decomposition of T - mu I (implicit-Q theorem).  Equivalent to
+// Spectra's explicit TridiagQR(H - mu I) followed by R Q + mu I.  The
+// implicit-Q theorem needs an unreduced matrix, so negligible off-diagonals
+// (|e_i| <= eps (|d_i| + |d_i+1|), zeroed as TridiagQR does) split T into
+// blocks and the chase restarts at the top of every block — a chase that
+// simply ran through a split would stop there and never shift the trailing
+// block, which is the one that carries the residual row (Q(m-1, :)).
+void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q) {
+    if (m < 2) return;
+    // dense band scratch (row-major m x m, only |i-j| <= 2 ever non-zero)
+    std::vector<double> A(size_t(m) * m, 0.0);
+    std::vector<char> split(size_t(m), 0);  // split[p]: a block starts at p
+    auto at = [&](int i, int j) -> double& { return A[size_t(i) * m + j]; };
+    for (int i = 0; i < m; ++i) at(i, i) = d[i];
+    for (int i = 0; i + 1 < m; ++i) {
+        const double ei = std::fabs(e[i]) <= DBL_EPSILON * (std::fabs(d[i]) + std::fabs(d[i + 1])) ? 0.0 : e[i];
+        at(i + 1, i) = at(i, i + 1) = ei;
+        split[size_t(i) + 1] = ei == 0.0;
+    }
+    split[0] = 1;
+    double x = 0.0, z = 0.0;
+    for (int p = 0; p + 1 < m; ++p) {
+        const int q = p + 1;
+        if (split[size_t(q)]) continue;  // 1x1 block or block end: nothing couples p and q
+        if (split[size_t(p)]) {          // top of an unreduced block: first column of T - mu I
+            x = at(p, p) - mu;
+            z = at(q, p);
+        } else {                          // chase the bulge
+            x = at(p, p - 1);
+            z = at(q, p - 1);
+        }
+        const double r = std::hypot(x, z);
+        const double c = r == 0.0 ? 1.0 : x / r, s = r == 0.0 ? 0.0 : z / r;
+        const int lo = std::max(0, p - 1), hi = std::min(m - 1, p + 2);
+        for (int j = lo; j <= hi; ++j) {  // rows p, q  (G^T T)
+            const double ap = at(p, j), aq = at(q, j);
+            at(p, j) = c * ap + s * aq;
+            at(q, j) = -s * ap + c * aq;
+        }
+        for (int i = lo; i <= hi; ++i) {  // cols p, q  (T G)
+            const double ap = at(i, p), aq = at(i, q);
+            at(i, p) = c * ap + s * aq;
+            at(i, q) = -s * ap + c * aq;
+        }
+        if (!split[size_t(p)]) at(q, p - 1) = at(p - 1, q) = 0.0;  // bulge annihilated
+        double* qp = Q + size_t(p) * m;
+        double* qq = Q + size_t(q) * m;
+        for (int i = 0; i < m; ++i) {
+            const double a = qp[i], b = qq[i];
+            qp[i] = c * a + s * b;
+            qq[i] = -s * a + c * b;
+        }
+    }
+    for (int i = 0; i < m; ++i) d[i] = at(i, i);
+    for (int i = 0; i + 1 < m; ++i) e[i] = 0.5 * (at(i + 1, i) + at(i, i + 1));
+}
+
+}  // namespace ek

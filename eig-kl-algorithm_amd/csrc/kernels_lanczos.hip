@@ -1,0 +1,230 @@
+// Dense fp64 kernels of the Lanczos iteration on gfx950: classical
+// Gram-Schmidt (twice) against the basis V (column-major, ld multiple of
+// GT_ROWS, padded rows are zero), norms, and the restart GEMM V*Q.
+// All HBM-bound (the basis is read 4x per step); every reduction is a fixed
+// tree (wave64 xor-butterfly + LDS across waves + fixed-order combine), so
+// the solver is bitwise reproducible run to run.
+//
+// Reference counterparts: Spectra's Lanczos factorization + DGKS
+// re-orthogonalisation inside SymEigsSolver (cEIG.cpp:195-198), and the
+// reference GPU computeNormKernel / normalizeVectorKernel (gKL2.cu:143-188),
+// whose float atomicAdd norm is replaced by deterministic fp64 trees.
+#include <hip/hip_runtime.h>
+
+#include "ek_internal.hpp"
+
+namespace ek {
+namespace dev {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block of 256: returns the block sum in thread 0
+__device__ __forceinline__ double block_sum256(double v, double* lds4) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) lds4[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+    __syncthreads();
+    return r;
+}
+
+// partial dot products of w with GT_COLS basis columns over GT_ROWS rows.
+// grid = (nrb, ceil((ncols + has_u0) / GT_COLS)); 256 threads, each 2 x double2.
+__global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
+                                               int has_u0, double u0val, int nreal, const double* __restrict__ w,
+                                               double* __restrict__ part) {
+    __shared__ double red[4][GT_COLS];
+    const int t = threadIdx.x;
+    const int rbk = blockIdx.x, j0 = blockIdx.y * GT_COLS;
+    const size_t r0 = size_t(rbk) * GT_ROWS + 2 * size_t(t);
+    const double2 w0 = *reinterpret_cast<const double2*>(w + r0);
+    const double2 w1 = *reinterpret_cast<const double2*>(w + r0 + 512);
+    double acc[GT_COLS];
+#pragma unroll
+    for (int jj = 0; jj < GT_COLS; ++jj) {
+        const int j = j0 + jj;
+        double a = 0.0;
+        if (j < ncols) {
+            const double* vj = V + size_t(j) * ldv;
+            const double2 v0 = *reinterpret_cast<const double2*>(vj + r0);
+            const double2 v1 = *reinterpret_cast<const double2*>(vj + r0 + 512);
+            a = v0.x * w0.x + v0.y * w0.y + v1.x * w1.x + v1.y * w1.y;
+        } else if (has_u0 && j == ncols) {
+            const size_t nr = size_t(nreal);
+            a = u0val * ((r0 < nr ? w0.x : 0.0) + (r0 + 1 < nr ? w0.y : 0.0) + (r0 + 512 < nr ? w1.x : 0.0) +
+                         (r0 + 513 < nr ? w1.y : 0.0));
+        }
+        acc[jj] = wave_sum(a);
+    }
+    if ((t & 63) == 0) {
+#pragma unroll
+        for (int jj = 0; jj < GT_COLS; ++jj) red[t >> 6][jj] = acc[jj];
+    }
+    __syncthreads();
+    if (t < GT_COLS && j0 + t < ncols + has_u0)
+        part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+}
+
+// h[j] = sum_b part[j*nrb + b]; one workgroup per column.
+__global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ part, int nrb, double* __restrict__ h) {
+    __shared__ double lds4[4];
+    const double* pj = part + size_t(blockIdx.x) * nrb;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nrb; i += 256) s += pj[i];
+    s = block_sum256(s, lds4);
+    if (threadIdx.x == 0) h[blockIdx.x] = s;
+}
+
+// dst = src - V[:, :ncols] h - u0 h[ncols]; 256 threads x 2 rows (double2).
+__global__ __launch_bounds__(256) void k_update(int ldv, const double* __restrict__ V, int ncols, int has_u0,
+                                                double u0val, int nreal, const double* __restrict__ h,
+                                                const double* __restrict__ src, double* __restrict__ dst,
+                                                double* __restrict__ npart) {
+    __shared__ double hs[MAX_NCV + 2];
+    __shared__ double lds4[4];
+    for (int j = threadIdx.x; j < ncols + has_u0; j += 256) hs[j] = h[j];
+    __syncthreads();
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    double2 x = *reinterpret_cast<const double2*>(src + r);
+    for (int j = 0; j < ncols; ++j) {
+        const double2 v = *reinterpret_cast<const double2*>(V + size_t(j) * ldv + r);
+        x.x -= v.x * hs[j];
+        x.y -= v.y * hs[j];
+    }
+    if (has_u0) {
+        const double c = u0val * hs[ncols];
+        if (r < size_t(nreal)) x.x -= c;
+        if (r + 1 < size_t(nreal)) x.y -= c;
+    }
+    *reinterpret_cast<double2*>(dst + r) = x;
+    if (npart) {
+        const double s = block_sum256(x.x * x.x + x.y * x.y, lds4);
+        if (threadIdx.x == 0) npart[blockIdx.x] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_finalize_step(const double* __restrict__ npart, int nb,
+                                                       double* __restrict__ fn2_out, const double* __restrict__ h1,
+                                                       const double* __restrict__ h2, int step,
+                                                       double* __restrict__ alpha, double* __restrict__ offd) {
+    __shared__ double lds4[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += 256) s += npart[i];
+    s = block_sum256(s, lds4);
+    if (threadIdx.x == 0) {
+        fn2_out[0] = s;
+        if (step >= 0) {
+            alpha[step] = h1[step] + h2[step];
+            if (step > 0) offd[step] = h1[step - 1] + h2[step - 1];
+        }
+    }
+}
+
+// out[:, j] = sum_{i<m} V[:, i] Q[i, j], j < kk; grid (ldv/512, ceil(kk/8)).
+__global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restrict__ V, int m,
+                                                 const double* __restrict__ Q, int kk, double* __restrict__ out) {
+    constexpr int TJ = 8;
+    __shared__ double qs[MAX_NCV][TJ];
+    const int j0 = blockIdx.y * TJ;
+    for (int i = threadIdx.x; i < m * TJ; i += 256) {
+        const int row = i / TJ, jj = i % TJ;
+        qs[row][jj] = (j0 + jj < kk) ? Q[size_t(j0 + jj) * m + row] : 0.0;
+    }
+    __syncthreads();
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    double2 acc[TJ];
+#pragma unroll
+    for (int jj = 0; jj < TJ; ++jj) acc[jj] = make_double2(0.0, 0.0);
+    for (int i = 0; i < m; ++i) {
+        const double2 v = *reinterpret_cast<const double2*>(V + size_t(i) * ldv + r);
+#pragma unroll
+        for (int jj = 0; jj < TJ; ++jj) {
+            acc[jj].x += v.x * qs[i][jj];
+            acc[jj].y += v.y * qs[i][jj];
+        }
+    }
+#pragma unroll
+    for (int jj = 0; jj < TJ; ++jj)
+        if (j0 + jj < kk) *reinterpret_cast<double2*>(out + size_t(j0 + jj) * ldv + r) = acc[jj];
+}
+
+// f = f*sigma + x*hk, per-block sum of f^2
+__global__ __launch_bounds__(256) void k_axpby_norm(double* __restrict__ f, double sigma,
+                                                    const double* __restrict__ x, double hk,
+                                                    double* __restrict__ npart) {
+    __shared__ double lds4[4];
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    double2 a = *reinterpret_cast<const double2*>(f + r);
+    const double2 b = *reinterpret_cast<const double2*>(x + r);
+    a.x = a.x * sigma + b.x * hk;
+    a.y = a.y * sigma + b.y * hk;
+    *reinterpret_cast<double2*>(f + r) = a;
+    const double s = block_sum256(a.x * a.x + a.y * a.y, lds4);
+    if (threadIdx.x == 0) npart[blockIdx.x] = s;
+}
+
+// per-block sum (or sum of squares) of x over real rows
+__global__ __launch_bounds__(256) void k_sum_partial(const double* __restrict__ x, int nreal,
+                                                     double* __restrict__ npart, int squares) {
+    __shared__ double lds4[4];
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    const double2 a = *reinterpret_cast<const double2*>(x + r);
+    const double ax = r < size_t(nreal) ? a.x : 0.0, ay = r + 1 < size_t(nreal) ? a.y : 0.0;
+    const double s = block_sum256(squares ? ax * ax + ay * ay : ax + ay, lds4);
+    if (threadIdx.x == 0) npart[blockIdx.x] = s;
+}
+
+// x[r] -= (*mean_sum) * inv_n on real rows (projection off the constant vector)
+__global__ __launch_bounds__(256) void k_sub_mean(double* __restrict__ x, int nreal, const double* __restrict__ sum,
+                                                  double inv_n) {
+    const size_t r = size_t(blockIdx.x) * 256 + threadIdx.x;
+    if (r < size_t(nreal)) x[r] -= (*sum) * inv_n;
+}
+
+void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
+           const double* w, double* part) {
+    const int cols = ncols + has_u0;
+    if (cols <= 0) return;
+    hipLaunchKernelGGL(k_gemvt, dim3(nrb, (cols + GT_COLS - 1) / GT_COLS), dim3(256), 0, s, ldv, nrb, V, ncols,
+                       has_u0, u0val, nreal, w, part);
+}
+
+void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h) {
+    if (ncols_total <= 0) return;
+    hipLaunchKernelGGL(k_reduce_cols, dim3(ncols_total), dim3(256), 0, s, part, nrb, h);
+}
+
+void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
+            const double* h, const double* src, double* dst, double* npart) {
+    hipLaunchKernelGGL(k_update, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal, h, src,
+                       dst, npart);
+}
+
+void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1, const double* h2,
+                   int step, double* alpha, double* offd) {
+    hipLaunchKernelGGL(k_finalize_step, dim3(1), dim3(256), 0, s, npart, nb, fn2_out, h1, h2, step, alpha, offd);
+}
+
+void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out) {
+    hipLaunchKernelGGL(k_gemm_vq, dim3(ldv / UPD_ROWS, (kk + 7) / 8), dim3(256), 0, s, ldv, V, m, Q, kk, out);
+}
+
+void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart) {
+    hipLaunchKernelGGL(k_axpby_norm, dim3(ldv / UPD_ROWS), dim3(256), 0, s, f, sigma, x, hk, npart);
+}
+
+void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares) {
+    hipLaunchKernelGGL(k_sum_partial, dim3(ldv / UPD_ROWS), dim3(256), 0, s, x, nreal, npart, squares);
+}
+
+void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* mean_sum, double inv_n) {
+    hipLaunchKernelGGL(k_sub_mean, dim3(ldv / 256), dim3(256), 0, s, x, nreal, mean_sum, inv_n);
+}
+
+}  // namespace dev
+}  // namespace ek

@@ -1,0 +1,218 @@
+/*
+ * eigkl.h — C-ABI of libeigkl_hip.so, the MI355X (gfx950) EIG+KL hypergraph
+ * bipartitioner.  Plain pointers and sizes only; no torch / HIP types.
+ *
+ * The reference (yhinai/EIG-KL-Algorithm) has no library or FFI: its seams
+ * are (1) the process/CLI + file boundary of cEIG/cKL/gKL/gKL2,
+ * (2) Spectra's MatOp `perform_op(x_in, y_out)` consumed by SymEigsSolver at
+ * cEIG.cpp:194-198, (3) gKL's `gpuConnections(...)` gain seam at
+ * gKL.cu:188-227 driven by the KL loop at cKL.cpp:334-390.  Each entry point
+ * below names the reference interface it replaces.
+ *
+ * Conventions: every int-returning call returns EK_OK (0) or a negative
+ * ek_status; ek_last_error() gives a thread-local message.  The library never
+ * calls exit() (unlike CHECK_CUDA at gKL.cu:87-94).  A context is bound to
+ * one GPU and is not thread-safe; use one host thread (or process) per GPU.
+ * There is NO CPU fallback: GPU entry points fail with EK_EHIP when no
+ * gfx950 device is usable.
+ */
+#ifndef EIGKL_H
+#define EIGKL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ek_status {
+    EK_OK = 0,
+    EK_EINVAL = -1,  /* bad argument / malformed input file */
+    EK_EIO = -2,     /* file cannot be opened / written */
+    EK_EHIP = -3,    /* HIP runtime error or no usable GPU */
+    EK_ENOMEM = -4,
+    EK_ENOCONV = -5, /* eigensolver did not converge ("Eigenvalue computation failed", cEIG.cpp:200-202) */
+    EK_ESTATE = -6,  /* call out of order (e.g. ek_kl_run before ek_kl_graph_setup) */
+    EK_ECOMM = -7    /* RCCL error */
+};
+
+const char* ek_last_error(void);
+const char* ek_version(void);
+
+/* ------------------------------------------------------------------ */
+/* Hypergraph ingest (host, no GPU)                                     */
+/* ------------------------------------------------------------------ */
+typedef struct ek_hgr ek_hgr;
+
+/* Read a .hgr file: header "nets nodes", then one line per net of 1-based
+ * pins.  Replaces the per-executable readers cEIG.cpp:177-182,91-101 and
+ * cKL.cpp:84-116 (same line semantics: exactly `nets` lines are read). */
+int ek_hgr_read(const char* path, ek_hgr** out);
+/* Seeded ISPD98-shaped synthetic circuit: floor(201920*mult) nodes,
+ * floor(210613*mult) nets, net sizes {2:84,3:2,4:6,5:2,6:4,8:2}/100, distinct
+ * sorted pins.  Replaces circuit_generator.py:41-59 (whose RNG is unseeded). */
+int ek_hgr_generate(double multiplier, uint64_t seed, ek_hgr** out);
+/* Build from 0-based pins: net e owns pins[net_ptr[e] .. net_ptr[e+1]). */
+int ek_hgr_from_pins(int64_t nets, int64_t nodes, const int64_t* net_ptr, const int32_t* pins,
+                     ek_hgr** out);
+/* Write in the reference .hgr text format (circuit_generator.py:61-68). */
+int ek_hgr_write(const ek_hgr* h, const char* path);
+int ek_hgr_dims(const ek_hgr* h, int64_t* nets, int64_t* nodes, int64_t* pins);
+int ek_hgr_copy_pins(const ek_hgr* h, int64_t* net_ptr /* nets+1 */, int32_t* pins /* pins */);
+void ek_hgr_free(ek_hgr* h);
+
+/* ------------------------------------------------------------------ */
+/* Clique expansions (host, no GPU)                                     */
+/* ------------------------------------------------------------------ */
+typedef struct ek_csr ek_csr;
+
+/* fp64 clique Laplacian, -2/|e| per pin pair, diagonal = -(row sum); rows
+ * with ascending columns, diagonal included.  Replaces initializeMatrix,
+ * cEIG.cpp:86-133. */
+int ek_laplacian_build(const ek_hgr* h, ek_csr** out);
+/* fp32 KL adjacency, w = 1/(|e|-1) accumulated in net order; each row holds
+ * its forward (upper-triangle) entries in the iteration order of cKL's
+ * std::unordered_map<uint32_t,float> (libstdc++ _Hashtable, emulated), then
+ * its backward entries by ascending id — the exact summation order of
+ * connections(), cKL.cpp:225-251.  Replaces InitializeSparsMatrix,
+ * cKL.cpp:84-149. */
+int ek_kl_graph_build(const ek_hgr* h, ek_csr** out);
+/* nrows, nnz, value size in bytes (8 = fp64 Laplacian, 4 = fp32 KL graph). */
+int ek_csr_dims(const ek_csr* c, int64_t* nrows, int64_t* nnz, int32_t* value_bytes);
+/* Copy out: rowptr[nrows+1], col[nnz], val[nnz] (double* or float*),
+ * nfwd[nrows] (KL graph: forward entries per row; may be NULL). */
+int ek_csr_copy(const ek_csr* c, int32_t* rowptr, int32_t* col, void* val, int32_t* nfwd);
+void ek_csr_free(ek_csr* c);
+
+/* 1-D row-block partition for the sharded Lanczos: rank r owns
+ * rows [row0, row0+nrows) with nrows <= nloc (equal padded blocks). */
+int ek_shard_rows(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows, int64_t* nloc);
+
+/* ------------------------------------------------------------------ */
+/* GPU context                                                          */
+/* ------------------------------------------------------------------ */
+typedef struct ek_ctx ek_ctx;
+
+int ek_init(int device, ek_ctx** out);
+void ek_destroy(ek_ctx* ctx);
+/* The context's hipStream_t (every kernel of this context runs on it). */
+int ek_get_stream(ek_ctx* ctx, void** stream_out);
+int ek_device_count(int* count);
+
+/* RCCL over xGMI: one process per GPU.  Rank 0 calls ek_comm_unique_id and
+ * ships the 128 bytes to the other ranks (e.g. torch.distributed broadcast). */
+int ek_comm_unique_id(void* id128);
+int ek_comm_init(ek_ctx* ctx, int nranks, int rank, const void* id128);
+
+/* ------------------------------------------------------------------ */
+/* SpMV seam: Spectra SparseSymMatProd<double>::perform_op, cEIG.cpp:194  */
+/* ------------------------------------------------------------------ */
+/* Upload the Laplacian rows this context owns.  n = global size; rowptr has
+ * nrows+1 entries starting at 0; col holds global column ids.  Host arrays
+ * are copied; the caller keeps ownership. */
+int ek_spmv_setup(ek_ctx* ctx, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr,
+                  const int32_t* col, const double* val);
+/* y[0:nrows] = L[row0:row0+nrows, :] x.  x_dev: n doubles, y_dev: nrows
+ * doubles, device pointers borrowed.  stream = hipStream_t or NULL (ctx
+ * stream).  Asynchronous. */
+int ek_spmv(ek_ctx* ctx, const double* x_dev, double* y_dev, void* stream);
+/* Same with host buffers (x: n, y: nrows); synchronous. */
+int ek_spmv_host(ek_ctx* ctx, const double* x, double* y);
+/* Algorithmic (compulsory) bytes of one ek_spmv over the owned rows, SURVEY
+ * §8d: 12*nnz (col+val) + 4*(nrows+1) (rowptr) + 8*n (x read once) +
+ * 8*nrows (y).  Single GPU: 12 nnz + 4(n+1) + 16 n. */
+int64_t ek_spmv_bytes(ek_ctx* ctx);
+
+/* ------------------------------------------------------------------ */
+/* Lanczos / Fiedler: Spectra SymEigsSolver(op, 2, min(100,n/2)),        */
+/* compute(SmallestAlge), cEIG.cpp:194-207                               */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int32_t ncv;        /* <= 0: min(100, n/2) (cEIG.cpp:195) */
+    int32_t maxit;      /* restarts; <= 0: 1000 (Spectra default) */
+    double tol;         /* <= 0: 1e-10 (Spectra default) */
+    int32_t deflate;    /* 1 (default): deflate the constant null vector, nev=1;
+                           0: Spectra-equivalent nev=2, Fiedler = 2nd smallest */
+    int32_t time_spmv;  /* 1: bracket every SpMV launch with HIP events (stats) */
+} ek_lanczos_opts;
+
+typedef struct {
+    int32_t restarts;
+    int32_t matvecs;
+    int32_t converged;
+    double residual;      /* ||L v - lambda v||_2 of the returned vector */
+    double total_ms;      /* wall time of the solve */
+    double spmv_ms;       /* sum of SpMV launch durations (time_spmv=1) */
+    int32_t spmv_timed;   /* SpMV launches timed */
+    double comm_ms;       /* time inside RCCL calls (host-observed, sharded) */
+} ek_lanczos_stats;
+
+void ek_lanczos_default_opts(ek_lanczos_opts* o);
+/* Fiedler pair of the Laplacian given to ek_spmv_setup.  v_host_out: n
+ * doubles (full vector on every rank when sharded).  Sign: the entry of
+ * largest magnitude is made positive (cKL bit parity for odd n
+ * may need ek_align_sign against the reference file). */
+int ek_lanczos_fiedler(ek_ctx* ctx, const ek_lanczos_opts* o, double* lambda_out, double* v_host_out,
+                       ek_lanczos_stats* stats);
+
+/* ------------------------------------------------------------------ */
+/* Median split + EIG file (cEIG.cpp:55-65, 209-220)                    */
+/* ------------------------------------------------------------------ */
+/* median (even n: mean of the two middle values), bits[i] = (median > v[i]). */
+int ek_median_split(int64_t n, const double* v, double* median_out, uint8_t* bits_out);
+/* Flip v if its dot product with ref is negative (--sign-ref). */
+int ek_align_sign(int64_t n, double* v, const double* ref);
+/* pre_saved_EIG/<base>_out.txt writer / reader (%.12g; cEIG.cpp:213-220,
+ * read as cKL.cpp:155-174).  The reader returns remain[] lists in file order. */
+int ek_eig_write(const char* path, int64_t n, double lambda, double median, const uint8_t* bits,
+                 const double* v);
+int ek_eig_read(const char* path, int64_t n, double* lambda, double* median, uint8_t* bits, double* v,
+                int32_t* order0, int64_t* n0, int32_t* order1, int64_t* n1);
+
+/* ------------------------------------------------------------------ */
+/* KL: KL() cKL.cpp:288-406; GPU gain seam gpuConnections gKL.cu:188-227 */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint32_t iter;       /* 1-based (cKL.cpp:371) */
+    uint32_t node_left;  /* node1: argmax gain over remain[0] (cKL.cpp:341-347) */
+    uint32_t node_right; /* node2: argmin gain over remain[1] (cKL.cpp:349-355) */
+    float max_gain, min_gain;
+    float gain;          /* maxGain - minGain - 2 w(node1,node2) (cKL.cpp:360) */
+    float cut;           /* running fp32 cut (cKL.cpp:362) */
+    uint32_t pad;
+} ek_swap;
+
+typedef struct {
+    int64_t iterations;
+    float initial_cut, best_cut, final_cut;
+    int64_t best_iter;   /* first iteration reaching best_cut (0 = initial) */
+    int64_t net_cut_initial, net_cut_best, net_cut_final; /* integer hyperedge cuts */
+    double loop_ms;      /* device time of the swap loop */
+    double total_ms;     /* device time of gain scan + loop + cuts */
+} ek_kl_result;
+
+/* Upload the KL graph (from ek_kl_graph_build, or any rows in cKL order). */
+int ek_kl_graph_setup(ek_ctx* ctx, int64_t n, const int32_t* rowptr, const int32_t* col, const float* w);
+/* Upload the hypergraph pins (for the integer net cut). */
+int ek_kl_nets_setup(ek_ctx* ctx, int64_t nets, const int64_t* net_ptr, const int32_t* pins);
+/* Initial remain[] lists (shuffleSparceMatrix, cKL.cpp:151-197): positions
+ * are list order; the sides are split[0] = order0, split[1] = order1. */
+int ek_kl_set_partition(ek_ctx* ctx, const int32_t* order0, int64_t n0, const int32_t* order1, int64_t n1);
+/* Run the swap loop to termination on the device (one persistent
+ * workgroup; no host round trip per iteration).  limit < 0: floor(log2 n)+5
+ * (cKL.cpp:303).  log_out may be NULL. */
+int ek_kl_run(ek_ctx* ctx, int32_t limit, ek_swap* log_out, int64_t cap, ek_kl_result* res);
+/* Side of every node: which = 0 initial, 1 best prefix, 2 final. */
+int ek_kl_sides(ek_ctx* ctx, int32_t which, uint8_t* sides_out);
+
+/* ------------------------------------------------------------------ */
+/* Drop-in CLIs: argv exactly as cEIG.cpp:138-237 / cKL.cpp:424-468 /    */
+/* gKL.cu:672-713 / gKL2.cu:989-1033, outputs relative to the CWD.       */
+/* tool = "cEIG" | "cKL" | "gKL" | "gKL2".  Returns the process exit code. */
+/* ------------------------------------------------------------------ */
+int ek_cli_main(const char* tool, int argc, char** argv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EIGKL_H */
