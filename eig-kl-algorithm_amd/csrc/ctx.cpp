@@ -74,9 +74,10 @@ struct ek_ctx {
     DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, Qd, scal;
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
-    DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gain, kl_order0, kl_order1, kl_pos,
+    DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
         kl_ckey0, kl_ckey1, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
     bool kl_graph_ready = false, kl_part_ready = false;
+    std::vector<int32_t> kl_rowptr_h;  // host copy (row descriptors)
 };
 
 namespace {
@@ -550,14 +551,14 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
         if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_kl_graph_setup: column out of range");
     hipStream_t s = c->stream;
     c->kl_n = n;
+    c->kl_rowptr_h.assign(rowptr, rowptr + n + 1);
     upload(c->kl_rowptr, rowptr, size_t(n) + 1, s);
     upload(c->kl_col, col, size_t(nnz), s);
     upload(c->kl_w, w, size_t(nnz), s);
     c->kl_side.ensure(size_t(n));
     c->kl_side_init.ensure(size_t(n));
     c->kl_locked.ensure(size_t(n));
-    c->kl_gain.ensure(size_t(n) * 4);
-    c->kl_pos.ensure(size_t(n) * 4);
+    c->kl_plist.ensure(size_t(n) * 4);
     c->kl_sides_tmp.ensure(size_t(n));
     c->kl_cutpart.ensure(size_t((n + 255) / 256) * 8);
     c->kl_cut0.ensure(16);
@@ -590,18 +591,18 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
     if (n0 < 0 || n1 < 0 || n0 + n1 != n || (n0 && !order0) || (n1 && !order1))
         ek::fail(EK_EINVAL, "ek_kl_set_partition: the two lists must cover all %lld nodes", (long long)n);
     std::vector<uint8_t> side(size_t(n), 2);
-    std::vector<int32_t> pos(size_t(n), -1);
+    std::vector<uint32_t> plist(size_t(n), 0);
     for (int64_t i = 0; i < n0; ++i) {
         const int32_t u = order0[i];
         if (u < 0 || u >= n || side[size_t(u)] != 2) ek::fail(EK_EINVAL, "ek_kl_set_partition: bad/duplicate node %d", u);
         side[size_t(u)] = 0;
-        pos[size_t(u)] = int32_t(i);
+        plist[size_t(u)] = uint32_t(i);
     }
     for (int64_t i = 0; i < n1; ++i) {
         const int32_t u = order1[i];
         if (u < 0 || u >= n || side[size_t(u)] != 2) ek::fail(EK_EINVAL, "ek_kl_set_partition: bad/duplicate node %d", u);
         side[size_t(u)] = 1;
-        pos[size_t(u)] = int32_t(i);
+        plist[size_t(u)] = uint32_t(i) | 0x80000000u;
     }
     hipStream_t s = c->stream;
     c->kl_n0 = n0;
@@ -609,7 +610,31 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
     upload(c->kl_order0, order0, size_t(n0), s);
     upload(c->kl_order1, order1, size_t(n1), s);
     upload(c->kl_side_init, side.data(), size_t(n), s);
-    upload(c->kl_pos, pos.data(), size_t(n), s);
+    upload(c->kl_plist, plist.data(), size_t(n), s);
+    // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr, rowlen, plist}
+    {
+        const auto& rp = c->kl_rowptr_h;
+        std::vector<ek::dev::KLInfo> p0(size_t(std::max<int64_t>(n0, 1))), p1(size_t(std::max<int64_t>(n1, 1))),
+            nd(static_cast<size_t>(n));
+        for (int64_t i = 0; i < n0; ++i) {
+            const int32_t u = order0[i];
+            p0[size_t(i)] = {u, rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], 0};
+        }
+        for (int64_t i = 0; i < n1; ++i) {
+            const int32_t u = order1[i];
+            p1[size_t(i)] = {u, rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], 0};
+        }
+        for (int64_t u = 0; u < n; ++u)
+            nd[size_t(u)] = {rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], int32_t(plist[size_t(u)]), 0};
+        upload(c->kl_pinfo0, p0.data(), p0.size(), s);
+        upload(c->kl_pinfo1, p1.data(), p1.size(), s);
+        upload(c->kl_nd, nd.data(), nd.size(), s);
+        c->kl_cinfo0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
+        c->kl_cinfo1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
+        HIPCHK(hipStreamSynchronize(s));  // host staging vectors go out of scope
+    }
+    c->kl_gp0.ensure(size_t(std::max<int64_t>(n0, 1)) * 4);
+    c->kl_gp1.ensure(size_t(std::max<int64_t>(n1, 1)) * 4);
     c->kl_ckey0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
     c->kl_ckey1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
     c->kl_log.ensure(size_t(std::max<int64_t>(1, std::min(n0, n1))) * sizeof(ek_swap));
@@ -632,10 +657,16 @@ ek::dev::KLDev kl_dev(ek_ctx* c) {
     d.side = c->kl_side.as<uint8_t>();
     d.side_init = c->kl_side_init.as<uint8_t>();
     d.locked = c->kl_locked.as<uint8_t>();
-    d.gain = c->kl_gain.as<float>();
+    d.gp0 = c->kl_gp0.as<float>();
+    d.gp1 = c->kl_gp1.as<float>();
     d.order0 = c->kl_order0.as<int32_t>();
     d.order1 = c->kl_order1.as<int32_t>();
-    d.pos = c->kl_pos.as<int32_t>();
+    d.plist = c->kl_plist.as<uint32_t>();
+    d.pinfo0 = c->kl_pinfo0.as<ek::dev::KLInfo>();
+    d.pinfo1 = c->kl_pinfo1.as<ek::dev::KLInfo>();
+    d.nd = c->kl_nd.as<ek::dev::KLInfo>();
+    d.cinfo0 = c->kl_cinfo0.as<ek::dev::KLInfo>();
+    d.cinfo1 = c->kl_cinfo1.as<ek::dev::KLInfo>();
     d.n0 = int(c->kl_n0);
     d.n1 = int(c->kl_n1);
     d.nck0 = int((c->kl_n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK);
@@ -718,6 +749,14 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_best = nets ? int64_t(hc[1]) : -1;
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
+        if (std::getenv("EK_KL_PROF"))
+            std::fprintf(stderr, "[kl] %lld swaps: select %.3f  weight+swap %.3f  gains %.3f  re-key %.3f us/swap\n",
+                         (long long)ho.iterations, ho.prof[0] * 0.01 / std::max<long long>(1, ho.iterations),
+                         ho.prof[1] * 0.01 / std::max<long long>(1, ho.iterations),
+                         ho.prof[2] * 0.01 / std::max<long long>(1, ho.iterations),
+                         ho.prof[3] * 0.01 / std::max<long long>(1, ho.iterations));
+        if (std::getenv("EK_KL_PROF") && ho.prof[5])
+            std::fprintf(stderr, "[kl] in-loop shader clock %.0f MHz\n", double(ho.prof[4]) / (double(ho.prof[5]) * 0.01));
         res->total_ms = double(loop_ms) + double(prep_ms);
     }
     return EK_OK;

@@ -109,29 +109,46 @@ void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npa
 // kernels_kl.hip
 constexpr int KL_LOOP_THREADS = 1024;
 constexpr int KL_CHUNK = 256;
+struct alignas(16) KLInfo {
+    int32_t a, b, c, d;
+};
 struct KLDev {
     int n = 0;
     const int32_t* rowptr = nullptr;
     const int32_t* col = nullptr;
     const float* w = nullptr;
-    uint8_t* side = nullptr;        // current split (0/1)
+    uint8_t* side = nullptr;        // current split (0/1); final sides after the loop
     const uint8_t* side_init = nullptr;
-    uint8_t* locked = nullptr;      // erased from remain[]
-    float* gain = nullptr;
+    uint8_t* locked = nullptr;      // erased from remain[] (global-state mode only)
+    float* gp0 = nullptr;           // gains of remain[0] nodes, by POSITION (NaN = erased)
+    float* gp1 = nullptr;           // gains of remain[1] nodes, by position
     const int32_t* order0 = nullptr;  // remain[0] positions -> node
     const int32_t* order1 = nullptr;
-    const int32_t* pos = nullptr;     // node -> position in its list
+    const uint32_t* plist = nullptr;  // node -> position | (list << 31)
     int n0 = 0, n1 = 0, nck0 = 0, nck1 = 0;
     unsigned long long* ckey0 = nullptr;  // per-chunk best (gain, first position) keys
     unsigned long long* ckey1 = nullptr;
     double* cut_part = nullptr;
     float* cut0 = nullptr;
+    // row descriptors: by position in each list {node, rowptr, rowlen, 0} and
+    // by node {rowptr, rowlen, plist, 0}; chunk winners' descriptors
+    const KLInfo* pinfo0 = nullptr;
+    const KLInfo* pinfo1 = nullptr;
+    const KLInfo* nd = nullptr;
+    KLInfo* cinfo0 = nullptr;
+    KLInfo* cinfo1 = nullptr;
 };
+constexpr int KL_ITEM_CAP = 1024;  // affected rows whose new key/descriptor are kept in LDS
+// LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
+// chunk winners on chip (0 when they do not fit: global-state mode).
+size_t kl_loop_lds_bytes(const KLDev& d);
 struct KLOut {
     long long iterations;
     long long best_iter;
     float initial_cut, best_cut, final_cut;
     unsigned int status;
+    unsigned long long prof[6];  // EK_KL_PROF: 100 MHz ticks in select / weight+swap / gains / re-key;
+                                 // [4] shader cycles, [5] 100 MHz ticks of the whole loop
 };
 void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk keys
 void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out);

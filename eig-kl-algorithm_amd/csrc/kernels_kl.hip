@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdlib>
 
 #include "ek_internal.hpp"
 
@@ -54,43 +55,73 @@ __device__ __forceinline__ u64 key_min(float g, int pos) {
     if (!(g < FLT_MAX)) return 0ull;
     return (u64(ord_f32(-g)) << 32) | u64(~uint32_t(pos));
 }
+// wave64 max of a 64-bit key without LDS traffic: DPP quad_perm / row
+// (half-)mirror inside each 16-lane row, then gfx950's v_permlane16_swap and
+// v_permlane32_swap across rows and halves.  Every lane ends with the max.
+template <int CTRL>
+__device__ __forceinline__ u64 dpp_max(u64 v) {
+    const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
+    const unsigned lo2 = __builtin_amdgcn_update_dpp(0u, lo, CTRL, 0xf, 0xf, false);
+    const unsigned hi2 = __builtin_amdgcn_update_dpp(0u, hi, CTRL, 0xf, 0xf, false);
+    const u64 o = (u64(hi2) << 32) | lo2;
+    return o > v ? o : v;
+}
 __device__ __forceinline__ u64 wave_max_u64(u64 v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const u64 x = __shfl_xor(v, o, 64);
-        v = x > v ? x : v;
+    v = dpp_max<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_max<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = dpp_max<0x141>(v);  // row_half_mirror
+    v = dpp_max<0x140>(v);  // row_mirror
+    {
+        const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
+        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        const u64 x = (u64(b[0]) << 32) | a[0], y = (u64(b[1]) << 32) | a[1];
+        v = x > y ? x : y;
+    }
+    {
+        const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        const u64 x = (u64(b[0]) << 32) | a[0], y = (u64(b[1]) << 32) | a[1];
+        v = x > y ? x : y;
     }
     return v;
 }
 
-// connections(node), cKL.cpp:225-251, over the cKL-ordered row.
+// side of node v (0/1): LDS bitmap or global byte array
+template <bool SMEM>
+__device__ __forceinline__ uint32_t side_of(const uint32_t* s_side, const uint8_t* g_side, int v) {
+    if constexpr (SMEM) return (s_side[v >> 5] >> (v & 31)) & 1u;
+    else return g_side[v];
+}
+
+// connections(node), cKL.cpp:225-251, over the cKL-ordered row: two
+// sequential fp32 accumulators, internal = neighbour on side 0.
+template <bool SMEM>
 __device__ __forceinline__ float row_gain(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                          const float* __restrict__ w, const uint8_t* __restrict__ side, int u,
-                                          float* ext_out) {
+                                          const float* __restrict__ w, const uint32_t* s_side,
+                                          const uint8_t* g_side, int u, float* ext_out) {
     float internal = 0.0f, external = 0.0f;
     const int p1 = rowptr[u + 1];
     for (int p = rowptr[u]; p < p1; ++p) {
         const float wt = w[p];
-        if (side[col[p]] == 0) internal += wt;
+        if (side_of<SMEM>(s_side, g_side, col[p]) == 0) internal += wt;
         else external += wt;
     }
     if (ext_out) *ext_out = external;
     return external - internal;
 }
 
-__device__ __forceinline__ u64 chunk_key(const KLDev& d, int s, int c, int lane) {
-    const int32_t* order = s ? d.order1 : d.order0;
-    const int ns = s ? d.n1 : d.n0;
+// best key of 256 consecutive positions of one remain[] list (gains by position)
+__device__ __forceinline__ u64 chunk_key(const float* __restrict__ gp, int ns, int s, int c, int lane) {
     u64 k = 0ull;
 #pragma unroll
     for (int q = 0; q < KL_CHUNK / 64; ++q) {
         const int p = c * KL_CHUNK + q * 64 + lane;
         if (p < ns) {
-            const int u = order[p];
-            if (!d.locked[u]) {
-                const u64 kk = s ? key_min(d.gain[u], p) : key_max(d.gain[u], p);
-                k = kk > k ? kk : k;
-            }
+            const float g = gp[p];
+            const u64 kk = s ? key_min(g, p) : key_max(g, p);
+            k = kk > k ? kk : k;
         }
     }
     return wave_max_u64(k);
@@ -102,8 +133,10 @@ __global__ __launch_bounds__(256) void k_gain_scan(KLDev d) {
     double c = 0.0;
     if (u < d.n) {
         float ext = 0.0f;
-        d.gain[u] = row_gain(d.rowptr, d.col, d.w, d.side, u, &ext);
-        if (d.side[u] == 0) c = double(ext);
+        const float g = row_gain<false>(d.rowptr, d.col, d.w, nullptr, d.side_init, u, &ext);
+        const uint32_t pl = d.plist[u];
+        ((pl >> 31) ? d.gp1 : d.gp0)[pl & 0x7fffffffu] = g;
+        if (d.side_init[u] == 0) c = double(ext);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
@@ -125,66 +158,409 @@ __global__ __launch_bounds__(256) void k_cut_final(KLDev d, int nb) {
     if (threadIdx.x == 0) *d.cut0 = float((lds4[0] + lds4[1]) + (lds4[2] + lds4[3]));
 }
 
+// Best key of one chunk together with its winner's row descriptor.  Gains and
+// descriptors are both read by position, so the winner needs no dependent
+// load.  Returns the key in every lane; the winner lane (or lane 0 for an
+// all-invalid chunk) has *mine = true and its descriptor in *info.
+__device__ __forceinline__ u64 chunk_best(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int ns,
+                                          int s, int c, int lane, KLInfo* info, bool* mine) {
+    u64 k = 0ull;
+    int4 bi = make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < KL_CHUNK / 64; ++q) {
+        const int p = c * KL_CHUNK + q * 64 + lane;
+        if (p < ns) {
+            const float g = gp[p];
+            const int4 pi = *reinterpret_cast<const int4*>(pinfo + p);
+            const u64 kk = s ? key_min(g, p) : key_max(g, p);
+            if (kk > k) {
+                k = kk;
+                bi = pi;
+            }
+        }
+    }
+    const u64 m = wave_max_u64(k);
+    const u64 bal = __ballot(m != 0ull && k == m);
+    *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
+    info->a = bi.x;
+    info->b = bi.y;
+    info->c = bi.z;
+    info->d = bi.w;
+    return m;
+}
+
 __global__ __launch_bounds__(256) void k_chunk_init(KLDev d) {
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wv < d.nck0) {
-        const u64 k = chunk_key(d, 0, wv, lane);
-        if (lane == 0) d.ckey0[wv] = k;
-    } else if (wv < d.nck0 + d.nck1) {
-        const u64 k = chunk_key(d, 1, wv - d.nck0, lane);
-        if (lane == 0) d.ckey1[wv - d.nck0] = k;
+    if (wv >= d.nck0 + d.nck1) return;
+    const int s = wv < d.nck0 ? 0 : 1, c = s ? wv - d.nck0 : wv;
+    if (d.pinfo0) {
+        KLInfo info;
+        bool mine;
+        const u64 k = s ? chunk_best(d.gp1, d.pinfo1, d.n1, 1, c, lane, &info, &mine)
+                        : chunk_best(d.gp0, d.pinfo0, d.n0, 0, c, lane, &info, &mine);
+        if (mine) {
+            (s ? d.ckey1 : d.ckey0)[c] = k;
+            (s ? d.cinfo1 : d.cinfo0)[c] = info;
+        }
+    } else {
+        const u64 k = s ? chunk_key(d.gp1, d.n1, 1, c, lane) : chunk_key(d.gp0, d.n0, 0, c, lane);
+        if (lane == 0) (s ? d.ckey1 : d.ckey0)[c] = k;
     }
 }
 
+size_t kl_loop_lds_bytes(const KLDev& d) {
+    const size_t words = (size_t(d.n) + 31) / 32;
+    const size_t b = (size_t(d.nck0) + size_t(d.nck1)) * (sizeof(KLInfo) + 8 + 8 + 4 + 4) +
+                     size_t(KL_ITEM_CAP) * (sizeof(KLInfo) + 8 + 4) + 16 + 2 * words * 4 + 64;
+    return b <= 152 * 1024 ? b : 0;
+}
+
+// Row gain with the side bitmap in LDS; the row's col/w are fetched 32 at a
+// time (independent loads in flight: one round trip for almost every row)
+// and then summed strictly in row order.
+__device__ __forceinline__ float row_gain_lds(const int32_t* __restrict__ col, const float* __restrict__ w,
+                                              const uint32_t* s_side, int rp, int len) {
+    constexpr int B = 32;
+    float internal = 0.0f, external = 0.0f;
+    const int e = rp + len;
+    for (int p = rp; p < e; p += B) {
+        int cc[B];
+        float ww[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            cc[j] = p + j < e ? col[p + j] : 0;
+            ww[j] = p + j < e ? w[p + j] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            if (p + j < e) {
+                if (((s_side[cc[j] >> 5] >> (cc[j] & 31)) & 1u) == 0) internal += ww[j];
+                else external += ww[j];
+            }
+        }
+    }
+    return external - internal;
+}
+
+// The swap loop (cKL.cpp:334-390) in ONE persistent workgroup, on-chip state:
+// LDS holds the side/locked bitmaps, every chunk's best key AND its winner's
+// row descriptor {node, rowptr, rowlen}, and the affected-chunk list.  Every
+// wave performs the selection itself from LDS (no barrier), so a swap costs
+// two workgroup barriers and four dependent global round trips: row of node1
+// (edge weight), descriptor + row of each affected node (gain), and the
+// gains + descriptors of each re-keyed chunk.
+template <bool PROF>
+__global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int limit, ek_swap* __restrict__ log,
+                                                                 long long cap, KLOut* __restrict__ out) {
+    constexpr int NW = KL_LOOP_THREADS / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int words = (d.n + 31) / 32;
+    // LDS carve (kl_loop_lds_bytes): 16-B records first, then 8-B, then 4-B
+    KLInfo* ci0 = reinterpret_cast<KLInfo*>(smem);  // chunk winners' descriptors
+    KLInfo* ci1 = ci0 + d.nck0;
+    KLInfo* it_info = ci1 + d.nck1;                   // per affected row: its descriptor
+    u64* ck0 = reinterpret_cast<u64*>(it_info + KL_ITEM_CAP);  // chunk keys (read by the selection)
+    u64* ck1 = ck0 + d.nck0;
+    u64* ckn0 = ck1 + d.nck1;  // shadow keys: G1 merges risen keys here, G2 publishes them to ck
+    u64* ckn1 = ckn0 + d.nck0;
+    u64* it_key = ckn1 + d.nck1;                                // per affected row: its new key
+    int* dtag0 = reinterpret_cast<int*>(it_key + KL_ITEM_CAP);  // iteration that tagged a rescan
+    int* dtag1 = dtag0 + d.nck0;
+    int* ctag0 = dtag1 + d.nck1;                               // iteration that claimed the rescan
+    int* ctag1 = ctag0 + d.nck0;
+    int* it_cs = ctag1 + d.nck1;                               // per affected row: list<<31 | chunk
+    int* s_stop = it_cs + KL_ITEM_CAP;                         // [2], by iteration parity
+    uint32_t* s_side = reinterpret_cast<uint32_t*>(s_stop + 4);
+    uint32_t* s_lock = s_side + words;
+    for (int i = tid; i < d.nck0; i += KL_LOOP_THREADS) {
+        ck0[i] = ckn0[i] = d.ckey0[i];
+        ci0[i] = d.cinfo0[i];
+        dtag0[i] = ctag0[i] = -1;
+    }
+    for (int i = tid; i < d.nck1; i += KL_LOOP_THREADS) {
+        ck1[i] = ckn1[i] = d.ckey1[i];
+        ci1[i] = d.cinfo1[i];
+        dtag1[i] = ctag1[i] = -1;
+    }
+    for (int i = tid; i < words; i += KL_LOOP_THREADS) {
+        uint32_t b = 0;
+        for (int j = 0; j < 32 && i * 32 + j < d.n; ++j) b |= uint32_t(d.side_init[i * 32 + j] == 1) << j;
+        s_side[i] = b;
+        s_lock[i] = 0u;
+    }
+    __syncthreads();
+    float cut = *d.cut0, best = cut;  // loop-carried scalars: thread 0 only
+    long long best_it = 0, it = 0;
+    unsigned term = 0;
+    unsigned long long tph[4] = {0, 0, 0, 0}, tstamp = 0;  // diagnostic build only (PROF)
+    const unsigned long long c_start = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long r_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    auto stamp = [&](int ph) {
+        if constexpr (PROF) {
+            if (tid == 0) {
+                const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                if (ph >= 0) tph[ph] += t - tstamp;
+                tstamp = t;
+            }
+        }
+    };
+    for (;; ++it) {
+        stamp(-1);
+        // S. selection (cKL.cpp:341-355), redundantly in every wave
+        u64 k0 = 0ull, k1 = 0ull;
+        for (int c = lane; c < d.nck0; c += 64) k0 = ck0[c] > k0 ? ck0[c] : k0;
+        for (int c = lane; c < d.nck1; c += 64) k1 = ck1[c] > k1 ? ck1[c] : k1;
+        k0 = wave_max_u64(k0);
+        k1 = wave_max_u64(k1);
+        if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
+        const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
+        const KLInfo ia = ci0[posA / KL_CHUNK], ib = ci1[posB / KL_CHUNK];
+        const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
+        stamp(0);
+        // W. swap + erase (swip, cKL.cpp:274-286): each wave applies the
+        // (idempotent) bitmap flips itself, so no barrier is needed before G
+        if (lane == 0) {
+            atomicOr(&s_side[A >> 5], 1u << (A & 31));
+            atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
+            atomicOr(&s_lock[A >> 5], 1u << (A & 31));
+            atomicOr(&s_lock[B >> 5], 1u << (B & 31));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (wv == 0) {  // w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
+            float gA = 0.f, gB = 0.f;
+            if (lane == 0) {
+                gA = d.gp0[posA];
+                gB = d.gp1[posB];
+            }
+            float wab = 0.0f;
+            bool found = false;
+            for (int i = lane; i < la; i += 64)
+                if (d.col[pa + i] == B) {
+                    wab = d.w[pa + i];
+                    found = true;
+                }
+            const u64 bal = __ballot(found);
+            if (bal) wab = __shfl(wab, __ffsll((long long)bal) - 1, 64);
+            if (lane == 0) {
+                d.gp0[posA] = __builtin_nanf("");
+                d.gp1[posB] = __builtin_nanf("");
+                dtag0[posA / KL_CHUNK] = int(it);  // A and B were their chunks' winners
+                dtag1[posB / KL_CHUNK] = int(it);
+                const float gain = gA - gB - 2.0f * wab;
+                cut -= gain;
+                if (cut < best) {
+                    best = cut;
+                    best_it = it + 1;
+                }
+                if (it < cap)
+                    log[it] = ek_swap{uint32_t(it + 1), uint32_t(A), uint32_t(B), gA, gB, gain, cut, 0u};
+                int stop = 0;
+                if (gain <= 0.0f) {
+                    if (++term > unsigned(limit)) stop = 1;
+                } else {
+                    term = 0;
+                }
+                if (it + 1 >= d.n0 || it + 1 >= d.n1) stop = 1;  // a remain[] list is exhausted
+                s_stop[it & 1] = stop;
+            }
+        }
+        stamp(1);
+        // G1. gains of N(A) u N(B) (updateAffectedNodeGains, cKL.cpp:253-272),
+        //     keeping the chunk keys exact incrementally: a risen key is merged
+        //     with an LDS atomicMax (its descriptor is written in G2 if it won);
+        //     a chunk whose winner fell (or was erased: A's, B's) is tagged for a
+        //     full rescan.  Chunks keys are exact at every iteration start, so
+        //     max(old key, risen keys) is exact for untagged chunks.
+        const int tot = la + lb;
+        const int tag = int(it);
+        for (int i = tid; i < tot; i += KL_LOOP_THREADS) {
+            const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
+            int cs = -1;
+            u64 kn = 0ull;
+            KLInfo inf{0, 0, 0, 0};
+            if (!((s_lock[u >> 5] >> (u & 31)) & 1u)) {
+                const int4 nd = *reinterpret_cast<const int4*>(d.nd + u);  // {rowptr, len, plist}
+                const float g = row_gain_lds(d.col, d.w, s_side, nd.x, nd.y);
+                const uint32_t pl = uint32_t(nd.z);
+                const int s = int(pl >> 31), p = int(pl & 0x7fffffffu), c = p / KL_CHUNK;
+                (s ? d.gp1 : d.gp0)[p] = g;
+                kn = s ? key_min(g, p) : key_max(g, p);
+                const u64 K = (s ? ck1 : ck0)[c];  // stable during the iteration (other waves may still select)
+                if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(p) && kn < K) {
+                    (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
+                } else if (kn > K) {
+                    atomicMax(&(s ? ckn1 : ckn0)[c], kn);
+                    if (i >= KL_ITEM_CAP) (s ? dtag1 : dtag0)[c] = tag;  // no LDS slot for its descriptor
+                }
+                cs = int((pl & 0x80000000u) | uint32_t(c));
+                inf = KLInfo{u, nd.x, nd.y, 0};
+            }
+            if (i < KL_ITEM_CAP) {
+                it_key[i] = kn;
+                it_cs[i] = cs;
+                it_info[i] = inf;
+            }
+        }
+        __syncthreads();  // (1) gains, merged keys and rescan tags visible
+        stamp(2);
+        // G2. publish merged keys of untagged chunks (every item of the chunk
+        // writes the same value) and the descriptor of the item that won ...
+        for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
+            const int cs = it_cs[i];
+            if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
+            const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
+            if ((s ? dtag1 : dtag0)[c] == tag) continue;
+            const u64 kmerged = (s ? ckn1 : ckn0)[c];
+            (s ? ck1 : ck0)[c] = kmerged;
+            if (kmerged == it_key[i]) (s ? ci1 : ci0)[c] = it_info[i];
+        }
+        // ... and full rescans of the tagged chunks (one wave each, claimed once)
+        for (int i = wv; i < tot + 2; i += NW) {
+            int cs;
+            if (i == tot) cs = posA / KL_CHUNK;
+            else if (i == tot + 1) cs = int(0x80000000u | uint32_t(posB / KL_CHUNK));
+            else if (i < KL_ITEM_CAP) cs = it_cs[i];
+            else {  // beyond the LDS item list (hubs): rederive
+                const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
+                cs = ((s_lock[u >> 5] >> (u & 31)) & 1u) ? -1 : int((uint32_t(d.nd[u].c) & 0x80000000u) |
+                                                                     ((uint32_t(d.nd[u].c) & 0x7fffffffu) / KL_CHUNK));
+            }
+            if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
+            const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
+            if ((s ? dtag1 : dtag0)[c] != tag) continue;
+            int claimed = 0;
+            if (lane == 0) claimed = atomicMax(&(s ? ctag1 : ctag0)[c], tag) < tag;
+            if (!__shfl(claimed, 0, 64)) continue;
+            KLInfo info;
+            bool mine;
+            const u64 k = s ? chunk_best(d.gp1, d.pinfo1, d.n1, 1, c, lane, &info, &mine)
+                            : chunk_best(d.gp0, d.pinfo0, d.n0, 0, c, lane, &info, &mine);
+            if (mine) {
+                (s ? ck1 : ck0)[c] = k;
+                (s ? ckn1 : ckn0)[c] = k;
+                (s ? ci1 : ci0)[c] = info;
+            }
+        }
+        __syncthreads();  // (2) keys visible to the next selection
+        stamp(3);
+        if (s_stop[it & 1]) {
+            ++it;
+            break;
+        }
+    }
+    __syncthreads();
+    for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
+    if (tid == 0) {
+        out->iterations = it;
+        out->best_iter = best_it;
+        out->initial_cut = *d.cut0;
+        out->best_cut = best;
+        out->final_cut = cut;
+        out->status = 2u;
+        for (int i = 0; i < 4; ++i) out->prof[i] = tph[i];
+        out->prof[4] = PROF ? __builtin_amdgcn_s_memtime() - c_start : 0ull;
+        out->prof[5] = PROF ? __builtin_amdgcn_s_memrealtime() - r_start : 0ull;
+    }
+}
+
+// The swap loop with its state in global memory: the fallback for graphs
+// whose bitmaps and chunk tables do not fit in LDS (and the A/B reference,
+// EK_KL_GLOBAL_STATE=1).  Four barriers per swap.  Only SMEM=false is launched.
+template <bool SMEM, bool PROF>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit, ek_swap* __restrict__ log,
                                                              long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ u64 red0[NW], red1[NW];
-    __shared__ int s_a, s_b, s_stop, s_go;
     __shared__ float s_w;
+    __shared__ int s_stop;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int words = (d.n + 31) / 32;
+    u64* ck0 = d.ckey0;
+    u64* ck1 = d.ckey1;
+    uint32_t* s_side = nullptr;
+    uint32_t* s_lock = nullptr;
+    if constexpr (SMEM) {
+        ck0 = reinterpret_cast<u64*>(smem);
+        ck1 = ck0 + d.nck0;
+        s_side = reinterpret_cast<uint32_t*>(ck1 + d.nck1);
+        s_lock = s_side + words;
+        for (int i = tid; i < d.nck0; i += KL_LOOP_THREADS) ck0[i] = d.ckey0[i];
+        for (int i = tid; i < d.nck1; i += KL_LOOP_THREADS) ck1[i] = d.ckey1[i];
+        for (int i = tid; i < words; i += KL_LOOP_THREADS) {
+            uint32_t b = 0;
+            for (int j = 0; j < 32 && i * 32 + j < d.n; ++j) b |= uint32_t(d.side_init[i * 32 + j] == 1) << j;
+            s_side[i] = b;
+            s_lock[i] = 0u;
+        }
+    }
+    if (tid == 0) s_w = 0.0f;
+    __syncthreads();
     // loop-carried scalars live in thread 0 only
     float cut = *d.cut0, best = cut;
     long long best_it = 0, it = 0;
     unsigned term = 0;
+    unsigned long long tph[4] = {0, 0, 0, 0}, tstamp = 0;  // diagnostic build only (PROF)
+    auto stamp = [&](int ph) {
+        if constexpr (PROF) {
+            if (tid == 0) {
+                const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                if (ph >= 0) tph[ph] += t - tstamp;
+                tstamp = t;
+            }
+        }
+    };
     for (;;) {
-        // 1. selection: max over chunk keys of both lists (cKL.cpp:341-355)
+        stamp(-1);
+        // S. selection (cKL.cpp:341-355): max key over both lists' chunks
         u64 k0 = 0ull, k1 = 0ull;
-        for (int c = tid; c < d.nck0; c += KL_LOOP_THREADS) k0 = d.ckey0[c] > k0 ? d.ckey0[c] : k0;
-        for (int c = tid; c < d.nck1; c += KL_LOOP_THREADS) k1 = d.ckey1[c] > k1 ? d.ckey1[c] : k1;
+        for (int c = tid; c < d.nck0; c += KL_LOOP_THREADS) k0 = ck0[c] > k0 ? ck0[c] : k0;
+        for (int c = tid; c < d.nck1; c += KL_LOOP_THREADS) k1 = ck1[c] > k1 ? ck1[c] : k1;
         k0 = wave_max_u64(k0);
         k1 = wave_max_u64(k1);
         if (lane == 0) {
             red0[wv] = k0;
             red1[wv] = k1;
         }
-        __syncthreads();
-        if (tid == 0) {
-            u64 a = 0ull, b = 0ull;
-            for (int i = 0; i < NW; ++i) {
-                a = red0[i] > a ? red0[i] : a;
-                b = red1[i] > b ? red1[i] : b;
-            }
-            s_go = (a != 0ull && b != 0ull);  // cKL.cpp:357,387-388
-            if (s_go) {
-                s_a = d.order0[~uint32_t(a & 0xffffffffull)];
-                s_b = d.order1[~uint32_t(b & 0xffffffffull)];
-            }
-            s_w = 0.0f;
+        __syncthreads();  // (1)
+        stamp(0);
+        k0 = red0[0];
+        k1 = red1[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            k0 = red0[i] > k0 ? red0[i] : k0;
+            k1 = red1[i] > k1 ? red1[i] : k1;
         }
-        __syncthreads();
-        if (!s_go) break;
-        const int A = s_a, B = s_b;
-        // 2. w(A,B) (getEdgeWeight, cKL.cpp:75-82): B occurs at most once in A's row
-        {
-            const int pa0 = d.rowptr[A], pa1 = d.rowptr[A + 1];
-            for (int p = pa0 + tid; p < pa1; p += KL_LOOP_THREADS)
-                if (d.col[p] == B) s_w = d.w[p];
-        }
-        __syncthreads();
-        // 3. pair gain, running cut, log, swap (cKL.cpp:358-386, swip :274-286)
+        if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (uniform)
+        const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
+        const int A = d.order0[posA], B = d.order1[posB];
+        const int pa = d.rowptr[A], la = d.rowptr[A + 1] - pa;
+        const int pb = d.rowptr[B], lb = d.rowptr[B + 1] - pb;
+        // W. w(A,B) (getEdgeWeight, cKL.cpp:75-82); swap + erase (swip, cKL.cpp:274-286)
+        float gA = 0.f, gB = 0.f;
         if (tid == 0) {
-            const float gA = d.gain[A], gB = d.gain[B];
+            gA = d.gp0[posA];
+            gB = d.gp1[posB];
+            d.gp0[posA] = __builtin_nanf("");
+            d.gp1[posB] = __builtin_nanf("");
+            if constexpr (SMEM) {
+                s_side[A >> 5] |= 1u << (A & 31);
+                s_side[B >> 5] &= ~(1u << (B & 31));
+                s_lock[A >> 5] |= 1u << (A & 31);
+                s_lock[B >> 5] |= 1u << (B & 31);
+            } else {
+                d.side[A] = 1;
+                d.side[B] = 0;
+                d.locked[A] = 1;
+                d.locked[B] = 1;
+            }
+        }
+        for (int i = tid; i < la; i += KL_LOOP_THREADS)
+            if (d.col[pa + i] == B) s_w = d.w[pa + i];  // B occurs at most once in A's row
+        __syncthreads();  // (2)
+        stamp(1);
+        if (tid == 0) {   // pair gain, running cut, log, termination (cKL.cpp:358-386)
             const float gain = gA - gB - 2.0f * s_w;
             cut -= gain;
             ++it;
@@ -193,10 +569,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
                 best_it = it;
             }
             if (it <= cap) log[it - 1] = ek_swap{uint32_t(it), uint32_t(A), uint32_t(B), gA, gB, gain, cut, 0u};
-            d.locked[A] = 1;
-            d.locked[B] = 1;
-            d.side[A] = 1;
-            d.side[B] = 0;
             int stop = 0;
             if (gain <= 0.0f) {
                 if (++term > unsigned(limit)) stop = 1;
@@ -206,25 +578,36 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
             if (it >= d.n0 || it >= d.n1) stop = 1;  // a remain[] list is exhausted
             s_stop = stop;
         }
-        __syncthreads();
-        // 4. gains of N(A) u N(B) (updateAffectedNodeGains, cKL.cpp:253-272)
-        const int pa = d.rowptr[A], la = d.rowptr[A + 1] - pa;
-        const int pb = d.rowptr[B], lb = d.rowptr[B + 1] - pb;
+        // G. gains of N(A) u N(B) (updateAffectedNodeGains, cKL.cpp:253-272)
         for (int i = tid; i < la + lb; i += KL_LOOP_THREADS) {
             const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
-            d.gain[u] = row_gain(d.rowptr, d.col, d.w, d.side, u, nullptr);
+            bool lk;
+            if constexpr (SMEM) lk = (s_lock[u >> 5] >> (u & 31)) & 1u;
+            else lk = d.locked[u] != 0;
+            if (!lk) {
+                const float g = row_gain<SMEM>(d.rowptr, d.col, d.w, s_side, d.side, u, nullptr);
+                const uint32_t pl = d.plist[u];
+                ((pl >> 31) ? d.gp1 : d.gp0)[pl & 0x7fffffffu] = g;
+            }
         }
-        __syncthreads();
-        // 5. re-key the chunks holding A, B and every affected node
+        __syncthreads();  // (3)
+        stamp(2);
+        // K. re-key the chunks holding A, B and every affected node
         for (int i = wv; i < la + lb + 2; i += NW) {
             const int u = i < la ? d.col[pa + i] : i < la + lb ? d.col[pb + i - la] : (i == la + lb ? A : B);
-            const int s = d.side_init[u];
-            const int c = d.pos[u] / KL_CHUNK;
-            const u64 k = chunk_key(d, s, c, lane);
-            if (lane == 0) (s ? d.ckey1 : d.ckey0)[c] = k;
+            const uint32_t pl = d.plist[u];
+            const int s = int(pl >> 31), c = int(pl & 0x7fffffffu) / KL_CHUNK;
+            const u64 k = s ? chunk_key(d.gp1, d.n1, 1, c, lane) : chunk_key(d.gp0, d.n0, 0, c, lane);
+            if (lane == 0) (s ? ck1 : ck0)[c] = k;
         }
-        __syncthreads();
+        if (tid == 0) s_w = 0.0f;
+        __syncthreads();  // (4)
+        stamp(3);
         if (s_stop) break;
+    }
+    if constexpr (SMEM) {
+        __syncthreads();
+        for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
     }
     if (tid == 0) {
         out->iterations = it;
@@ -232,7 +615,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
         out->initial_cut = *d.cut0;
         out->best_cut = best;
         out->final_cut = cut;
-        out->status = 0u;
+        out->status = SMEM ? 1u : 0u;
+        for (int i = 0; i < 4; ++i) out->prof[i] = tph[i];
     }
 }
 
@@ -278,7 +662,17 @@ void kl_prepare(hipStream_t s, const KLDev& d) {
 }
 
 void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out) {
-    hipLaunchKernelGGL(k_kl_loop, dim3(1), dim3(KL_LOOP_THREADS), 0, s, d, limit, log, cap, out);
+    const size_t lds = kl_loop_lds_bytes(d);
+    const bool prof = std::getenv("EK_KL_PROF") != nullptr;  // phase stamps: diagnostic instantiation
+    const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
+    if (lds && !global_state && prof)
+        hipLaunchKernelGGL((k_kl_loop_lds<true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+    else if (lds && !global_state)
+        hipLaunchKernelGGL((k_kl_loop_lds<false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+    else if (prof)
+        hipLaunchKernelGGL((k_kl_loop<false, true>), dim3(1), dim3(KL_LOOP_THREADS), 0, s, d, limit, log, cap, out);
+    else
+        hipLaunchKernelGGL((k_kl_loop<false, false>), dim3(1), dim3(KL_LOOP_THREADS), 0, s, d, limit, log, cap, out);
 }
 
 void kl_replay(hipStream_t s, int n, const uint8_t* side_init, const ek_swap* log, const long long* count,
