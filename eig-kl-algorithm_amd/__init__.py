@@ -41,7 +41,7 @@ SWAP_DTYPE = np.dtype([("iter", "<u4"), ("node_left", "<u4"), ("node_right", "<u
 
 class LanczosOpts(ctypes.Structure):
     _fields_ = [("ncv", _I32), ("maxit", _I32), ("tol", ctypes.c_double), ("deflate", _I32),
-                ("time_spmv", _I32)]
+                ("time_spmv", _I32), ("reorth", _I32)]
 
 
 class LanczosStats(ctypes.Structure):
@@ -320,9 +320,9 @@ class Context:
     def spmv_bytes(self):
         return _lib.ek_spmv_bytes(self._c)
 
-    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False):
+    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=1):
         """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207)."""
-        o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0)
+        o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0, int(reorth))
         st = LanczosStats()
         lam = ctypes.c_double()
         v = np.empty(self.n, np.float64)

@@ -71,7 +71,7 @@ struct ek_ctx {
     int block_nnz = 1024, nrb_spmv = 0;
     DBuf rb, rowptr, col, val;
     // Lanczos workspace
-    DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, Qd, scal;
+    DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, apart, Qd, scal, bov;
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
@@ -200,7 +200,7 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     c->nnz = nnz;
     c->block_nnz = nnz < 512ll * 1024 ? 512 : 1024;
     const auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
-    c->nrb_spmv = int(rbv.size()) - 1;
+    c->nrb_spmv = int(rbv.size() / 4);
     upload(c->rb, rbv.data(), rbv.size(), c->stream);
     upload(c->rowptr, rowptr, size_t(nrows) + 1, c->stream);
     upload(c->col, col, size_t(nnz), c->stream);
@@ -216,7 +216,7 @@ int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv before ek_spmv_setup");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                  c->val.as<double>(), x, y, nullptr, nullptr, nullptr, c->block_nnz);
+                  c->val.as<double>(), x, y, nullptr, nullptr, nullptr, nullptr, c->block_nnz);
     HIPCHK(hipGetLastError());
     return EK_OK;
     EK_CATCH
@@ -230,7 +230,8 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     upload(dx, x, size_t(c->n), c->stream);
     dy.ensure(size_t(std::max<int64_t>(c->nrows, 1)) * 8);
     ek::dev::spmv(c->stream, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                  c->val.as<double>(), dx.as<double>(), dy.as<double>(), nullptr, nullptr, nullptr, c->block_nnz);
+                  c->val.as<double>(), dx.as<double>(), dy.as<double>(), nullptr, nullptr, nullptr, nullptr,
+                  c->block_nnz);
     HIPCHK(hipGetLastError());
     if (c->nrows) HIPCHK(hipMemcpyAsync(y, dy.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -252,6 +253,7 @@ void ek_lanczos_default_opts(ek_lanczos_opts* o) {
     o->tol = 1e-10;
     o->deflate = 1;
     o->time_spmv = 0;
+    o->reorth = 1;
 }
 
 }  // extern "C"
@@ -296,8 +298,15 @@ struct Lanczos {
         allreduce(c, dst, 1);
     }
 
-    // Lanczos steps i = k .. m-1 (Spectra Lanczos::factorize_from): CGS2
-    // against the basis (+ the deflated constant vector).
+    // Lanczos steps i = k .. m-1 (Spectra Lanczos::factorize_from), with the
+    // deflated constant vector u0 in every projection.
+    //   reorth 1: three-term recurrence f' = w - alpha v_i - beta_i v_{i-1}
+    //             (alpha from the SpMV's fused partials), then ONE classical
+    //             Gram-Schmidt pass f = f' - V (V^T f'): 2 passes over V;
+    //   reorth 2: CGS2 from w (twice is enough): 4 passes over V.
+    // H(i,i) / H(i-1,i) take the projections as corrections (Spectra's
+    // H += V^T f after its re-orthogonalisation).
+    int reorth = 1;
     void factorize(int k) {
         double* fn2 = c->fn2.as<double>();
         for (int i = k; i < m; ++i) {
@@ -305,10 +314,34 @@ struct Lanczos {
             const bool timed = time_spmv && size_t(2 * (i - k) + 1) < ev.size();
             if (timed) HIPCHK(hipEventRecord(ev[size_t(2 * (i - k))], s));
             ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                          c->val.as<double>(), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i), c->block_nnz);
+                          c->val.as<double>(), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
+                          reorth == 1 ? c->apart.as<double>() : nullptr, c->block_nnz);
             if (timed) HIPCHK(hipEventRecord(ev[size_t(2 * (i - k) + 1)], s));
             ++matvecs;
             const int nc = i + 1, tot = nc + has_u0;
+            if (reorth == 1) {
+                double* a3 = c->scal.as<double>() + 2;
+                const double* bov = c->bov.as<double>() + i;
+                if (c->nranks == 1) {
+                    ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
+                                        i > 0 ? col(i - 1) : nullptr, fn2 + i, bov, c->f.as<double>());
+                } else {
+                    ek::dev::finalize_step(s, c->apart.as<double>(), c->nrb_spmv, a3, nullptr, nullptr, -1, nullptr,
+                                           nullptr);
+                    allreduce(c, a3, 1);
+                    ek::dev::three_term(s, ldv, nullptr, 0, a3, c->w.as<double>(), col(i),
+                                        i > 0 ? col(i - 1) : nullptr, fn2 + i, bov, c->f.as<double>());
+                }
+                ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
+                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot, c->h2.as<double>());
+                allreduce(c, c->h2.as<double>(), size_t(tot));
+                ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
+                                c->f.as<double>(), c->npart.as<double>());
+                ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + i + 1, nullptr, c->h2.as<double>(), i,
+                                       c->alpha.as<double>(), c->offd.as<double>(), a3, fn2 + i, bov);
+                allreduce(c, fn2 + i + 1, 1);
+                continue;
+            }
             ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), c->part.as<double>());
             ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot, c->h1.as<double>());
             allreduce(c, c->h1.as<double>(), size_t(tot));
@@ -324,6 +357,32 @@ struct Lanczos {
             allreduce(c, fn2 + i + 1, 1);
         }
         HIPCHK(hipGetLastError());
+    }
+
+    // Invariant subspace found at step j1-1 (||f|| collapsed, as on a graph
+    // with several components): continue the sequence from a fresh random
+    // vector orthogonal to V[:, :j1] and u0, with H(j1, j1-1) = 0 — Spectra's
+    // Lanczos::factorize_from restart-on-breakdown.  The vector is generated
+    // over GLOBAL indices so every rank builds the same one.
+    void inject(int j1, int tag) {
+        std::vector<double> h(size_t(ldv), 0.0);
+        uint64_t st = 2654435761ull * uint64_t(tag) % 2147483647ull + 1;
+        for (int64_t g = 0; g < c->row0 + c->nrows; ++g) {
+            st = (st * 48271ull) % 2147483647ull;
+            if (g >= c->row0) h[size_t(g - c->row0)] = double(st) / 2147483647.0 - 0.5;
+        }
+        double* f = c->f.as<double>();
+        HIPCHK(hipMemcpyAsync(f, h.data(), size_t(ldv) * 8, hipMemcpyHostToDevice, s));
+        for (int pass = 0; pass < 2; ++pass) {
+            ek::dev::gemvt(s, ldv, nrb, V(), j1, has_u0, u0val, nreal, f, c->part.as<double>());
+            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, j1 + has_u0, c->h1.as<double>());
+            allreduce(c, c->h1.as<double>(), size_t(j1 + has_u0));
+            ek::dev::update(s, ldv, V(), j1, has_u0, u0val, nreal, c->h1.as<double>(), f, f,
+                            pass == 1 ? c->npart.as<double>() : nullptr);
+        }
+        reduce_scalar(c->fn2.as<double>() + j1);
+        HIPCHK(hipMemsetAsync(c->bov.as<double>() + j1, 0, 8, s));  // beta_j1 = +0.0
+        HIPCHK(hipStreamSynchronize(s));                             // h is a host temporary
     }
 
     void collect_spmv_times(int k) {
@@ -372,6 +431,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.nreal = int(c->nrows);
     L.u0val = 1.0 / std::sqrt(double(n));
     L.time_spmv = o.time_spmv != 0;
+    L.reorth = o.reorth == 2 ? 2 : 1;
     hipStream_t s = c->stream;
 
     const size_t ldv = size_t(L.ldv);
@@ -386,7 +446,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     c->alpha.ensure(size_t(m + 1) * 8);
     c->offd.ensure(size_t(m + 1) * 8);
     c->fn2.ensure(size_t(m + 2) * 8);
+    c->bov.ensure(size_t(m + 2) * 8);
     c->npart.ensure(size_t(L.nub) * 8);
+    c->apart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
     c->Qd.ensure(size_t(m) * size_t(m + 1) * 8);
     c->scal.ensure(64);
     HIPCHK(hipMemsetAsync(c->V.p, 0, c->V.bytes, s));  // padded rows must stay exactly 0
@@ -426,18 +488,36 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
 
     std::vector<double> d(size_t(m), 0.0), e(size_t(m), 0.0), theta(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
     std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
-    int k = 0, restarts = 0, nconv = 0;
+    int k = 0, restarts = 0, nconv = 0, breakdowns = 0;
     bool converged = false;
+    const double beta_eps = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     for (;;) {
-        L.factorize(k);
-        L.collect_spmv_times(k);
-        HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(offd_h.data(), c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(fn2_h.data(), c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        for (int i = k; i < m; ++i) {
-            d[size_t(i)] = alpha_h[size_t(i)];
-            if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
+        HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
+        for (int from = k;;) {
+            L.factorize(from);
+            L.collect_spmv_times(from);
+            HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(offd_h.data(), c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(fn2_h.data(), c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (int i = from; i < m; ++i) {
+                d[size_t(i)] = alpha_h[size_t(i)];
+                if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
+            }
+            double anorm = 1.0;
+            for (int i = 0; i < m; ++i)
+                anorm = std::max(anorm, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
+            int j1 = -1;
+            for (int i = from + 1; i < m; ++i)
+                if (!(std::sqrt(std::max(0.0, fn2_h[size_t(i)])) > beta_eps * anorm)) {
+                    j1 = i;
+                    break;
+                }
+            if (j1 < 0) break;
+            if (trace) std::fprintf(stderr, "[lanczos] breakdown at step %d (|f|^2=%.3e)\n", j1, fn2_h[size_t(j1)]);
+            if (++breakdowns > 4 * m) ek::fail(EK_ENOCONV, "Lanczos: repeated breakdown");
+            L.inject(j1, breakdowns);
+            from = j1;
         }
         if (!ek::tridiag_eig(m, d.data(), e.data(), theta.data(), zl.data(), nullptr))
             ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
@@ -496,7 +576,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     HIPCHK(hipMemcpyAsync(v.data(), xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
     // residual ||L x - lambda x|| on the owned rows
     ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                  c->val.as<double>(), xg, c->w.as<double>(), nullptr, nullptr, nullptr, c->block_nnz);
+                  c->val.as<double>(), xg, c->w.as<double>(), nullptr, nullptr, nullptr, nullptr, c->block_nnz);
     std::vector<double> y(size_t(std::max<int64_t>(c->nrows, 1)));
     if (c->nrows) HIPCHK(hipMemcpyAsync(y.data(), c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

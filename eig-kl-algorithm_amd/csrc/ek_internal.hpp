@@ -75,10 +75,12 @@ namespace dev {
 constexpr int SPMV_THREADS = 256;
 std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int block_nnz);
 // y[r] = scale * sum_c L[r,c] x[c]; scale = 1/sqrt(*fn2) when fn2 != null else 1.
-// If vcol != null also writes vcol[r] = f[r] * scale (Lanczos basis column).
-void spmv(hipStream_t s, int nblocks, const int32_t* rb, const int32_t* rowptr, const int32_t* col,
+// If vcol != null also writes vcol[r] = f[r] * scale (Lanczos basis column), and
+// if apart != null the per-block partials of vcol . y (one per block).
+// desc: 4 ints per block {row0, nrows, nnz0, cnt} from spmv_row_blocks.
+void spmv(hipStream_t s, int nblocks, const int32_t* desc, const int32_t* rowptr, const int32_t* col,
           const double* val, const double* x, double* y, const double* fn2, const double* f, double* vcol,
-          int block_nnz);
+          double* apart, int block_nnz);
 
 // kernels_lanczos.hip
 constexpr int GT_ROWS = 1024;  // rows per gemv-T block; ldv is a multiple of this
@@ -94,10 +96,17 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart);
-// fn2_out[0] = sum(npart[0:nb]); if step >= 0: alpha[step] = h1[step]+h2[step],
-// offd[step] = h1[step-1]+h2[step-1]
+// fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
+// alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
+// alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]
 void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1,
-                   const double* h2, int step, double* alpha, double* offd);
+                   const double* h2, int step, double* alpha, double* offd, const double* a3 = nullptr,
+                   const double* fn2_i = nullptr, const double* bov_i = nullptr);
+// fp = w - alpha vi - beta_i vim1 (vim1 may be null), beta_i = sqrt(*fn2_i) unless the override
+// *bov_i is not NaN (0 after an injected restart vector); alpha = sum(apart[0:nparts]) when
+// nparts > 0 (written to *alpha_io), else read from *alpha_io
+void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,
+                const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp);
 // out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device)
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out);
 // f = f*sigma + x*hk ; per-block sum of f^2 -> npart

@@ -108,21 +108,68 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     }
 }
 
+// fn2_out = sum(npart); H(step,step) / H(step-1,step) from the projections:
+// CGS2 (a3 == null): h1 + h2 of both passes; three-term (a3 != null):
+// alpha + h2[step] and beta_step + h2[step-1] (Spectra's H += Vf correction).
 __global__ __launch_bounds__(256) void k_finalize_step(const double* __restrict__ npart, int nb,
                                                        double* __restrict__ fn2_out, const double* __restrict__ h1,
                                                        const double* __restrict__ h2, int step,
-                                                       double* __restrict__ alpha, double* __restrict__ offd) {
+                                                       double* __restrict__ alpha, double* __restrict__ offd,
+                                                       const double* __restrict__ a3, const double* __restrict__ beff_i,
+                                                       const double* __restrict__ bov_i) {
     __shared__ double lds4[4];
     double s = 0.0;
     for (int i = threadIdx.x; i < nb; i += 256) s += npart[i];
     s = block_sum256(s, lds4);
     if (threadIdx.x == 0) {
         fn2_out[0] = s;
-        if (step >= 0) {
+        if (step >= 0 && a3) {
+            alpha[step] = *a3 + h2[step];
+            if (step > 0) offd[step] = (isnan(bov_i[0]) ? sqrt(beff_i[0]) : bov_i[0]) + h2[step - 1];
+        } else if (step >= 0) {
             alpha[step] = h1[step] + h2[step];
             if (step > 0) offd[step] = h1[step - 1] + h2[step - 1];
         }
     }
+}
+
+// Three-term recurrence f' = w - alpha v_i - beta_i v_{i-1}, alpha = sum of the
+// SpMV's per-block partials (nparts > 0: every block reduces them itself, in
+// the same fixed order, so no extra launch; nparts == 0: alpha precomputed,
+// e.g. all-reduced across ranks).  Block 0 publishes alpha for the finalize.
+__global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ apart, int nparts,
+                                                    double* __restrict__ alpha_io, const double* __restrict__ w,
+                                                    const double* __restrict__ vi, const double* __restrict__ vim1,
+                                                    const double* __restrict__ fn2_i, const double* __restrict__ bov_i,
+                                                    double* __restrict__ fp) {
+    __shared__ double lds4[4];
+    __shared__ double s_alpha;
+    if (nparts > 0) {
+        double s = 0.0;
+        for (int i = threadIdx.x; i < nparts; i += 256) s += apart[i];
+        s = block_sum256(s, lds4);
+        if (threadIdx.x == 0) {
+            s_alpha = s;
+            if (blockIdx.x == 0) *alpha_io = s;
+        }
+    } else if (threadIdx.x == 0) {
+        s_alpha = *alpha_io;
+    }
+    __syncthreads();
+    // beta_i = ||f_i||, or 0 after an injected restart vector (override not NaN)
+    const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
+    const double a = s_alpha;
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    double2 x = *reinterpret_cast<const double2*>(w + r);
+    const double2 v = *reinterpret_cast<const double2*>(vi + r);
+    x.x -= a * v.x;
+    x.y -= a * v.y;
+    if (vim1) {
+        const double2 u = *reinterpret_cast<const double2*>(vim1 + r);
+        x.x -= b * u.x;
+        x.y -= b * u.y;
+    }
+    *reinterpret_cast<double2*>(fp + r) = x;
 }
 
 // out[:, j] = sum_{i<m} V[:, i] Q[i, j], j < kk; grid (ldv/512, ceil(kk/8)).
@@ -206,8 +253,15 @@ void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, doub
 }
 
 void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1, const double* h2,
-                   int step, double* alpha, double* offd) {
-    hipLaunchKernelGGL(k_finalize_step, dim3(1), dim3(256), 0, s, npart, nb, fn2_out, h1, h2, step, alpha, offd);
+                   int step, double* alpha, double* offd, const double* a3, const double* fn2_i, const double* bov_i) {
+    hipLaunchKernelGGL(k_finalize_step, dim3(1), dim3(256), 0, s, npart, nb, fn2_out, h1, h2, step, alpha, offd, a3,
+                       fn2_i, bov_i);
+}
+
+void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,
+                const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp) {
+    hipLaunchKernelGGL(k_three_term, dim3(ldv / UPD_ROWS), dim3(256), 0, s, apart, nparts, alpha_io, w, vi, vim1, fn2_i,
+                       bov_i, fp);
 }
 
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out) {

@@ -134,6 +134,8 @@ typedef struct {
     int32_t deflate;    /* 1 (default): deflate the constant null vector, nev=1;
                            0: Spectra-equivalent nev=2, Fiedler = 2nd smallest */
     int32_t time_spmv;  /* 1: bracket every SpMV launch with HIP events (stats) */
+    int32_t reorth;     /* 1 (default): three-term recurrence + one full classical
+                           Gram-Schmidt pass; 2: CGS2 (twice) from the matvec */
 } ek_lanczos_opts;
 
 typedef struct {

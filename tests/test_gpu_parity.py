@@ -131,12 +131,12 @@ def _fiedler_parity(name, lam, v, lam_ref, med_ref, bits_ref, v_ref, ek):
 
 
 @pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
-@pytest.mark.parametrize("deflate", [True, False])
-def test_lanczos_golden(ek, ctx, name, deflate):
+@pytest.mark.parametrize("deflate,reorth", [(True, 1), (False, 1), (True, 2), (False, 2)])
+def test_lanczos_golden(ek, ctx, name, deflate, reorth):
     h = ek.Hypergraph.read(circuit_path(name))
     L = h.laplacian()
     ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
-    lam, v, st = ctx.lanczos_fiedler(deflate=deflate)
+    lam, v, st = ctx.lanczos_fiedler(deflate=deflate, reorth=reorth)
     assert st["converged"] and st["residual"] < 1e-9
     lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
     _fiedler_parity(name, lam, v, lam_ref, med_ref, bits_ref, v_ref, ek)
