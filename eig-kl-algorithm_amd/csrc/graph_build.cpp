@@ -22,7 +22,7 @@ namespace ek {
 // rehashes to 13 (_M_next_bkt(12) via the small-size table), after that a
 // rehash to the smallest listed prime >= 2B happens when the element count
 // reaches B.  Checked against the live libstdc++ by
-// tests/test_host_logic.py::test_bucket_growth_matches_libstdcxx.
+// tests/test_host_logic.py::test_kl_row_order_large_rows (live libstdc++ rows).
 static const uint64_t kBucketSeq[] = {13,     29,     59,      127,     257,     541,     1109,
                                       2357,   5087,   10273,   20753,   42043,   85229,   172933,
                                       351061, 712697, 1447153, 2938679, 5967347, 12117689};

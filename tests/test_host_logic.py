@@ -1,0 +1,202 @@
+"""Host-side logic of the product (no GPU): .hgr ingest, the two clique
+expansions, the libstdc++ row-order emulation, the generator, EIG-file I/O,
+median split and the row shard map.  Checked against the oracle, the live
+libstdc++ container and the reference's shipped data files."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import CIRCUITS, REPO, circuit_path, eig_path
+
+HELPER_SRC = os.path.join(REPO, "tests", "helpers", "umap_rows.cpp")
+
+
+@pytest.fixture(scope="session")
+def umap_rows(tmp_path_factory):
+    """Build the live-libstdc++ row dumper (test helper) once per session."""
+    exe = str(tmp_path_factory.mktemp("helper") / "umap_rows")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", HELPER_SRC, "-o", exe])
+    return exe
+
+
+def _forward_rows(G):
+    return [G.col[G.rowptr[r]: G.rowptr[r] + G.nfwd[r]] for r in range(G.nrows)]
+
+
+def _live_rows(exe, hgr_path):
+    out = subprocess.run([exe, "rows", hgr_path], check=True, capture_output=True, text=True).stdout
+    return [np.array(ln.split(), np.int64) for ln in out.split("\n")[:-1]]
+
+
+# ------------------------------------------------------------ K2 row order
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
+def test_kl_row_order_matches_libstdcxx(ek, umap_rows, name):
+    """Forward entries of every row in the order cKL's unordered_map iterates them
+     — the summation order of connections(), cKL.cpp:225-251."""
+    G = ek.Hypergraph.read(circuit_path(name)).kl_graph()
+    live = _live_rows(umap_rows, circuit_path(name))
+    mine = _forward_rows(G)
+    assert len(live) == len(mine)
+    bad = [r for r in range(len(live)) if not np.array_equal(live[r], mine[r])]
+    assert not bad, f"{len(bad)} rows differ, first {bad[:5]}"
+
+
+def test_kl_row_order_large_rows(ek, umap_rows, tmp_path):
+    """Rows whose key count crosses many rehash thresholds (13 .. 2357 buckets)."""
+    rng = np.random.default_rng(5)
+    n = 3000
+    nets = [np.sort(rng.choice(n, size=k, replace=False)) for k in (2100, 700, 300, 40)]
+    nets += [np.sort(rng.choice(n, size=2, replace=False)) for _ in range(4000)]
+    net_ptr = np.concatenate([[0], np.cumsum([len(e) for e in nets])]).astype(np.int64)
+    pins = np.concatenate(nets).astype(np.int32)
+    h = ek.Hypergraph.from_pins(n, net_ptr, pins)
+    path = str(tmp_path / "big.hgr")
+    h.write(path)
+    mine = _forward_rows(h.kl_graph())
+    live = _live_rows(umap_rows, path)
+    assert max(len(r) for r in live) > 2000
+    bad = [r for r in range(n) if not np.array_equal(live[r], mine[r])]
+    assert not bad, f"{len(bad)} rows differ, first {bad[:5]}"
+
+
+def test_bucket_growth_is_libstdcxx(oracle, umap_rows):
+    """The oracle's bucket sequence and the helper agree (both the live container)."""
+    out = subprocess.run([umap_rows, "buckets", "6000"], check=True, capture_output=True, text=True).stdout
+    live = np.array(out.split(), np.int64)
+    assert np.array_equal(live, oracle.bucket_growth(6000))
+    assert sorted(set(live.tolist()))[:6] == [13, 29, 59, 127, 257, 541]
+
+
+# ------------------------------------------------------ clique expansions
+@pytest.mark.parametrize("name", CIRCUITS)
+def test_kl_graph_matches_oracle(ek, oracle, name):
+    G = ek.Hypergraph.read(circuit_path(name)).kl_graph()
+    rp, col, w, nf = oracle.Graph.read(circuit_path(name)).kl_csr()
+    assert np.array_equal(G.rowptr, rp) and np.array_equal(G.col, col) and np.array_equal(G.nfwd, nf)
+    assert np.array_equal(G.val.view(np.uint32), w.view(np.uint32))  # fp32 bit-exact (cKL.cpp:117-128)
+
+
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
+def test_laplacian_matches_oracle(ek, oracle, name):
+    L = ek.Hypergraph.read(circuit_path(name)).laplacian()
+    rp, col, val = oracle.Graph.read(circuit_path(name)).laplacian()
+    assert np.array_equal(L.rowptr, rp) and np.array_equal(L.col, col)
+    assert np.allclose(L.val, val, rtol=1e-14, atol=0)
+    # structure: symmetric, zero row sums, diagonal = -(off-diagonal row sum) (cEIG.cpp:86-133)
+    n = L.nrows
+    rows = np.repeat(np.arange(n), np.diff(L.rowptr))
+    A = {(int(r), int(c)): v for r, c, v in zip(rows[:5000], L.col[:5000], L.val[:5000])}
+    for (r, c), v in list(A.items())[:500]:
+        lo, hi = L.rowptr[c], L.rowptr[c + 1]
+        j = lo + np.searchsorted(L.col[lo:hi], r)
+        assert L.col[j] == r and L.val[j] == v
+    assert np.abs(np.add.reduceat(L.val, L.rowptr[:-1])).max() < 1e-12
+
+
+def test_laplacian_synthetic_properties(ek):
+    h = ek.Hypergraph.generate(0.05, 2)
+    L = h.laplacian()
+    net_ptr, pins = h.pins()
+    k = np.diff(net_ptr)
+    # sum of all off-diagonal weights = sum over nets of k(k-1) * 2/k
+    off = L.val[L.col != np.repeat(np.arange(L.nrows), np.diff(L.rowptr))]
+    assert abs(-off.sum() - float((2.0 * (k - 1))[k >= 2].sum())) < 1e-6
+    for r in range(0, L.nrows, 101):  # ascending columns within a row
+        assert np.all(np.diff(L.col[L.rowptr[r]: L.rowptr[r + 1]]) > 0)
+
+
+# ------------------------------------------------------------- generator
+def test_generator_shape_and_determinism(ek):
+    a = ek.Hypergraph.generate(0.05, 11)
+    b = ek.Hypergraph.generate(0.05, 11)
+    c = ek.Hypergraph.generate(0.05, 12)
+    nets, nodes, npins = a.dims()
+    assert (nets, nodes) == (int(210613 * 0.05), int(201920 * 0.05))  # circuit_generator.py:41-44
+    pa, pb, pc = a.pins(), b.pins(), c.pins()
+    assert np.array_equal(pa[0], pb[0]) and np.array_equal(pa[1], pb[1])
+    assert not np.array_equal(pa[1][:1000], pc[1][:1000])
+    net_ptr, pins = pa
+    k = np.diff(net_ptr)
+    assert pins.min() >= 0 and pins.max() < nodes
+    for e in range(0, nets, 97):  # distinct, sorted pins (random.sample + sort)
+        s = pins[net_ptr[e]: net_ptr[e + 1]]
+        assert np.all(np.diff(s) > 0)
+    mix = {2: .84, 3: .02, 4: .06, 5: .02, 6: .04, 8: .02}  # circuit_generator.py:12-19
+    assert set(np.unique(k).tolist()) <= set(mix)
+    for size, frac in mix.items():
+        assert abs(np.mean(k == size) - frac) < 0.015, size
+
+
+def test_hgr_write_read_roundtrip(ek, tmp_path):
+    h = ek.Hypergraph.generate(0.02, 4)
+    p = str(tmp_path / "syn.hgr")
+    h.write(p)
+    g = ek.Hypergraph.read(p)
+    assert g.dims() == h.dims()
+    for x, y in zip(g.pins(), h.pins()):
+        assert np.array_equal(x, y)
+    head = open(p).readline().split()
+    assert head == [str(h.nets), str(h.nodes)]
+
+
+def test_hgr_read_errors(ek, tmp_path):
+    with pytest.raises(ek.EKError) as e:
+        ek.Hypergraph.read(str(tmp_path / "missing.hgr"))
+    assert e.value.code == ek.EK_EIO
+    bad = tmp_path / "bad.hgr"
+    bad.write_text("2 3\n1 2\n3 9\n")  # pin 9 > 3 nodes
+    with pytest.raises(ek.EKError) as e:
+        ek.Hypergraph.read(str(bad))
+    assert e.value.code == ek.EK_EINVAL
+
+
+# ------------------------------------------------------ EIG file + median
+@pytest.mark.parametrize("name", CIRCUITS)
+def test_eig_read_matches_reference_reader(ek, oracle, name):
+    n = ek.Hypergraph.read(circuit_path(name)).nodes
+    lam, med, bits, v, o0, o1 = ek.eig_read(eig_path(name), n)
+    lam_r, med_r, bits_r, v_r, o0_r, o1_r = oracle.read_eig_file(eig_path(name))
+    assert lam == lam_r and med == med_r
+    assert np.array_equal(bits, bits_r) and np.array_equal(v, v_r)
+    assert np.array_equal(o0, o0_r) and np.array_equal(o1, o1_r)
+
+
+def test_eig_write_roundtrip_format(ek, tmp_path):
+    rng = np.random.default_rng(1)
+    v = rng.standard_normal(101)
+    med, bits = ek.median_split(v)
+    p = str(tmp_path / "x_out.txt")
+    ek.eig_write(p, 0.125, med, bits, v)
+    lines = open(p).read().splitlines()
+    assert lines[0] == "0.125" and float(lines[1]) == float(f"{med:.12g}")
+    assert lines[2] == f"0\t{bits[0]}\t{v[0]:.12g}"  # cEIG.cpp:213-220
+    lam, med2, bits2, v2, o0, o1 = ek.eig_read(p, 101)
+    assert np.array_equal(bits2, bits) and np.allclose(v2, v, rtol=1e-11)
+    assert len(o0) + len(o1) == 101
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 1001])
+def test_median_split_rule(ek, n):
+    rng = np.random.default_rng(n)
+    v = rng.standard_normal(n)
+    v[: n // 3] = v[0]  # ties
+    med, bits = ek.median_split(v)
+    s = np.sort(v)
+    ref = s[n // 2] if n % 2 else (s[(n - 1) // 2] + s[n // 2]) / 2.0  # cEIG.cpp:55-65
+    assert med == ref
+    assert np.array_equal(bits, (ref > v).astype(np.uint8))  # cEIG.cpp:218
+
+
+# ------------------------------------------------------------- shard map
+@pytest.mark.parametrize("n,ranks", [(1000, 3), (201920, 8), (64, 8), (7, 2)])
+def test_shard_rows_tile_the_matrix(ek, n, ranks):
+    covered = 0
+    for r in range(ranks):
+        row0, nrows, nloc = ek.shard_rows(n, ranks, r)
+        assert nloc % 64 == 0 and nrows <= nloc
+        assert row0 == min(n, r * nloc)  # rank-major slices: all-gather lands rows in place
+        assert row0 == covered
+        covered += nrows
+    assert covered == n

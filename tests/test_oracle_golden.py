@@ -1,0 +1,75 @@
+"""Pin the oracle (CPU restatement, oracle/) to the reference's own outputs
+before it is trusted as the checker: the real cKL's results files
+(tests/golden/ref_results, produced by oracle/gen_golden.py from the compiled
+reference), the SURVEY §8c swap-log md5s and known-answer swaps, the derived
+integer net cuts, and the reference's shipped cEIG Fiedler files
+(tests/golden/pre_saved_EIG)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import CIRCUITS, NET_CUTS, SWAP_MD5, circuit_path, compare_results_text, eig_path, ref_results_path
+
+# SURVEY §8c known answers: (swap index, node1, node2, hex gain)
+KAT = {"ibm01": (0, 10028, 11654, "0x1.59999cp+3"), "industry2": (0, 5263, 6568, "0x1.d1451ap+2"),
+       "ibm10": (0, 57282, 5140, "0x1.a9e78cp+3"), "fract": (1, 121, 148, "0x1.2p+1")}
+
+
+@pytest.mark.parametrize("name", CIRCUITS)
+def test_oracle_kl_matches_reference(oracle, name):
+    g = oracle.Graph.read(circuit_path(name))
+    _, _, _, _, o0, o1 = oracle.read_eig_file(eig_path(name))
+    log, res = g.kl(o0, o1)
+    gold = NET_CUTS[name]
+    assert res["iterations"] == gold["iterations"]
+    assert res["best_iter"] == gold["best_iter"]
+    assert res["net_cut_best"] == gold["net_cut_best"] and res["net_cut_final"] == gold["net_cut_final"]
+    assert hashlib.md5(oracle.swap_log_text(log).encode()).hexdigest().startswith(SWAP_MD5[name])
+    i, a, b, gain = KAT[name]
+    assert (int(log["node_left"][i]), int(log["node_right"][i])) == (a, b)
+    assert oracle.c_hexfloat(log["gain"][i]) == gain
+    compare_results_text(oracle.format_results(log, res["initial_cut"]), open(ref_results_path(name)).read())
+
+
+def test_oracle_kl_termination_and_cut_rules(oracle):
+    # fract random split: monotone log, the stop rule floor(log2 n)+5 (cKL.cpp:301-304, 382-389)
+    g = oracle.Graph.read(circuit_path("fract"))
+    n = g.nodes
+    perm = np.random.default_rng(0).permutation(n).astype(np.int32)
+    log, res = g.kl(perm[: n // 2], perm[n // 2:])
+    assert 0 < res["iterations"] <= n // 2
+    limit = int(np.floor(np.log2(n))) + 5
+    tail = 0
+    for gval in log["gain"]:
+        tail = tail + 1 if gval <= 0 else 0
+    assert tail == limit + 1 or res["iterations"] == n // 2
+    cut = res["initial_cut"] - np.cumsum(log["gain"].astype(np.float64))
+    assert np.allclose(cut, log["cut"], rtol=1e-5)
+    assert res["best_cut"] == min(res["initial_cut"], float(log["cut"].min()))
+
+
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
+def test_oracle_lanczos_matches_golden(oracle, name):
+    g = oracle.Graph.read(circuit_path(name))
+    lam, v, st = g.lanczos()
+    assert st["converged"] and st["residual"] < 1e-9
+    lam_r, med_r, bits_r, v_r, _, _ = oracle.read_eig_file(eig_path(name))
+    v = v * np.sign(v @ v_r)
+    assert abs(lam - lam_r) <= 1e-10
+    assert np.abs(v - v_r).max() <= 1e-8
+    s = np.sort(v)
+    n = len(v)
+    med = s[n // 2] if n % 2 else (s[(n - 1) // 2] + s[n // 2]) / 2
+    mask = np.abs(v_r - med_r) > 1e-8
+    assert np.array_equal((med > v).astype(np.uint8)[mask], bits_r[mask])
+
+
+def test_oracle_spmv_is_the_laplacian(oracle):
+    g = oracle.Graph.read(circuit_path("ibm01"))
+    rp, col, val = g.laplacian()
+    x = np.random.default_rng(2).standard_normal(g.nodes)
+    y = g.spmv(x)
+    ref = np.add.reduceat(val * x[col], rp[:-1])
+    assert np.allclose(y, ref, rtol=1e-13, atol=1e-13)
+    assert np.abs(g.spmv(np.ones(g.nodes))).max() < 1e-12
