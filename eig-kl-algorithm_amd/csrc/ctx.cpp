@@ -57,6 +57,7 @@ void upload(DBuf& d, const T* h, size_t n, hipStream_t s) {
 }
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::dev::KL_CHUNK), ek::dev::KL_CHUNK); }
 
 }  // namespace
 
@@ -75,8 +76,8 @@ struct ek_ctx {
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
-        kl_ckey0, kl_ckey1, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
-    bool kl_graph_ready = false, kl_part_ready = false;
+        kl_ckey0, kl_ckey1, kl_aux, kl_seg, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
+    bool kl_graph_ready = false, kl_part_ready = false, kl_seg_ok = false;
     std::vector<int32_t> kl_rowptr_h;  // host copy (row descriptors)
 };
 
@@ -635,6 +636,14 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     upload(c->kl_rowptr, rowptr, size_t(n) + 1, s);
     upload(c->kl_col, col, size_t(nnz), s);
     upload(c->kl_w, w, size_t(nnz), s);
+    // inline neighbour-row segments for the swap loop (128 B per entry; skipped past 32 GB)
+    c->kl_seg_ok = size_t(nnz) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30);
+    if (c->kl_seg_ok) {
+        c->kl_seg.ensure(size_t(std::max<int64_t>(nnz, 1)) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo));
+        ek::dev::kl_build_seg(s, nnz, c->kl_rowptr.as<int32_t>(), c->kl_col.as<int32_t>(), c->kl_w.as<float>(),
+                              c->kl_seg.as<ek::dev::KLInfo>());
+        HIPCHK(hipGetLastError());
+    }
     c->kl_side.ensure(size_t(n));
     c->kl_side_init.ensure(size_t(n));
     c->kl_locked.ensure(size_t(n));
@@ -694,8 +703,9 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
     // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr, rowlen, plist}
     {
         const auto& rp = c->kl_rowptr_h;
-        std::vector<ek::dev::KLInfo> p0(size_t(std::max<int64_t>(n0, 1))), p1(size_t(std::max<int64_t>(n1, 1))),
-            nd(static_cast<size_t>(n));
+        // by-position arrays are padded to whole chunks (zero descriptors, NaN
+        // gains = invalid keys) so the chunk scans load unconditionally
+        std::vector<ek::dev::KLInfo> p0(size_t(chunk_pad(n0))), p1(size_t(chunk_pad(n1))), nd(static_cast<size_t>(n));
         for (int64_t i = 0; i < n0; ++i) {
             const int32_t u = order0[i];
             p0[size_t(i)] = {u, rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], 0};
@@ -709,12 +719,19 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
         upload(c->kl_pinfo0, p0.data(), p0.size(), s);
         upload(c->kl_pinfo1, p1.data(), p1.size(), s);
         upload(c->kl_nd, nd.data(), nd.size(), s);
+        const int64_t nnz = c->kl_rowptr_h[size_t(n)];
+        c->kl_aux.ensure(size_t(std::max<int64_t>(nnz, 1)) * sizeof(ek::dev::KLInfo));
+        ek::dev::kl_build_aux(s, nnz, c->kl_col.as<int32_t>(), c->kl_nd.as<ek::dev::KLInfo>(),
+                              c->kl_aux.as<ek::dev::KLInfo>());
+        HIPCHK(hipGetLastError());
         c->kl_cinfo0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
         c->kl_cinfo1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
         HIPCHK(hipStreamSynchronize(s));  // host staging vectors go out of scope
     }
-    c->kl_gp0.ensure(size_t(std::max<int64_t>(n0, 1)) * 4);
-    c->kl_gp1.ensure(size_t(std::max<int64_t>(n1, 1)) * 4);
+    c->kl_gp0.ensure(size_t(chunk_pad(n0)) * 4);
+    c->kl_gp1.ensure(size_t(chunk_pad(n1)) * 4);
+    HIPCHK(hipMemsetAsync(c->kl_gp0.p, 0xFF, c->kl_gp0.bytes, s));  // NaN padding
+    HIPCHK(hipMemsetAsync(c->kl_gp1.p, 0xFF, c->kl_gp1.bytes, s));
     c->kl_ckey0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
     c->kl_ckey1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
     c->kl_log.ensure(size_t(std::max<int64_t>(1, std::min(n0, n1))) * sizeof(ek_swap));
@@ -747,6 +764,8 @@ ek::dev::KLDev kl_dev(ek_ctx* c) {
     d.nd = c->kl_nd.as<ek::dev::KLInfo>();
     d.cinfo0 = c->kl_cinfo0.as<ek::dev::KLInfo>();
     d.cinfo1 = c->kl_cinfo1.as<ek::dev::KLInfo>();
+    d.aux = c->kl_aux.as<ek::dev::KLInfo>();
+    d.seg = c->kl_seg_ok && !std::getenv("EK_KL_NOSEG") ? c->kl_seg.as<ek::dev::KLInfo>() : nullptr;  // env: A/B
     d.n0 = int(c->kl_n0);
     d.n1 = int(c->kl_n1);
     d.nck0 = int((c->kl_n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK);
@@ -829,14 +848,16 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_best = nets ? int64_t(hc[1]) : -1;
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
-        if (std::getenv("EK_KL_PROF"))
-            std::fprintf(stderr, "[kl] %lld swaps: select %.3f  weight+swap %.3f  gains %.3f  re-key %.3f us/swap\n",
-                         (long long)ho.iterations, ho.prof[0] * 0.01 / std::max<long long>(1, ho.iterations),
-                         ho.prof[1] * 0.01 / std::max<long long>(1, ho.iterations),
-                         ho.prof[2] * 0.01 / std::max<long long>(1, ho.iterations),
-                         ho.prof[3] * 0.01 / std::max<long long>(1, ho.iterations));
-        if (std::getenv("EK_KL_PROF") && ho.prof[5])
-            std::fprintf(stderr, "[kl] in-loop shader clock %.0f MHz\n", double(ho.prof[4]) / (double(ho.prof[5]) * 0.01));
+        if (std::getenv("EK_KL_PROF")) {
+            static const char* names[8] = {"select", "swap", "G1-desc", "G1-sum", "G1-key", "bar1",
+                                           "G2", "bar2"};
+            std::fprintf(stderr, "[kl] %lld swaps, us/swap:", (long long)ho.iterations);
+            for (int i = 0; i < 8; ++i)
+                std::fprintf(stderr, " %s %.3f", names[i], ho.prof[i] * 0.01 / std::max<long long>(1, ho.iterations));
+            std::fprintf(stderr, "\n");
+            if (ho.prof[9])
+                std::fprintf(stderr, "[kl] in-loop shader clock %.0f MHz\n", double(ho.prof[8]) / (double(ho.prof[9]) * 0.01));
+        }
         res->total_ms = double(loop_ms) + double(prep_ms);
     }
     return EK_OK;

@@ -146,7 +146,13 @@ struct KLDev {
     const KLInfo* nd = nullptr;
     KLInfo* cinfo0 = nullptr;
     KLInfo* cinfo1 = nullptr;
+    // per CSR entry p: the neighbour's descriptor {col[p], rowptr, rowlen, plist}
+    const KLInfo* aux = nullptr;
+    // per CSR entry p: the first 16 {col, w} entries of row col[p], 8 x 16 B
+    // (KL_SEG_LANES lanes each load one); null when it would not fit
+    const KLInfo* seg = nullptr;
 };
+constexpr int KL_SEG_LANES = 8;
 constexpr int KL_ITEM_CAP = 1024;  // affected rows whose new key/descriptor are kept in LDS
 // LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
 // chunk winners on chip (0 when they do not fit: global-state mode).
@@ -156,10 +162,13 @@ struct KLOut {
     long long best_iter;
     float initial_cut, best_cut, final_cut;
     unsigned int status;
-    unsigned long long prof[6];  // EK_KL_PROF: 100 MHz ticks in select / weight+swap / gains / re-key;
-                                 // [4] shader cycles, [5] 100 MHz ticks of the whole loop
+    unsigned long long prof[10];  // EK_KL_PROF: [0..7] 100 MHz ticks per loop phase (thread 0's view),
+                                  // [8] shader cycles, [9] 100 MHz ticks of the whole loop
 };
 void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk keys
+// aux[p] = {col[p], nd[col[p]].{rowptr, len, plist}} for p < nnz (after the partition is set)
+void kl_build_aux(hipStream_t s, int64_t nnz, const int32_t* col, const KLInfo* nd, KLInfo* aux);
+void kl_build_seg(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* w, KLInfo* seg);
 void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out);
 // sides_out = side_init with the first `count` swaps of `log` applied (count on device: *best or *iters)
 void kl_replay(hipStream_t s, int n, const uint8_t* side_init, const ek_swap* log, const long long* count,

@@ -112,17 +112,19 @@ __device__ __forceinline__ float row_gain(const int32_t* __restrict__ rowptr, co
     return external - internal;
 }
 
-// best key of 256 consecutive positions of one remain[] list (gains by position)
-__device__ __forceinline__ u64 chunk_key(const float* __restrict__ gp, int ns, int s, int c, int lane) {
+// best key of 256 consecutive positions of one remain[] list (gains by
+// position).  The gain arrays are padded with NaN (invalid key) to a whole
+// number of chunks, so every load is unconditional and all are in flight at once.
+__device__ __forceinline__ u64 chunk_key(const float* __restrict__ gp, int s, int c, int lane) {
+    float g[KL_CHUNK / 64];
+#pragma unroll
+    for (int q = 0; q < KL_CHUNK / 64; ++q) g[q] = gp[c * KL_CHUNK + q * 64 + lane];
     u64 k = 0ull;
 #pragma unroll
     for (int q = 0; q < KL_CHUNK / 64; ++q) {
         const int p = c * KL_CHUNK + q * 64 + lane;
-        if (p < ns) {
-            const float g = gp[p];
-            const u64 kk = s ? key_min(g, p) : key_max(g, p);
-            k = kk > k ? kk : k;
-        }
+        const u64 kk = s ? key_min(g[q], p) : key_max(g[q], p);
+        k = kk > k ? kk : k;
     }
     return wave_max_u64(k);
 }
@@ -162,21 +164,25 @@ __global__ __launch_bounds__(256) void k_cut_final(KLDev d, int nb) {
 // descriptors are both read by position, so the winner needs no dependent
 // load.  Returns the key in every lane; the winner lane (or lane 0 for an
 // all-invalid chunk) has *mine = true and its descriptor in *info.
-__device__ __forceinline__ u64 chunk_best(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int ns,
-                                          int s, int c, int lane, KLInfo* info, bool* mine) {
+__device__ __forceinline__ u64 chunk_best(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
+                                          int c, int lane, KLInfo* info, bool* mine) {
+    float g[KL_CHUNK / 64];
+    int4 pi[KL_CHUNK / 64];
+#pragma unroll
+    for (int q = 0; q < KL_CHUNK / 64; ++q) {  // padded arrays: unconditional, all in flight
+        const int p = c * KL_CHUNK + q * 64 + lane;
+        g[q] = gp[p];
+        pi[q] = *reinterpret_cast<const int4*>(pinfo + p);
+    }
     u64 k = 0ull;
     int4 bi = make_int4(0, 0, 0, 0);
 #pragma unroll
     for (int q = 0; q < KL_CHUNK / 64; ++q) {
         const int p = c * KL_CHUNK + q * 64 + lane;
-        if (p < ns) {
-            const float g = gp[p];
-            const int4 pi = *reinterpret_cast<const int4*>(pinfo + p);
-            const u64 kk = s ? key_min(g, p) : key_max(g, p);
-            if (kk > k) {
-                k = kk;
-                bi = pi;
-            }
+        const u64 kk = s ? key_min(g[q], p) : key_max(g[q], p);
+        if (kk > k) {
+            k = kk;
+            bi = pi[q];
         }
     }
     const u64 m = wave_max_u64(k);
@@ -196,21 +202,31 @@ __global__ __launch_bounds__(256) void k_chunk_init(KLDev d) {
     if (d.pinfo0) {
         KLInfo info;
         bool mine;
-        const u64 k = s ? chunk_best(d.gp1, d.pinfo1, d.n1, 1, c, lane, &info, &mine)
-                        : chunk_best(d.gp0, d.pinfo0, d.n0, 0, c, lane, &info, &mine);
+        const u64 k = s ? chunk_best(d.gp1, d.pinfo1, 1, c, lane, &info, &mine)
+                        : chunk_best(d.gp0, d.pinfo0, 0, c, lane, &info, &mine);
         if (mine) {
             (s ? d.ckey1 : d.ckey0)[c] = k;
             (s ? d.cinfo1 : d.cinfo0)[c] = info;
         }
     } else {
-        const u64 k = s ? chunk_key(d.gp1, d.n1, 1, c, lane) : chunk_key(d.gp0, d.n0, 0, c, lane);
+        const u64 k = s ? chunk_key(d.gp1, 1, c, lane) : chunk_key(d.gp0, 0, c, lane);
         if (lane == 0) (s ? d.ckey1 : d.ckey0)[c] = k;
     }
 }
 
+// chunk-key arrays the selection reads are padded with zero keys to whole
+// SEL_UNROLL*64 blocks (both lists to the same count), so it issues all of a
+// lane's reads before the first compare
+constexpr int KL_SEL_UNROLL = 8;
+__host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
+    const int m = nck0 > nck1 ? nck0 : nck1;
+    return (m + KL_SEL_UNROLL * 64 - 1) / (KL_SEL_UNROLL * 64) * (KL_SEL_UNROLL * 64);
+}
+
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
-    const size_t b = (size_t(d.nck0) + size_t(d.nck1)) * (sizeof(KLInfo) + 8 + 8 + 4 + 4) +
+    const size_t b = (size_t(d.nck0) + size_t(d.nck1)) * (sizeof(KLInfo) + 8 + 4 + 4) +
+                     2 * size_t(kl_sel_pad(d.nck0, d.nck1)) * 8 +
                      size_t(KL_ITEM_CAP) * (sizeof(KLInfo) + 8 + 4) + 16 + 2 * words * 4 + 64;
     return b <= 152 * 1024 ? b : 0;
 }
@@ -255,14 +271,16 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     constexpr int NW = KL_LOOP_THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nckp = kl_sel_pad(d.nck0, d.nck1);
+    const bool wlead = tid == (NW - 1) * 64;  // owns the loop-carried scalars (cut, best, stop counter)
     const int words = (d.n + 31) / 32;
     // LDS carve (kl_loop_lds_bytes): 16-B records first, then 8-B, then 4-B
     KLInfo* ci0 = reinterpret_cast<KLInfo*>(smem);  // chunk winners' descriptors
     KLInfo* ci1 = ci0 + d.nck0;
     KLInfo* it_info = ci1 + d.nck1;                   // per affected row: its descriptor
     u64* ck0 = reinterpret_cast<u64*>(it_info + KL_ITEM_CAP);  // chunk keys (read by the selection)
-    u64* ck1 = ck0 + d.nck0;
-    u64* ckn0 = ck1 + d.nck1;  // shadow keys: G1 merges risen keys here, G2 publishes them to ck
+    u64* ck1 = ck0 + nckp;     // (both padded to nckp with zero keys)
+    u64* ckn0 = ck1 + nckp;    // shadow keys: G1 merges risen keys here, G2 publishes them to ck
     u64* ckn1 = ckn0 + d.nck0;
     u64* it_key = ckn1 + d.nck1;                                // per affected row: its new key
     int* dtag0 = reinterpret_cast<int*>(it_key + KL_ITEM_CAP);  // iteration that tagged a rescan
@@ -273,13 +291,17 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     int* s_stop = it_cs + KL_ITEM_CAP;                         // [2], by iteration parity
     uint32_t* s_side = reinterpret_cast<uint32_t*>(s_stop + 4);
     uint32_t* s_lock = s_side + words;
+    for (int i = tid; i < nckp; i += KL_LOOP_THREADS) {
+        ck0[i] = i < d.nck0 ? d.ckey0[i] : 0ull;
+        ck1[i] = i < d.nck1 ? d.ckey1[i] : 0ull;
+    }
     for (int i = tid; i < d.nck0; i += KL_LOOP_THREADS) {
-        ck0[i] = ckn0[i] = d.ckey0[i];
+        ckn0[i] = d.ckey0[i];
         ci0[i] = d.cinfo0[i];
         dtag0[i] = ctag0[i] = -1;
     }
     for (int i = tid; i < d.nck1; i += KL_LOOP_THREADS) {
-        ck1[i] = ckn1[i] = d.ckey1[i];
+        ckn1[i] = d.ckey1[i];
         ci1[i] = d.cinfo1[i];
         dtag1[i] = ctag1[i] = -1;
     }
@@ -293,7 +315,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     float cut = *d.cut0, best = cut;  // loop-carried scalars: thread 0 only
     long long best_it = 0, it = 0;
     unsigned term = 0;
-    unsigned long long tph[4] = {0, 0, 0, 0}, tstamp = 0;  // diagnostic build only (PROF)
+    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tstamp = 0;  // diagnostic build only (PROF)
     const unsigned long long c_start = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long r_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
     auto stamp = [&](int ph) {
@@ -308,9 +330,22 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     for (;; ++it) {
         stamp(-1);
         // S. selection (cKL.cpp:341-355), redundantly in every wave
+        // all of a lane's key reads are issued before the first compare (a
+        // rolled loop would pay one LDS round trip per 64 chunks)
         u64 k0 = 0ull, k1 = 0ull;
-        for (int c = lane; c < d.nck0; c += 64) k0 = ck0[c] > k0 ? ck0[c] : k0;
-        for (int c = lane; c < d.nck1; c += 64) k1 = ck1[c] > k1 ? ck1[c] : k1;
+        for (int c0 = 0; c0 < nckp; c0 += KL_SEL_UNROLL * 64) {
+            u64 a[KL_SEL_UNROLL], b[KL_SEL_UNROLL];
+#pragma unroll
+            for (int j = 0; j < KL_SEL_UNROLL; ++j) {
+                a[j] = ck0[c0 + j * 64 + lane];
+                b[j] = ck1[c0 + j * 64 + lane];
+            }
+#pragma unroll
+            for (int j = 0; j < KL_SEL_UNROLL; ++j) {
+                k0 = a[j] > k0 ? a[j] : k0;
+                k1 = b[j] > k1 ? b[j] : k1;
+            }
+        }
         k0 = wave_max_u64(k0);
         k1 = wave_max_u64(k1);
         if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
@@ -327,7 +362,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
             atomicOr(&s_lock[B >> 5], 1u << (B & 31));
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        if (wv == 0) {  // w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
+        if (wv == NW - 1) {  // w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386);
+                             // the last wave, so the gain items (from wave 0 up) start at once
             float gA = 0.f, gB = 0.f;
             if (lane == 0) {
                 gA = d.gp0[posA];
@@ -374,36 +410,85 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
         //     max(old key, risen keys) is exact for untagged chunks.
         const int tot = la + lb;
         const int tag = int(it);
+        // one lane per affected row: the neighbour's descriptor {node,
+        // rowptr, len, plist} (aux) and its first 16 {col, w} entries (seg)
+        // are both addressed by the CSR position alone, so every load of the
+        // row is issued at once; the sums run strictly in row order, the
+        // zero-weight padding of short segments adds exact zeros
         for (int i = tid; i < tot; i += KL_LOOP_THREADS) {
-            const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
-            int cs = -1;
-            u64 kn = 0ull;
-            KLInfo inf{0, 0, 0, 0};
-            if (!((s_lock[u >> 5] >> (u & 31)) & 1u)) {
-                const int4 nd = *reinterpret_cast<const int4*>(d.nd + u);  // {rowptr, len, plist}
-                const float g = row_gain_lds(d.col, d.w, s_side, nd.x, nd.y);
-                const uint32_t pl = uint32_t(nd.z);
-                const int s = int(pl >> 31), p = int(pl & 0x7fffffffu), c = p / KL_CHUNK;
-                (s ? d.gp1 : d.gp0)[p] = g;
-                kn = s ? key_min(g, p) : key_max(g, p);
-                const u64 K = (s ? ck1 : ck0)[c];  // stable during the iteration (other waves may still select)
-                if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(p) && kn < K) {
-                    (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
-                } else if (kn > K) {
-                    atomicMax(&(s ? ckn1 : ckn0)[c], kn);
-                    if (i >= KL_ITEM_CAP) (s ? dtag1 : dtag0)[c] = tag;  // no LDS slot for its descriptor
-                }
-                cs = int((pl & 0x80000000u) | uint32_t(c));
-                inf = KLInfo{u, nd.x, nd.y, 0};
+            const int p = i < la ? pa + i : pb + i - la;
+            const int4 a = *reinterpret_cast<const int4*>(d.aux + p);
+            int4 sg[KL_SEG_LANES];
+            if (d.seg) {
+#pragma unroll
+                for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = *reinterpret_cast<const int4*>(d.seg + size_t(p) * KL_SEG_LANES + j);
             }
-            if (i < KL_ITEM_CAP) {
-                it_key[i] = kn;
-                it_cs[i] = cs;
-                it_info[i] = inf;
+            const int u = a.x, rp = a.y, len = a.z;
+            const bool act = !((s_lock[u >> 5] >> (u & 31)) & 1u);
+            stamp(2);
+            float internal = 0.0f, external = 0.0f;
+            if (act) {
+                int q = 0;
+                if (d.seg) {
+#pragma unroll
+                    for (int j = 0; j < KL_SEG_LANES; ++j) {
+                        const float w0 = __int_as_float(sg[j].y), w1 = __int_as_float(sg[j].w);
+                        const bool e0 = (s_side[sg[j].x >> 5] >> (sg[j].x & 31)) & 1u;
+                        const bool e1 = (s_side[sg[j].z >> 5] >> (sg[j].z & 31)) & 1u;
+                        internal += e0 ? 0.0f : w0;
+                        external += e0 ? w0 : 0.0f;
+                        internal += e1 ? 0.0f : w1;
+                        external += e1 ? w1 : 0.0f;
+                    }
+                    q = 2 * KL_SEG_LANES;
+                }
+                for (; q < len; q += 16) {  // beyond the inline segment: 16 loads in flight per pass
+                    int cc[16];
+                    float ww[16];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        cc[k] = q + k < len ? d.col[rp + q + k] : 0;
+                        ww[k] = q + k < len ? d.w[rp + q + k] : 0.0f;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        const bool e = (s_side[cc[k] >> 5] >> (cc[k] & 31)) & 1u;
+                        internal += e ? 0.0f : ww[k];
+                        external += e ? ww[k] : 0.0f;
+                    }
+                }
+            }
+            stamp(3);
+            {
+                int cs = -1;
+                u64 kn = 0ull;
+                KLInfo inf{0, 0, 0, 0};
+                if (act) {
+                    const float g = external - internal;
+                    const uint32_t pl = uint32_t(a.w);
+                    const int s = int(pl >> 31), p = int(pl & 0x7fffffffu), c = p / KL_CHUNK;
+                    (s ? d.gp1 : d.gp0)[p] = g;
+                    kn = s ? key_min(g, p) : key_max(g, p);
+                    const u64 K = (s ? ck1 : ck0)[c];  // stable during the iteration (other waves may still select)
+                    if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(p) && kn < K) {
+                        (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
+                    } else if (kn > K) {
+                        atomicMax(&(s ? ckn1 : ckn0)[c], kn);
+                        if (i >= KL_ITEM_CAP) (s ? dtag1 : dtag0)[c] = tag;  // no LDS slot for its descriptor
+                    }
+                    cs = int((pl & 0x80000000u) | uint32_t(c));
+                    inf = KLInfo{u, rp, len, 0};
+                }
+                if (i < KL_ITEM_CAP) {
+                    it_key[i] = kn;
+                    it_cs[i] = cs;
+                    it_info[i] = inf;
+                }
             }
         }
+        stamp(4);
         __syncthreads();  // (1) gains, merged keys and rescan tags visible
-        stamp(2);
+        stamp(5);
         // G2. publish merged keys of untagged chunks (every item of the chunk
         // writes the same value) and the descriptor of the item that won ...
         for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
@@ -434,16 +519,17 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
             if (!__shfl(claimed, 0, 64)) continue;
             KLInfo info;
             bool mine;
-            const u64 k = s ? chunk_best(d.gp1, d.pinfo1, d.n1, 1, c, lane, &info, &mine)
-                            : chunk_best(d.gp0, d.pinfo0, d.n0, 0, c, lane, &info, &mine);
+            const u64 k = s ? chunk_best(d.gp1, d.pinfo1, 1, c, lane, &info, &mine)
+                            : chunk_best(d.gp0, d.pinfo0, 0, c, lane, &info, &mine);
             if (mine) {
                 (s ? ck1 : ck0)[c] = k;
                 (s ? ckn1 : ckn0)[c] = k;
                 (s ? ci1 : ci0)[c] = info;
             }
         }
+        stamp(6);
         __syncthreads();  // (2) keys visible to the next selection
-        stamp(3);
+        stamp(7);
         if (s_stop[it & 1]) {
             ++it;
             break;
@@ -451,16 +537,18 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     }
     __syncthreads();
     for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
-    if (tid == 0) {
+    if (wlead) {
         out->iterations = it;
         out->best_iter = best_it;
         out->initial_cut = *d.cut0;
         out->best_cut = best;
         out->final_cut = cut;
         out->status = 2u;
-        for (int i = 0; i < 4; ++i) out->prof[i] = tph[i];
-        out->prof[4] = PROF ? __builtin_amdgcn_s_memtime() - c_start : 0ull;
-        out->prof[5] = PROF ? __builtin_amdgcn_s_memrealtime() - r_start : 0ull;
+    }
+    if (tid == 0) {  // phase stamps are taken by thread 0
+        for (int i = 0; i < 8; ++i) out->prof[i] = tph[i];
+        out->prof[8] = PROF ? __builtin_amdgcn_s_memtime() - c_start : 0ull;
+        out->prof[9] = PROF ? __builtin_amdgcn_s_memrealtime() - r_start : 0ull;
     }
 }
 
@@ -597,7 +685,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
             const int u = i < la ? d.col[pa + i] : i < la + lb ? d.col[pb + i - la] : (i == la + lb ? A : B);
             const uint32_t pl = d.plist[u];
             const int s = int(pl >> 31), c = int(pl & 0x7fffffffu) / KL_CHUNK;
-            const u64 k = s ? chunk_key(d.gp1, d.n1, 1, c, lane) : chunk_key(d.gp0, d.n0, 0, c, lane);
+            const u64 k = s ? chunk_key(d.gp1, 1, c, lane) : chunk_key(d.gp0, 0, c, lane);
             if (lane == 0) (s ? ck1 : ck0)[c] = k;
         }
         if (tid == 0) s_w = 0.0f;
@@ -616,7 +704,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
         out->best_cut = best;
         out->final_cut = cut;
         out->status = SMEM ? 1u : 0u;
-        for (int i = 0; i < 4; ++i) out->prof[i] = tph[i];
+        for (int i = 0; i < 4; ++i) out->prof[i] = tph[i];  // global-state loop: 4 phases
     }
 }
 
@@ -651,6 +739,48 @@ __global__ __launch_bounds__(256) void k_net_cut(long long nets, const int64_t* 
     }
     const u64 m = __ballot(cut);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+}
+
+__global__ __launch_bounds__(256) void k_build_aux(long long nnz, const int32_t* __restrict__ col,
+                                                   const KLInfo* __restrict__ nd, KLInfo* __restrict__ aux) {
+    const long long p = blockIdx.x * 256ll + threadIdx.x;
+    if (p >= nnz) return;
+    const int v = col[p];
+    const int4 x = *reinterpret_cast<const int4*>(nd + v);
+    *reinterpret_cast<int4*>(aux + p) = make_int4(v, x.x, x.y, x.z);
+}
+
+// seg[p*8 + j] = entries 2j, 2j+1 of row col[p] as {col, w bits, col, w bits} (0 past its end)
+__global__ __launch_bounds__(256) void k_build_seg(long long nnz, const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ col, const float* __restrict__ w,
+                                                   KLInfo* __restrict__ seg) {
+    const long long t = blockIdx.x * 256ll + threadIdx.x;
+    const long long p = t >> 3;
+    if (p >= nnz) return;
+    const int j = int(t & 7), v = col[p];
+    const int rp = rowptr[v], len = rowptr[v + 1] - rp;
+    const int e0 = 2 * j, e1 = 2 * j + 1;
+    int4 o = make_int4(0, 0, 0, 0);
+    if (e0 < len) {
+        o.x = col[rp + e0];
+        o.y = __float_as_int(w[rp + e0]);
+    }
+    if (e1 < len) {
+        o.z = col[rp + e1];
+        o.w = __float_as_int(w[rp + e1]);
+    }
+    *reinterpret_cast<int4*>(seg + t) = o;
+}
+
+void kl_build_aux(hipStream_t s, int64_t nnz, const int32_t* col, const KLInfo* nd, KLInfo* aux) {
+    if (nnz <= 0) return;
+    hipLaunchKernelGGL(k_build_aux, dim3(unsigned((nnz + 255) / 256)), dim3(256), 0, s, (long long)nnz, col, nd, aux);
+}
+
+void kl_build_seg(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* w, KLInfo* seg) {
+    if (nnz <= 0) return;
+    hipLaunchKernelGGL(k_build_seg, dim3(unsigned((nnz * 8 + 255) / 256)), dim3(256), 0, s, (long long)nnz, rowptr,
+                       col, w, seg);
 }
 
 void kl_prepare(hipStream_t s, const KLDev& d) {

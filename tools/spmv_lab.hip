@@ -95,22 +95,27 @@ __global__ __launch_bounds__(T) void kA(const int4* __restrict__ desc, const int
 
 // ---- B: every global load of the block issued before any use (fixed trip count)
 template <int BN>
-__global__ __launch_bounds__(T) void kB(const int4* __restrict__ desc, const int* __restrict__ rowptr,
-                                        const int* __restrict__ col, const double* __restrict__ val,
-                                        const double* __restrict__ x, double* __restrict__ y,
-                                        const double* __restrict__ fn2, const double* __restrict__ f,
-                                        double* __restrict__ vcol, double* __restrict__ apart) {
+__device__ __forceinline__ void blockB(int b, const int4* __restrict__ desc, const int* __restrict__ rowptr,
+                                       const int* __restrict__ col, const double* __restrict__ val,
+                                       const double* __restrict__ x, double* __restrict__ y,
+                                       const double* __restrict__ fn2, const double* __restrict__ f,
+                                       double* __restrict__ vcol, double* __restrict__ apart, double* prod, int* rbeg,
+                                       double* yrow, double* wsum) {
     constexpr int PER = BN / T;
-    __shared__ double prod[BN];
-    __shared__ int rbeg[T + 1];
-    __shared__ double yrow[T];
-    __shared__ double wsum[T / 64];
     const int t = threadIdx.x;
-    const int4 d = desc[blockIdx.x];
+    const int4 d = desc[b];
     const int r0 = d.x, nr = d.y, p0 = d.z, cnt = d.w;
     if (cnt > BN) {
         const double scale = *fn2 > 0.0 ? 1.0 / sqrt(*fn2) : 0.0;
-        long_row(r0, p0, cnt, col, val, x, y, scale, f, vcol, apart, wsum);
+        double s = 0.0;
+        for (int i = t; i < cnt; i += T) s += val[p0 + i] * x[col[p0 + i]];
+        const double a = block4(s, wsum);
+        if (t == 0) {
+            y[r0] = a * scale;
+            const double v = f[r0] * scale;
+            vcol[r0] = v;
+            apart[b] = v * (a * scale);
+        }
         return;
     }
     int ci[PER];
@@ -157,7 +162,37 @@ __global__ __launch_bounds__(T) void kB(const int4* __restrict__ desc, const int
         av = v * yrow[t];
     }
     av = block4(av, wsum);
-    if (t == 0) apart[blockIdx.x] = av;
+    if (t == 0) apart[b] = av;
+}
+
+template <int BN>
+__global__ __launch_bounds__(T) void kB(const int4* __restrict__ desc, const int* __restrict__ rowptr,
+                                        const int* __restrict__ col, const double* __restrict__ val,
+                                        const double* __restrict__ x, double* __restrict__ y,
+                                        const double* __restrict__ fn2, const double* __restrict__ f,
+                                        double* __restrict__ vcol, double* __restrict__ apart) {
+    __shared__ double prod[BN];
+    __shared__ int rbeg[T + 1];
+    __shared__ double yrow[T];
+    __shared__ double wsum[T / 64];
+    blockB<BN>(blockIdx.x, desc, rowptr, col, val, x, y, fn2, f, vcol, apart, prod, rbeg, yrow, wsum);
+}
+
+// ---- P: persistent grid, each workgroup walks row blocks b, b + grid, ...
+template <int BN>
+__global__ __launch_bounds__(T) void kP(int nb, const int4* __restrict__ desc, const int* __restrict__ rowptr,
+                                        const int* __restrict__ col, const double* __restrict__ val,
+                                        const double* __restrict__ x, double* __restrict__ y,
+                                        const double* __restrict__ fn2, const double* __restrict__ f,
+                                        double* __restrict__ vcol, double* __restrict__ apart) {
+    __shared__ double prod[BN];
+    __shared__ int rbeg[T + 1];
+    __shared__ double yrow[T];
+    __shared__ double wsum[T / 64];
+    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
+        blockB<BN>(b, desc, rowptr, col, val, x, y, fn2, f, vcol, apart, prod, rbeg, yrow, wsum);
+        __syncthreads();
+    }
 }
 
 // ---- C: vector CSR, G lanes per row, no LDS staging; one partial per block of T/G rows
@@ -307,7 +342,7 @@ int main(int argc, char** argv) {
             CK(hipEventElapsedTime(&ms, e0, e1));
             us_pair += 1e3 * ms / 50;
         }
-        std::printf("%-8s batch %7.2f us (%6.0f GB/s fused)  pair %7.2f us  maxerr %.2e rel\n", name, us_batch,
+        std::printf("%-10s batch %7.2f us (%6.0f GB/s fused)  pair %7.2f us  maxerr %.2e rel\n", name, us_batch,
                     fused / us_batch * 1e-3, us_pair, err / ymax);
         std::fflush(stdout);
     };
@@ -326,13 +361,30 @@ int main(int argc, char** argv) {
     run("B512", LAUNCH_DESC(kB, 512, 0));
     run("B1024", LAUNCH_DESC(kB, 1024, 1));
     run("B2048", LAUNCH_DESC(kB, 2048, 2));
+    for (int g : {256, 512, 1024}) {
+        char nm[16];
+        std::snprintf(nm, sizeof nm, "P512x%d", g);
+        run(nm, [&] {
+            hipLaunchKernelGGL(kP<512>, dim3(g), dim3(T), 0, s, nb[0], (const int4*)d_desc[0], d_rp, d_cl, d_vl, d_f,
+                               d_y, d_fn2, d_f, d_vc, d_ap);
+        });
+        std::snprintf(nm, sizeof nm, "P1024x%d", g);
+        run(nm, [&] {
+            hipLaunchKernelGGL(kP<1024>, dim3(g), dim3(T), 0, s, nb[1], (const int4*)d_desc[1], d_rp, d_cl, d_vl, d_f,
+                               d_y, d_fn2, d_f, d_vc, d_ap);
+        });
+    }
     run("C4", LAUNCH_VEC(4));
     run("C8", LAUNCH_VEC(8));
     run("C16", LAUNCH_VEC(16));
-    // launch floor: the same grid as A1024 doing no row work
-    run("floor", [&] {
-        hipLaunchKernelGGL(kC<8>, dim3(nb[1]), dim3(T), 0, s, 0, d_rp, d_cl, d_vl, d_f, d_y, d_fn2, d_f, d_vc, d_ap);
-    });
+    // launch floor: grids doing no row work
+    for (int g : {256, 1286, 2583}) {
+        char nm[16];
+        std::snprintf(nm, sizeof nm, "floor%d", g);
+        run(nm, [&] {
+            hipLaunchKernelGGL(kC<8>, dim3(g), dim3(T), 0, s, 0, d_rp, d_cl, d_vl, d_f, d_y, d_fn2, d_f, d_vc, d_ap);
+        });
+    }
     ek_csr_free(L);
     ek_hgr_free(h);
     return 0;
