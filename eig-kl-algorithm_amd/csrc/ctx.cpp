@@ -634,8 +634,13 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     c->kl_n = n;
     c->kl_rowptr_h.assign(rowptr, rowptr + n + 1);
     upload(c->kl_rowptr, rowptr, size_t(n) + 1, s);
-    upload(c->kl_col, col, size_t(nnz), s);
-    upload(c->kl_w, w, size_t(nnz), s);
+    // 16 zero entries of tail padding: the swap loop reads rows 16 at a time unconditionally
+    c->kl_col.ensure((size_t(nnz) + 16) * 4);
+    c->kl_w.ensure((size_t(nnz) + 16) * 4);
+    HIPCHK(hipMemsetAsync(c->kl_col.as<int32_t>() + nnz, 0, 16 * 4, s));
+    HIPCHK(hipMemsetAsync(c->kl_w.as<float>() + nnz, 0, 16 * 4, s));
+    if (nnz) HIPCHK(hipMemcpyAsync(c->kl_col.p, col, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
+    if (nnz) HIPCHK(hipMemcpyAsync(c->kl_w.p, w, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
     // inline neighbour-row segments for the swap loop (128 B per entry; skipped past 32 GB)
     c->kl_seg_ok = size_t(nnz) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30);
     if (c->kl_seg_ok) {

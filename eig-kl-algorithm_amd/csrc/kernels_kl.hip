@@ -66,6 +66,18 @@ __device__ __forceinline__ u64 dpp_max(u64 v) {
     const u64 o = (u64(hi2) << 32) | lo2;
     return o > v ? o : v;
 }
+// max within each 32-lane half of the wave (lanes 0-31 and 32-63 separately)
+__device__ __forceinline__ u64 half_max_u64(u64 v) {
+    v = dpp_max<0xB1>(v);
+    v = dpp_max<0x4E>(v);
+    v = dpp_max<0x141>(v);
+    v = dpp_max<0x140>(v);
+    const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const u64 x = (u64(b[0]) << 32) | a[0], y = (u64(b[1]) << 32) | a[1];
+    return x > y ? x : y;
+}
 __device__ __forceinline__ u64 wave_max_u64(u64 v) {
     v = dpp_max<0xB1>(v);   // quad_perm [1,0,3,2]
     v = dpp_max<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -226,7 +238,7 @@ __host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
     const size_t b = (size_t(d.nck0) + size_t(d.nck1)) * (sizeof(KLInfo) + 8 + 4 + 4) +
-                     2 * size_t(kl_sel_pad(d.nck0, d.nck1)) * 8 +
+                     2 * size_t(kl_sel_pad(d.nck0, d.nck1)) * 8 + 2 * (KL_LOOP_THREADS / 64) * 8 +
                      size_t(KL_ITEM_CAP) * (sizeof(KLInfo) + 8 + 4) + 16 + 2 * words * 4 + 64;
     return b <= 152 * 1024 ? b : 0;
 }
@@ -283,7 +295,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     u64* ckn0 = ck1 + nckp;    // shadow keys: G1 merges risen keys here, G2 publishes them to ck
     u64* ckn1 = ckn0 + d.nck0;
     u64* it_key = ckn1 + d.nck1;                                // per affected row: its new key
-    int* dtag0 = reinterpret_cast<int*>(it_key + KL_ITEM_CAP);  // iteration that tagged a rescan
+    u64* sel_part = it_key + KL_ITEM_CAP;                       // [2][NW] per-wave selection partials
+    int* dtag0 = reinterpret_cast<int*>(sel_part + 2 * NW);     // iteration that tagged a rescan
     int* dtag1 = dtag0 + d.nck0;
     int* ctag0 = dtag1 + d.nck1;                               // iteration that claimed the rescan
     int* ctag1 = ctag0 + d.nck0;
@@ -330,24 +343,26 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     for (;; ++it) {
         stamp(-1);
         // S. selection (cKL.cpp:341-355), redundantly in every wave
-        // all of a lane's key reads are issued before the first compare (a
-        // rolled loop would pay one LDS round trip per 64 chunks)
-        u64 k0 = 0ull, k1 = 0ull;
-        for (int c0 = 0; c0 < nckp; c0 += KL_SEL_UNROLL * 64) {
-            u64 a[KL_SEL_UNROLL], b[KL_SEL_UNROLL];
-#pragma unroll
-            for (int j = 0; j < KL_SEL_UNROLL; ++j) {
-                a[j] = ck0[c0 + j * 64 + lane];
-                b[j] = ck1[c0 + j * 64 + lane];
-            }
-#pragma unroll
-            for (int j = 0; j < KL_SEL_UNROLL; ++j) {
-                k0 = a[j] > k0 ? a[j] : k0;
-                k1 = b[j] > k1 ? b[j] : k1;
-            }
+        // the waves split the chunk keys (lanes 0-31: remain[0], 32-63:
+        // remain[1]; 32 chunks per wave and pass, unconditional reads of the
+        // zero-padded arrays), reduce per half-wave, and meet at one barrier;
+        // then every wave reduces the NW partials itself
+        const int half = lane >> 5, hl = lane & 31;
+        {
+            const u64* ck = half ? ck1 : ck0;
+            u64 k = 0ull;
+            for (int c = wv * 32 + hl; c < nckp; c += NW * 32) k = ck[c] > k ? ck[c] : k;
+            k = half_max_u64(k);
+            if (hl == 0) sel_part[half * NW + wv] = k;
         }
-        k0 = wave_max_u64(k0);
-        k1 = wave_max_u64(k1);
+        __syncthreads();  // (0) selection partials
+        u64 k0, k1;
+        {
+            u64 k = hl < NW ? sel_part[half * NW + hl] : 0ull;
+            k = half_max_u64(k);
+            k0 = __shfl(k, 0, 64);
+            k1 = __shfl(k, 32, 64);
+        }
         if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
         const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
         const KLInfo ia = ci0[posA / KL_CHUNK], ib = ci1[posB / KL_CHUNK];
@@ -446,12 +461,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
                     int cc[16];
                     float ww[16];
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        cc[k] = q + k < len ? d.col[rp + q + k] : 0;
+                    for (int k = 0; k < 16; ++k) {  // col/w carry 16 zero entries of tail padding
+                        cc[k] = d.col[rp + q + k];
                         ww[k] = q + k < len ? d.w[rp + q + k] : 0.0f;
                     }
 #pragma unroll
                     for (int k = 0; k < 16; ++k) {
+                        cc[k] = q + k < len ? cc[k] : 0;
                         const bool e = (s_side[cc[k] >> 5] >> (cc[k] & 31)) & 1u;
                         internal += e ? 0.0f : ww[k];
                         external += e ? ww[k] : 0.0f;
