@@ -199,7 +199,7 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     c->nrows = nrows;
     c->nloc = c->nranks > 1 ? nloc : n;
     c->nnz = nnz;
-    c->block_nnz = nnz < 512ll * 1024 ? 512 : 1024;
+    c->block_nnz = 512;  // lab (tools/spmv_lab.hip): 512-nnz blocks are the fastest at every size tried
     const auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
     c->nrb_spmv = int(rbv.size() / 4);
     upload(c->rb, rbv.data(), rbv.size(), c->stream);
@@ -309,15 +309,15 @@ struct Lanczos {
     // H += V^T f after its re-orthogonalisation).
     int reorth = 1;
     void factorize(int k) {
+        if (c->nranks == 1 && reorth == 1) return factorize_fused(k);
         double* fn2 = c->fn2.as<double>();
         for (int i = k; i < m; ++i) {
             const double* x = gather_f();
             const bool timed = time_spmv && size_t(2 * (i - k) + 1) < ev.size();
-            if (timed) HIPCHK(hipEventRecord(ev[size_t(2 * (i - k))], s));
             ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
                           c->val.as<double>(), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
-                          reorth == 1 ? c->apart.as<double>() : nullptr, c->block_nnz);
-            if (timed) HIPCHK(hipEventRecord(ev[size_t(2 * (i - k) + 1)], s));
+                          reorth == 1 ? c->apart.as<double>() : nullptr, c->block_nnz, nullptr,
+                          timed ? ev[size_t(2 * (i - k))] : nullptr, timed ? ev[size_t(2 * (i - k) + 1)] : nullptr);
             ++matvecs;
             const int nc = i + 1, tot = nc + has_u0;
             if (reorth == 1) {
@@ -357,6 +357,48 @@ struct Lanczos {
                                    c->h2.as<double>(), i, c->alpha.as<double>(), c->offd.as<double>());
             allreduce(c, fn2 + i + 1, 1);
         }
+        HIPCHK(hipGetLastError());
+    }
+
+    // Single GPU, reorth 1: four launches per step.  The SpMV also runs the
+    // previous step's finalize (||f||^2, alpha, beta) and the update reduces
+    // the projection partials itself (same column-sum order as k_reduce_cols,
+    // so the fused and unfused paths give identical bits).  Folding the
+    // three-term recurrence into the projection was measured slower: every
+    // column tile re-reads w, v_i and v_{i-1}.
+    void factorize_fused(int k) {
+        double* fn2 = c->fn2.as<double>();
+        double* a3 = c->scal.as<double>() + 2;
+        const double* bov = c->bov.as<double>();
+        for (int i = k; i < m; ++i) {
+            ek::dev::StepFin fin;
+            if (i > k) {
+                fin.npart = c->npart.as<double>();
+                fin.nb = nub;
+                fin.fn2_out = fn2 + i;
+                fin.h2 = c->h2.as<double>();
+                fin.step = i - 1;
+                fin.alpha = c->alpha.as<double>();
+                fin.offd = c->offd.as<double>();
+                fin.a3 = a3;
+                fin.fn2_i = fn2 + i - 1;
+                fin.bov_i = bov + i - 1;
+            }
+            const bool timed = time_spmv && size_t(2 * (i - k) + 1) < ev.size();
+            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                          c->val.as<double>(), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
+                          c->apart.as<double>(), c->block_nnz, i > k ? &fin : nullptr,
+                          timed ? ev[size_t(2 * (i - k))] : nullptr, timed ? ev[size_t(2 * (i - k) + 1)] : nullptr);
+            ++matvecs;
+            const int nc = i + 1;
+            ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
+                                i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>());
+            ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
+            ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
+                              c->f.as<double>(), c->f.as<double>(), c->npart.as<double>());
+        }
+        ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + m, nullptr, c->h2.as<double>(), m - 1,
+                               c->alpha.as<double>(), c->offd.as<double>(), a3, fn2 + m - 1, bov + m - 1);
         HIPCHK(hipGetLastError());
     }
 

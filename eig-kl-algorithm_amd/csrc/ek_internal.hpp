@@ -71,6 +71,26 @@ typedef struct ihipStream_t* hipStream_t;
 namespace ek {
 namespace dev {
 
+typedef struct ihipEvent_t* hipEvent_t;
+
+// The finalize of Lanczos step `step`, folded into the next step's first
+// kernel (k_finalize_step's a3 form): fn2_out = sum(npart[0:nb]) — every
+// block sums the same partials in the same order — and block 0 publishes
+// fn2_out, alpha[step] = *a3 + h2[step], offd[step] = beta_step + h2[step-1]
+// with beta_step = *bov_i unless NaN, else sqrt(*fn2_i).  npart == null: none.
+struct StepFin {
+    const double* npart = nullptr;
+    int nb = 0;
+    double* fn2_out = nullptr;
+    const double* h2 = nullptr;
+    int step = -1;
+    double* alpha = nullptr;
+    double* offd = nullptr;
+    const double* a3 = nullptr;
+    const double* fn2_i = nullptr;
+    const double* bov_i = nullptr;
+};
+
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
 constexpr int SPMV_THREADS = 256;
 std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int block_nnz);
@@ -78,9 +98,12 @@ std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int b
 // If vcol != null also writes vcol[r] = f[r] * scale (Lanczos basis column), and
 // if apart != null the per-block partials of vcol . y (one per block).
 // desc: 4 ints per block {row0, nrows, nnz0, cnt} from spmv_row_blocks.
+// fin: the previous step's finalize folded in (then ||f||^2 comes from it, not *fn2).
+// ev_start/ev_stop: kernel start/end timestamps (hipExtLaunchKernelGGL), optional.
 void spmv(hipStream_t s, int nblocks, const int32_t* desc, const int32_t* rowptr, const int32_t* col,
           const double* val, const double* x, double* y, const double* fn2, const double* f, double* vcol,
-          double* apart, int block_nnz);
+          double* apart, int block_nnz, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
+          hipEvent_t ev_stop = nullptr);
 
 // kernels_lanczos.hip
 constexpr int GT_ROWS = 1024;  // rows per gemv-T block; ldv is a multiple of this
@@ -93,6 +116,12 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
            int nreal, const double* w, double* part);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
+
+// Fused single-GPU step (reorth 1):
+// update_r: h = column sums of part (every block, fixed order; block 0 writes
+// h_out), then dst = src - V h - u0 h[ncols] with ||dst||^2 partials -> npart
+void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
+              const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart);
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart);

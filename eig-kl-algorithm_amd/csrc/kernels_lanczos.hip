@@ -34,33 +34,35 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 }
 
 // partial dot products of w with GT_COLS basis columns over GT_ROWS rows.
-// grid = (nrb, ceil((ncols + has_u0) / GT_COLS)); 256 threads, each 2 x double2.
+// grid = (nrb, ceil((ncols + has_u0) / GT_COLS)); 256 threads, each
+// GT_ROWS/512 double2 rows; column ncols is the deflation vector u0.
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part) {
     __shared__ double red[4][GT_COLS];
     const int t = threadIdx.x;
     const int rbk = blockIdx.x, j0 = blockIdx.y * GT_COLS;
-    const size_t r0 = size_t(rbk) * GT_ROWS + 2 * size_t(t);
-    const double2 w0 = *reinterpret_cast<const double2*>(w + r0);
-    const double2 w1 = *reinterpret_cast<const double2*>(w + r0 + 512);
     double acc[GT_COLS];
 #pragma unroll
-    for (int jj = 0; jj < GT_COLS; ++jj) {
-        const int j = j0 + jj;
-        double a = 0.0;
-        if (j < ncols) {
-            const double* vj = V + size_t(j) * ldv;
-            const double2 v0 = *reinterpret_cast<const double2*>(vj + r0);
-            const double2 v1 = *reinterpret_cast<const double2*>(vj + r0 + 512);
-            a = v0.x * w0.x + v0.y * w0.y + v1.x * w1.x + v1.y * w1.y;
-        } else if (has_u0 && j == ncols) {
-            const size_t nr = size_t(nreal);
-            a = u0val * ((r0 < nr ? w0.x : 0.0) + (r0 + 1 < nr ? w0.y : 0.0) + (r0 + 512 < nr ? w1.x : 0.0) +
-                         (r0 + 513 < nr ? w1.y : 0.0));
+    for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
+    const size_t nr = size_t(nreal);
+#pragma unroll
+    for (int k = 0; k < GT_ROWS / 512; ++k) {
+        const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+        const double2 x = *reinterpret_cast<const double2*>(w + r);
+#pragma unroll
+        for (int jj = 0; jj < GT_COLS; ++jj) {
+            const int j = j0 + jj;
+            if (j < ncols) {
+                const double2 v = *reinterpret_cast<const double2*>(V + size_t(j) * ldv + r);
+                acc[jj] += v.x * x.x + v.y * x.y;
+            } else if (has_u0 && j == ncols) {
+                acc[jj] += u0val * ((r < nr ? x.x : 0.0) + (r + 1 < nr ? x.y : 0.0));
+            }
         }
-        acc[jj] = wave_sum(a);
     }
+#pragma unroll
+    for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = wave_sum(acc[jj]);
     if ((t & 63) == 0) {
 #pragma unroll
         for (int jj = 0; jj < GT_COLS; ++jj) red[t >> 6][jj] = acc[jj];
@@ -70,24 +72,49 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
         part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
 }
 
-// h[j] = sum_b part[j*nrb + b]; one workgroup per column.
-__global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ part, int nrb, double* __restrict__ h) {
-    __shared__ double lds4[4];
-    const double* pj = part + size_t(blockIdx.x) * nrb;
+// The canonical order of a column sum over the projection partials: lane
+// pair (2j, 2j+1) sums the even / odd blocks in order, then one add.  Used by
+// k_reduce_cols and by the fused update alike, so both give the same bits.
+__device__ __forceinline__ double col_sum(const double* __restrict__ pj, int nrb, int half) {
     double s = 0.0;
-    for (int i = threadIdx.x; i < nrb; i += 256) s += pj[i];
-    s = block_sum256(s, lds4);
-    if (threadIdx.x == 0) h[blockIdx.x] = s;
+#pragma unroll 4
+    for (int b = half; b < nrb; b += 2) s += pj[b];
+    return s + __shfl_xor(s, 1, 64);
+}
+
+// h[j] = sum_b part[j*nrb + b]; 128 columns per workgroup.
+__global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ part, int nrb, int ncols,
+                                                     double* __restrict__ h) {
+    const int j = blockIdx.x * 128 + (threadIdx.x >> 1);
+    const double s = col_sum(part + size_t(j < ncols ? j : 0) * nrb, nrb, threadIdx.x & 1);
+    if (j < ncols && (threadIdx.x & 1) == 0) h[j] = s;
 }
 
 // dst = src - V[:, :ncols] h - u0 h[ncols]; 256 threads x 2 rows (double2).
+// RED: h is first reduced from the projection partials (column j: two lanes
+// each summing every other block in order, then one add — the same in every
+// workgroup; workgroup 0 publishes h_out).
+template <bool RED>
 __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restrict__ V, int ncols, int has_u0,
                                                 double u0val, int nreal, const double* __restrict__ h,
                                                 const double* __restrict__ src, double* __restrict__ dst,
-                                                double* __restrict__ npart) {
+                                                double* __restrict__ npart, const double* __restrict__ part, int nrb,
+                                                double* __restrict__ h_out) {
     __shared__ double hs[MAX_NCV + 2];
     __shared__ double lds4[4];
-    for (int j = threadIdx.x; j < ncols + has_u0; j += 256) hs[j] = h[j];
+    const int tot = ncols + has_u0;
+    if constexpr (RED) {
+        for (int j0 = 0; j0 < tot; j0 += 128) {
+            const int j = j0 + (threadIdx.x >> 1);
+            const double s = col_sum(part + size_t(j < tot ? j : 0) * nrb, nrb, threadIdx.x & 1);
+            if (j < tot && (threadIdx.x & 1) == 0) {
+                hs[j] = s;
+                if (blockIdx.x == 0) h_out[j] = s;
+            }
+        }
+    } else {
+        for (int j = threadIdx.x; j < tot; j += 256) hs[j] = h[j];
+    }
     __syncthreads();
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
     double2 x = *reinterpret_cast<const double2*>(src + r);
@@ -237,19 +264,26 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
            const double* w, double* part) {
     const int cols = ncols + has_u0;
     if (cols <= 0) return;
-    hipLaunchKernelGGL(k_gemvt, dim3(nrb, (cols + GT_COLS - 1) / GT_COLS), dim3(256), 0, s, ldv, nrb, V, ncols,
-                       has_u0, u0val, nreal, w, part);
+    hipLaunchKernelGGL(k_gemvt, dim3(nrb, (cols + GT_COLS - 1) / GT_COLS), dim3(256), 0, s, ldv, nrb, V, ncols, has_u0,
+                       u0val, nreal, w, part);
 }
+
 
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h) {
     if (ncols_total <= 0) return;
-    hipLaunchKernelGGL(k_reduce_cols, dim3(ncols_total), dim3(256), 0, s, part, nrb, h);
+    hipLaunchKernelGGL(k_reduce_cols, dim3((ncols_total + 127) / 128), dim3(256), 0, s, part, nrb, ncols_total, h);
 }
 
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart) {
-    hipLaunchKernelGGL(k_update, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal, h, src,
-                       dst, npart);
+    hipLaunchKernelGGL(k_update<false>, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal, h,
+                       src, dst, npart, nullptr, 0, nullptr);
+}
+
+void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
+              const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart) {
+    hipLaunchKernelGGL(k_update<true>, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal,
+                       nullptr, src, dst, npart, part, nrb, h_out);
 }
 
 void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1, const double* h2,

@@ -21,6 +21,7 @@
 // matvec runs on the unscaled residual f, so there is no separate normalise
 // kernel as in gKL2.cu:177-188), and when apart != null the block's partial of
 // alpha = vcol . y is written (fixed tree) for the three-term recurrence.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "ek_internal.hpp"
@@ -58,6 +59,27 @@ std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int b
     return desc;
 }
 
+__device__ __forceinline__ void finalize_publish(const StepFin& f, double n2) {
+    f.fn2_out[0] = n2;
+    if (f.step >= 0) {
+        f.alpha[f.step] = *f.a3 + f.h2[f.step];
+        if (f.step > 0) f.offd[f.step] = (isnan(f.bov_i[0]) ? sqrt(f.fn2_i[0]) : f.bov_i[0]) + f.h2[f.step - 1];
+    }
+}
+
+// sum of x[0:n) over the workgroup in a fixed tree; every thread gets it
+__device__ __forceinline__ double block_sum_all(const double* __restrict__ x, int n, double* wsum) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += SPMV_THREADS) s += x[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    const double r = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    __syncthreads();
+    return r;
+}
+
 template <int BLOCK_NNZ>
 __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __restrict__ desc,
                                                                 const int32_t* __restrict__ rowptr,
@@ -66,7 +88,9 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
                                                                 const double* __restrict__ x, double* __restrict__ y,
                                                                 const double* __restrict__ fn2,
                                                                 const double* __restrict__ f,
-                                                                double* __restrict__ vcol, double* __restrict__ apart) {
+                                                                double* __restrict__ vcol, double* __restrict__ apart,
+                                                                StepFin fin) {
+    constexpr int PER = BLOCK_NNZ / SPMV_THREADS;
     __shared__ double prod[BLOCK_NNZ];
     __shared__ int rbeg[SPMV_THREADS + 1];
     __shared__ double yrow[SPMV_THREADS];
@@ -74,9 +98,18 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     const int t = threadIdx.x;
     const int4 dsc = desc[blockIdx.x];
     const int r0 = dsc.x, nr = dsc.y, p0 = dsc.z, cnt = dsc.w;
+    // ||f||^2: folded finalize of the previous Lanczos step (every block sums
+    // the same partials in the same order; block 0 publishes) or read
+    double n2 = 1.0;
+    if (fin.npart) {
+        n2 = block_sum_all(fin.npart, fin.nb, wsum);
+        if (blockIdx.x == 0 && t == 0) finalize_publish(fin, n2);
+    } else if (fn2) {
+        n2 = *fn2;
+    }
     // an exact breakdown (f = 0) yields a zero column instead of NaN; the host
-    // driver detects it and injects a fresh vector (see Lanczos::breakdown)
-    const double scale = fn2 ? (*fn2 > 0.0 ? 1.0 / sqrt(*fn2) : 0.0) : 1.0;
+    // driver detects it and injects a fresh vector (Lanczos::inject)
+    const double scale = (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0;
 
     if (cnt > BLOCK_NNZ) {  // vector mode: single long row
         double s = 0.0;
@@ -96,10 +129,29 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         }
         return;
     }
-    // stream mode: row boundaries to LDS, coalesced products into LDS
-    for (int i = t; i <= nr; i += SPMV_THREADS) rbeg[i] = rowptr[r0 + i] - p0;  // nr may be 256: 257 bounds
+    // stream mode: every global load of the block is issued before the first
+    // use (fixed trip count), products to LDS, row boundaries to LDS
+    int ci[PER];
+    double vv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int i = t + u * SPMV_THREADS;
+        ci[u] = i < cnt ? col[p0 + i] : -1;
+        vv[u] = i < cnt ? val[p0 + i] : 0.0;
+    }
+    const int rb0 = t <= nr ? rowptr[r0 + t] - p0 : 0;
+    const int rb1 = (t == 0 && nr == SPMV_THREADS) ? rowptr[r0 + SPMV_THREADS] - p0 : 0;
     const double fr = (vcol && t < nr) ? f[r0 + t] : 0.0;  // prefetched for the epilogue
-    for (int i = t; i < cnt; i += SPMV_THREADS) prod[i] = val[p0 + i] * x[col[p0 + i]];
+    double xv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) xv[u] = ci[u] >= 0 ? x[ci[u]] : 0.0;
+    if (t <= nr) rbeg[t] = rb0;
+    if (t == 0 && nr == SPMV_THREADS) rbeg[SPMV_THREADS] = rb1;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int i = t + u * SPMV_THREADS;
+        if (i < cnt) prod[i] = vv[u] * xv[u];
+    }
     __syncthreads();
     // lanes per row: largest power of two with nr * L <= 256, capped at one wave
     int L = SPMV_THREADS / (nr > 0 ? nr : 1);
@@ -135,23 +187,21 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
 
 void spmv(hipStream_t s, int nblocks, const int32_t* desc, const int32_t* rowptr, const int32_t* col,
           const double* val, const double* x, double* y, const double* fn2, const double* f, double* vcol,
-          double* apart, int block_nnz) {
+          double* apart, int block_nnz, const StepFin* fin, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (nblocks <= 0) return;
     const int4* d = reinterpret_cast<const int4*>(desc);
+    const StepFin fv = fin ? *fin : StepFin{};
+    // with events: HIP records the kernel's own start/end timestamps (what
+    // rocprofv3 reports), not event packets around it
+#define EK_SPMV_LAUNCH(BN)                                                                                         \
+    hipExtLaunchKernelGGL(k_spmv_adaptive<BN>, dim3(nblocks), dim3(SPMV_THREADS), 0, s, ev_start, ev_stop, 0, d, \
+                          rowptr, col, val, x, y, fn2, f, vcol, apart, fv)
     switch (block_nnz) {
-        case 512:
-            hipLaunchKernelGGL(k_spmv_adaptive<512>, dim3(nblocks), dim3(SPMV_THREADS), 0, s, d, rowptr, col, val, x,
-                               y, fn2, f, vcol, apart);
-            break;
-        case 2048:
-            hipLaunchKernelGGL(k_spmv_adaptive<2048>, dim3(nblocks), dim3(SPMV_THREADS), 0, s, d, rowptr, col, val, x,
-                               y, fn2, f, vcol, apart);
-            break;
-        default:
-            hipLaunchKernelGGL(k_spmv_adaptive<1024>, dim3(nblocks), dim3(SPMV_THREADS), 0, s, d, rowptr, col, val,
-                               x, y, fn2, f, vcol, apart);
-            break;
+        case 512: EK_SPMV_LAUNCH(512); break;
+        case 2048: EK_SPMV_LAUNCH(2048); break;
+        default: EK_SPMV_LAUNCH(1024); break;
     }
+#undef EK_SPMV_LAUNCH
 }
 
 }  // namespace dev
