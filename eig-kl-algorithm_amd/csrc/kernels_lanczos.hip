@@ -171,6 +171,14 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
                                                     double* __restrict__ fp) {
     __shared__ double lds4[4];
     __shared__ double s_alpha;
+    // the row loads go out first: they do not depend on alpha and overlap
+    // the reduction of its partials
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    double2 x = *reinterpret_cast<const double2*>(w + r);
+    const double2 v = *reinterpret_cast<const double2*>(vi + r);
+    const double2 u = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
+    // beta_i = ||f_i||, or 0 after an injected restart vector (override not NaN)
+    const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
     if (nparts > 0) {
         double s = 0.0;
         for (int i = threadIdx.x; i < nparts; i += 256) s += apart[i];
@@ -183,16 +191,10 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
         s_alpha = *alpha_io;
     }
     __syncthreads();
-    // beta_i = ||f_i||, or 0 after an injected restart vector (override not NaN)
-    const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
     const double a = s_alpha;
-    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
-    double2 x = *reinterpret_cast<const double2*>(w + r);
-    const double2 v = *reinterpret_cast<const double2*>(vi + r);
     x.x -= a * v.x;
     x.y -= a * v.y;
     if (vim1) {
-        const double2 u = *reinterpret_cast<const double2*>(vim1 + r);
         x.x -= b * u.x;
         x.y -= b * u.y;
     }

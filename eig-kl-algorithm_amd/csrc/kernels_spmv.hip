@@ -99,19 +99,23 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     const int4 dsc = desc[blockIdx.x];
     const int r0 = dsc.x, nr = dsc.y, p0 = dsc.z, cnt = dsc.w;
     // ||f||^2: folded finalize of the previous Lanczos step (every block sums
-    // the same partials in the same order; block 0 publishes) or read
-    double n2 = 1.0;
-    if (fin.npart) {
-        n2 = block_sum_all(fin.npart, fin.nb, wsum);
-        if (blockIdx.x == 0 && t == 0) finalize_publish(fin, n2);
-    } else if (fn2) {
-        n2 = *fn2;
-    }
+    // the same partials in the same order; block 0 publishes) or read.  The
+    // scale is only needed by the epilogue, so in stream mode the reduction
+    // runs after the block's loads are issued (see below).
+    auto norm2 = [&]() -> double {
+        if (fin.npart) {
+            const double n2 = block_sum_all(fin.npart, fin.nb, wsum);
+            if (blockIdx.x == 0 && t == 0) finalize_publish(fin, n2);
+            return n2;
+        }
+        return fn2 ? *fn2 : 1.0;
+    };
     // an exact breakdown (f = 0) yields a zero column instead of NaN; the host
     // driver detects it and injects a fresh vector (Lanczos::inject)
-    const double scale = (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0;
+    auto scale_of = [&](double n2) { return (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0; };
 
     if (cnt > BLOCK_NNZ) {  // vector mode: single long row
+        const double scale = scale_of(norm2());
         double s = 0.0;
         for (int i = t; i < cnt; i += SPMV_THREADS) s += val[p0 + i] * x[col[p0 + i]];
 #pragma unroll
@@ -145,6 +149,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     double xv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) xv[u] = ci[u] >= 0 ? x[ci[u]] : 0.0;
+    const double scale = scale_of(norm2());  // overlaps the gathers in flight
     if (t <= nr) rbeg[t] = rb0;
     if (t == 0 && nr == SPMV_THREADS) rbeg[SPMV_THREADS] = rb1;
 #pragma unroll
