@@ -90,6 +90,7 @@ _sig("ek_spmv_setup", ctypes.c_int, _P, _I64, _I64, _I64, _P, _P, _P)
 _sig("ek_spmv", ctypes.c_int, _P, _P, _P, _P)
 _sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
 _sig("ek_spmv_bytes", _I64, _P)
+_sig("ek_spmv_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
 _sig("ek_lanczos_fiedler", ctypes.c_int, _P, ctypes.POINTER(LanczosOpts), ctypes.POINTER(ctypes.c_double), _P,
      ctypes.POINTER(LanczosStats))
@@ -317,8 +318,15 @@ class Context:
     def spmv_device(self, x_ptr, y_ptr, stream=None):
         _chk(_lib.ek_spmv(self._c, x_ptr, y_ptr, stream), "spmv")
 
-    def spmv_bytes(self):
-        return _lib.ek_spmv_bytes(self._c)
+    def spmv_bytes(self, fused=False):
+        """Algorithmic bytes of one SpMV; fused: the Lanczos form (+ f read, basis column write)."""
+        return _lib.ek_spmv_bytes(self._c) + (16 * self.nrows if fused else 0)
+
+    def spmv_bench(self, iters=200, fused=True):
+        """Average microseconds per back-to-back SpMV launch on resident buffers."""
+        us = ctypes.c_double()
+        _chk(_lib.ek_spmv_bench(self._c, int(iters), 1 if fused else 0, ctypes.byref(us)), "spmv_bench")
+        return us.value
 
     def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=1):
         """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207)."""

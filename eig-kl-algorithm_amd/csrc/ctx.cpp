@@ -240,6 +240,54 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     EK_CATCH
 }
 
+int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_bench before ek_spmv_setup");
+    if (iters <= 0 || !avg_us) ek::fail(EK_EINVAL, "ek_spmv_bench: bad argument");
+    if (c->nranks > 1) ek::fail(EK_EINVAL, "ek_spmv_bench: single-context measurement");
+    hipStream_t s = c->stream;
+    const size_t n = size_t(c->n);
+    DBuf x, y, vcol, apart, fn2;
+    x.ensure(n * 8);
+    y.ensure(n * 8);
+    vcol.ensure(n * 8);
+    apart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
+    fn2.ensure(8);
+    std::vector<double> h(n);
+    for (size_t i = 0; i < n; ++i) h[i] = double((i * 2654435761u) % 1000u) / 1000.0 - 0.5;
+    double nrm = 0.0;
+    for (double v : h) nrm += v * v;
+    HIPCHK(hipMemcpyAsync(x.p, h.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(fn2.p, &nrm, 8, hipMemcpyHostToDevice, s));
+    auto launch = [&] {
+        if (fused)
+            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                          c->val.as<double>(), x.as<double>(), y.as<double>(), fn2.as<double>(), x.as<double>(),
+                          vcol.as<double>(), apart.as<double>(), c->block_nnz);
+        else
+            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
+                          c->val.as<double>(), x.as<double>(), y.as<double>(), nullptr, nullptr, nullptr, nullptr,
+                          c->block_nnz);
+    };
+    for (int i = 0; i < 10; ++i) launch();
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) launch();
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIPCHK(hipGetLastError());
+    *avg_us = 1e3 * double(ms) / iters;
+    return EK_OK;
+    EK_CATCH
+}
+
 int64_t ek_spmv_bytes(ek_ctx* c) {
     if (!c) return 0;
     return 12 * c->nnz + 4 * (c->nrows + 1) + 8 * c->n + 8 * c->nrows;

@@ -122,6 +122,12 @@ int ek_spmv_host(ek_ctx* ctx, const double* x, double* y);
  * §8d: 12*nnz (col+val) + 4*(nrows+1) (rowptr) + 8*n (x read once) +
  * 8*nrows (y).  Single GPU: 12 nnz + 4(n+1) + 16 n. */
 int64_t ek_spmv_bytes(ek_ctx* ctx);
+/* Back-to-back SpMV launches on context-owned buffers, timed with HIP events
+ * around the batch: *avg_us = average per launch.  fused = 1 times the
+ * Lanczos form (y scaled by 1/||x||, basis column + alpha partials written:
+ * + 16*nrows bytes over ek_spmv_bytes).  Measurement helper for bench.py's
+ * size sweep; no reference counterpart. */
+int ek_spmv_bench(ek_ctx* ctx, int iters, int fused, double* avg_us);
 
 /* ------------------------------------------------------------------ */
 /* Lanczos / Fiedler: Spectra SymEigsSolver(op, 2, min(100,n/2)),        */
