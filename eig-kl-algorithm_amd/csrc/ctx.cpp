@@ -357,7 +357,9 @@ struct Lanczos {
     // H += V^T f after its re-orthogonalisation).
     int reorth = 1;
     void factorize(int k) {
-        if (c->nranks == 1 && reorth == 1) return factorize_fused(k);
+        // EK_LANCZOS_UNFUSED: run the multi-rank step sequence on one GPU (tests)
+        static const bool unfused = std::getenv("EK_LANCZOS_UNFUSED") != nullptr;
+        if (c->nranks == 1 && reorth == 1 && !unfused) return factorize_fused(k);
         double* fn2 = c->fn2.as<double>();
         for (int i = k; i < m; ++i) {
             const double* x = gather_f();

@@ -143,6 +143,27 @@ def test_lanczos_golden(ek, ctx, name, deflate, reorth):
     assert abs(np.linalg.norm(v) - 1) < 1e-12 and abs(v.sum()) < 1e-8
 
 
+def test_lanczos_multirank_step_sequence_on_one_gpu(ek, tmp_path):
+    """The step sequence the sharded path runs (separate alpha / projection /
+    finalize launches with the all-reduce points between them; RCCL is a no-op
+    at one rank) must reproduce the fused single-GPU sequence bit for bit."""
+    import subprocess
+    import sys
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); from conftest import load_package, circuit_path; "
+        "ek = load_package(); h = ek.Hypergraph.read(circuit_path('ibm01')); L = h.laplacian(); "
+        "c = ek.Context(0); c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val); lam, v, st = c.lanczos_fiedler(); "
+        "np.save(sys.argv[1], np.concatenate([[lam, st['matvecs']], v]))") % os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ)
+    a, b = str(tmp_path / "fused.npy"), str(tmp_path / "unfused.npy")
+    subprocess.run([sys.executable, "-c", code, a], check=True, timeout=120, env=env)
+    env["EK_LANCZOS_UNFUSED"] = "1"
+    subprocess.run([sys.executable, "-c", code, b], check=True, timeout=120, env=env)
+    x, y = np.load(a), np.load(b)
+    assert x[1] == y[1]  # same matvec count
+    assert np.array_equal(x, y)
+
+
 def test_lanczos_ibm10_unconverged_golden(ek, ctx):
     # the shipped ibm10 golden is not converged (SURVEY §0 finding 5): pin by residual
     h = ek.Hypergraph.read(circuit_path("ibm10"))

@@ -12,7 +12,7 @@ TAG="${1:-r01}"
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-BENCH=(python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline)
+BENCH=(python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-sweep)
 if [ -x "$ROOT/tools/build/spmv_lab" ]; then
     timeout -k 10 120 "$ROOT/tools/build/spmv_lab" 1.0 200 > "$OUT/${TAG}_spmv_lab.txt" 2>&1
 fi
