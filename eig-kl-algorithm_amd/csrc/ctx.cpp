@@ -845,6 +845,7 @@ namespace {
 ek::dev::KLDev kl_dev(ek_ctx* c) {
     ek::dev::KLDev d;
     d.n = int(c->kl_n);
+    d.nnz = c->kl_rowptr_h.empty() ? 0 : c->kl_rowptr_h.back();
     d.rowptr = c->kl_rowptr.as<int32_t>();
     d.col = c->kl_col.as<int32_t>();
     d.w = c->kl_w.as<float>();
@@ -946,14 +947,14 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
         if (std::getenv("EK_KL_PROF")) {
-            static const char* names[8] = {"select", "swap", "G1-desc", "G1-sum", "G1-key", "bar1",
-                                           "G2", "bar2"};
+            static const char* names[10] = {"select", "G1-key", "bar1", "G2a", "G2bc", "bar2", "G1-aux", "G1-sum",
+                                            "n_stale", "n_late+tail"};
             std::fprintf(stderr, "[kl] %lld swaps, us/swap:", (long long)ho.iterations);
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 10; ++i)
                 std::fprintf(stderr, " %s %.3f", names[i], ho.prof[i] * 0.01 / std::max<long long>(1, ho.iterations));
             std::fprintf(stderr, "\n");
-            if (ho.prof[9])
-                std::fprintf(stderr, "[kl] in-loop shader clock %.0f MHz\n", double(ho.prof[8]) / (double(ho.prof[9]) * 0.01));
+            if (ho.prof[15])
+                std::fprintf(stderr, "[kl] in-loop shader clock %.0f MHz\n", double(ho.prof[14]) / (double(ho.prof[15]) * 0.01));
         }
         res->total_ms = double(loop_ms) + double(prep_ms);
     }

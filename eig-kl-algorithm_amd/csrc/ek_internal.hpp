@@ -145,13 +145,14 @@ void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* 
 void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares);
 
 // kernels_kl.hip
-constexpr int KL_LOOP_THREADS = 1024;
-constexpr int KL_CHUNK = 256;
+constexpr int KL_LOOP_THREADS = 512;  // 8 waves: 256 VGPRs per lane, no spills in the swap loop
+constexpr int KL_CHUNK = 1024;  // positions per chunk key (a few keys per lane: barrier-free selection)
 struct alignas(16) KLInfo {
     int32_t a, b, c, d;
 };
 struct KLDev {
     int n = 0;
+    long long nnz = 0;  // rowptr[n]
     const int32_t* rowptr = nullptr;
     const int32_t* col = nullptr;
     const float* w = nullptr;
@@ -177,11 +178,11 @@ struct KLDev {
     KLInfo* cinfo1 = nullptr;
     // per CSR entry p: the neighbour's descriptor {col[p], rowptr, rowlen, plist}
     const KLInfo* aux = nullptr;
-    // per CSR entry p: the first 16 {col, w} entries of row col[p], 8 x 16 B
-    // (KL_SEG_LANES lanes each load one); null when it would not fit
+    // per CSR entry p: the first 2*KL_SEG_LANES {col, w} entries of row col[p]
+    // as KL_SEG_LANES 16-B pieces (zero-padded); null when it would not fit
     const KLInfo* seg = nullptr;
 };
-constexpr int KL_SEG_LANES = 8;
+constexpr int KL_SEG_LANES = 16;  // 16-B pieces of 2 entries: 32 entries inline (all but 0.05% of touched rows)
 constexpr int KL_ITEM_CAP = 1024;  // affected rows whose new key/descriptor are kept in LDS
 // LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
 // chunk winners on chip (0 when they do not fit: global-state mode).
@@ -191,7 +192,8 @@ struct KLOut {
     long long best_iter;
     float initial_cut, best_cut, final_cut;
     unsigned int status;
-    unsigned long long prof[10];  // EK_KL_PROF: [0..7] 100 MHz ticks per loop phase (thread 0's view),
+    unsigned long long prof[16];  // EK_KL_PROF: [0..11] 100 MHz ticks per loop phase (thread 0's view)
+                                  // or event counts x100, [14] shader cycles, [15] 100 MHz ticks of the loop;
                                   // [8] shader cycles, [9] 100 MHz ticks of the whole loop
 };
 void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk keys

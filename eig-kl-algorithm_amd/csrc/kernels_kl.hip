@@ -16,11 +16,11 @@
 //   * k_gain_scan   : one lane per row (the sequential fp32 order forbids
 //                     splitting a row), all n rows; also fp64 per-block
 //                     partials of the initial cut.
-//   * k_chunk_init  : one wave64 per 256-position chunk of each remain[]
+//   * k_chunk_init  : one wave64 per KL_CHUNK-position chunk of each remain[]
 //                     list; the chunk's best (gain, first position) packed in
 //                     a 64-bit key whose unsigned max IS the cKL selection
 //                     rule, so a wave64 shuffle max is an exact argmax.
-//   * k_kl_loop     : the whole swap loop in ONE persistent 1024-thread
+//   * k_kl_swap_loop: the whole swap loop in ONE persistent 1024-thread
 //                     workgroup (no grid-wide sync, no host round trip per
 //                     iteration — the reference gKL paid 2 launches + PCIe
 //                     copies of remain and membership per iteration,
@@ -100,6 +100,12 @@ __device__ __forceinline__ u64 wave_max_u64(u64 v) {
     return v;
 }
 
+// uniform broadcast of lane `l` (v_readlane: no LDS round trip, unlike __shfl)
+__device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
+    const unsigned lo = __builtin_amdgcn_readlane(unsigned(v), l), hi = __builtin_amdgcn_readlane(unsigned(v >> 32), l);
+    return (u64(hi) << 32) | lo;
+}
+
 // side of node v (0/1): LDS bitmap or global byte array
 template <bool SMEM>
 __device__ __forceinline__ uint32_t side_of(const uint32_t* s_side, const uint8_t* g_side, int v) {
@@ -124,7 +130,7 @@ __device__ __forceinline__ float row_gain(const int32_t* __restrict__ rowptr, co
     return external - internal;
 }
 
-// best key of 256 consecutive positions of one remain[] list (gains by
+// best key of KL_CHUNK consecutive positions of one remain[] list (gains by
 // position).  The gain arrays are padded with NaN (invalid key) to a whole
 // number of chunks, so every load is unconditional and all are in flight at once.
 __device__ __forceinline__ u64 chunk_key(const float* __restrict__ gp, int s, int c, int lane) {
@@ -226,85 +232,108 @@ __global__ __launch_bounds__(256) void k_chunk_init(KLDev d) {
     }
 }
 
-// chunk-key arrays the selection reads are padded with zero keys to whole
-// SEL_UNROLL*64 blocks (both lists to the same count), so it issues all of a
-// lane's reads before the first compare
-constexpr int KL_SEL_UNROLL = 8;
+// chunk-key arrays the selection reads are padded with zero keys to a whole
+// number of 32-lane passes (both lists to the same count): every wave reduces
+// all of them itself, one half-wave per list
 __host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
     const int m = nck0 > nck1 ? nck0 : nck1;
-    return (m + KL_SEL_UNROLL * 64 - 1) / (KL_SEL_UNROLL * 64) * (KL_SEL_UNROLL * 64);
+    return (m + 31) / 32 * 32;
 }
 
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
-    const size_t b = (size_t(d.nck0) + size_t(d.nck1)) * (sizeof(KLInfo) + 8 + 4 + 4) +
-                     2 * size_t(kl_sel_pad(d.nck0, d.nck1)) * 8 + 2 * (KL_LOOP_THREADS / 64) * 8 +
-                     size_t(KL_ITEM_CAP) * (sizeof(KLInfo) + 8 + 4) + 16 + 2 * words * 4 + 64;
+    const size_t nck = size_t(d.nck0) + size_t(d.nck1);
+    const size_t b = (nck + KL_ITEM_CAP + 2 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_SEG_LANES) * sizeof(KLInfo) +
+                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 2) * 8 +
+                     (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4;
     return b <= 152 * 1024 ? b : 0;
 }
 
-// Row gain with the side bitmap in LDS; the row's col/w are fetched 32 at a
-// time (independent loads in flight: one round trip for almost every row)
-// and then summed strictly in row order.
-__device__ __forceinline__ float row_gain_lds(const int32_t* __restrict__ col, const float* __restrict__ w,
-                                              const uint32_t* s_side, int rp, int len) {
-    constexpr int B = 32;
-    float internal = 0.0f, external = 0.0f;
-    const int e = rp + len;
-    for (int p = rp; p < e; p += B) {
-        int cc[B];
-        float ww[B];
+// Best key of chunk c of one remain[] list over its positions other than
+// `skip` (gains by position; the arrays are padded, so the loads are
+// unconditional and all in flight at once).  Every lane gets the key; the
+// winner lane (lane 0 for an all-invalid chunk) has *mine set and loads the
+// winner's row descriptor into *info.
+__device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
+                                            int c, int skip, int lane, KLInfo* info, bool* mine) {
+    float g[KL_CHUNK / 64];
 #pragma unroll
-        for (int j = 0; j < B; ++j) {
-            cc[j] = p + j < e ? col[p + j] : 0;
-            ww[j] = p + j < e ? w[p + j] : 0.0f;
-        }
+    for (int q = 0; q < KL_CHUNK / 64; ++q) g[q] = gp[c * KL_CHUNK + q * 64 + lane];
+    u64 k = 0ull;
+    int bp = 0;
 #pragma unroll
-        for (int j = 0; j < B; ++j) {
-            if (p + j < e) {
-                if (((s_side[cc[j] >> 5] >> (cc[j] & 31)) & 1u) == 0) internal += ww[j];
-                else external += ww[j];
-            }
+    for (int q = 0; q < KL_CHUNK / 64; ++q) {
+        const int p = c * KL_CHUNK + q * 64 + lane;
+        const u64 kk = p == skip ? 0ull : (s ? key_min(g[q], p) : key_max(g[q], p));
+        if (kk > k) {
+            k = kk;
+            bp = p;
         }
     }
-    return external - internal;
+    const u64 m = wave_max_u64(k);
+    const u64 bal = __ballot(m != 0ull && k == m);  // keys carry the position: one lane at most
+    *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
+    KLInfo inf{0, 0, 0, 0};
+    if (bal && *mine) {
+        const int4 x = *reinterpret_cast<const int4*>(pinfo + bp);
+        inf = KLInfo{x.x, x.y, x.z, x.w};
+    }
+    *info = inf;
+    return m;
 }
 
-// The swap loop (cKL.cpp:334-390) in ONE persistent workgroup, on-chip state:
-// LDS holds the side/locked bitmaps, every chunk's best key AND its winner's
-// row descriptor {node, rowptr, rowlen}, and the affected-chunk list.  Every
-// wave performs the selection itself from LDS (no barrier), so a swap costs
-// two workgroup barriers and four dependent global round trips: row of node1
-// (edge weight), descriptor + row of each affected node (gain), and the
-// gains + descriptors of each re-keyed chunk.
+// The swap loop (cKL.cpp:334-390) in ONE persistent 1024-thread workgroup,
+// its state on chip: LDS holds the side/locked bitmaps, every chunk's best key
+// and its winner's row descriptor {node, rowptr, rowlen}.  Per swap:
+//   S   every wave selects node1 / node2 itself from the chunk keys (a few
+//       keys per lane, DPP + permlane reductions per half-wave): no barrier;
+//   W   the last wave: w(node1, node2), pair gain, running cut, log, stop rule;
+//   E   two waves rescan the chunks node1 and node2 leave (they were those
+//       chunks' winners) CONCURRENTLY with G1, off its dependency chain;
+//   G1  the other waves recompute the gains of N(node1) u N(node2) (one lane
+//       per row, the reference's sequential fp32 order) and merge the risen
+//       keys of every other chunk into shadow keys (LDS atomicMax);
+//   --- barrier ---
+//   G2  resolve node1's / node2's chunk from the early rescan and the new keys
+//       of the updated rows in it, publish merged keys, rescan the (rare)
+//       chunks whose winner fell;
+//   --- barrier ---
+// Early-rescan rule: the rescan skips node1 (node2) and may read either the
+// old or the new gain of a row G1 updates meanwhile.  If its winner R is not
+// such a row, the chunk's key is exactly max(R, new keys of the updated rows
+// in the chunk); if R is one whose new key is below R, R was a stale value and
+// the chunk is rescanned after the barrier.
 template <bool PROF>
-__global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int limit, ek_swap* __restrict__ log,
-                                                                 long long cap, KLOut* __restrict__ out) {
+__global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int limit, ek_swap* __restrict__ log,
+                                                                  long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
+    constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = NW - 3, NG = NW - 3;  // waves 0 .. NG-1 run G1
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nckp = kl_sel_pad(d.nck0, d.nck1);
-    const bool wlead = tid == (NW - 1) * 64;  // owns the loop-carried scalars (cut, best, stop counter)
+    const int half = lane >> 5, hl = lane & 31;
+    const int nsel = kl_sel_pad(d.nck0, d.nck1);
     const int words = (d.n + 31) / 32;
     // LDS carve (kl_loop_lds_bytes): 16-B records first, then 8-B, then 4-B
     KLInfo* ci0 = reinterpret_cast<KLInfo*>(smem);  // chunk winners' descriptors
     KLInfo* ci1 = ci0 + d.nck0;
-    KLInfo* it_info = ci1 + d.nck1;                   // per affected row: its descriptor
-    u64* ck0 = reinterpret_cast<u64*>(it_info + KL_ITEM_CAP);  // chunk keys (read by the selection)
-    u64* ck1 = ck0 + nckp;     // (both padded to nckp with zero keys)
-    u64* ckn0 = ck1 + nckp;    // shadow keys: G1 merges risen keys here, G2 publishes them to ck
+    KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
+    KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2] early-rescan winners
+    int4* sg_stage = reinterpret_cast<int4*>(er_info + 2);  // [NG][8 rows][KL_SEG_LANES] G1 segment staging
+    u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * 8 * KL_SEG_LANES);  // chunk keys (zero-padded to nsel)
+    u64* ck1 = ck0 + nsel;
+    u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
     u64* ckn1 = ckn0 + d.nck0;
-    u64* it_key = ckn1 + d.nck1;                                // per affected row: its new key
-    u64* sel_part = it_key + KL_ITEM_CAP;                       // [2][NW] per-wave selection partials
-    int* dtag0 = reinterpret_cast<int*>(sel_part + 2 * NW);     // iteration that tagged a rescan
+    u64* it_key = ckn1 + d.nck1;           // per updated row: its new key
+    u64* er_key = it_key + KL_ITEM_CAP;     // [2] early-rescan keys
+    int* dtag0 = reinterpret_cast<int*>(er_key + 2);  // iteration that tagged a late rescan
     int* dtag1 = dtag0 + d.nck0;
-    int* ctag0 = dtag1 + d.nck1;                               // iteration that claimed the rescan
+    int* ctag0 = dtag1 + d.nck1;  // iteration that claimed it
     int* ctag1 = ctag0 + d.nck0;
-    int* it_cs = ctag1 + d.nck1;                               // per affected row: list<<31 | chunk
-    int* s_stop = it_cs + KL_ITEM_CAP;                         // [2], by iteration parity
+    int* it_cs = ctag1 + d.nck1;  // per updated row: list << 31 | chunk (-1: locked)
+    int* s_stop = it_cs + KL_ITEM_CAP;  // [4], by iteration parity
     uint32_t* s_side = reinterpret_cast<uint32_t*>(s_stop + 4);
     uint32_t* s_lock = s_side + words;
-    for (int i = tid; i < nckp; i += KL_LOOP_THREADS) {
+    for (int i = tid; i < nsel; i += KL_LOOP_THREADS) {
         ck0[i] = i < d.nck0 ? d.ckey0[i] : 0ull;
         ck1[i] = i < d.nck1 ? d.ckey1[i] : 0ull;
     }
@@ -324,11 +353,12 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
         s_side[i] = b;
         s_lock[i] = 0u;
     }
+    if (tid < 4) s_stop[tid] = tid == 3 ? -1 : 0;
     __syncthreads();
-    float cut = *d.cut0, best = cut;  // loop-carried scalars: thread 0 only
+    float cut = *d.cut0, best = cut;  // loop-carried scalars: the W wave's lane 0 only
     long long best_it = 0, it = 0;
     unsigned term = 0;
-    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tstamp = 0;  // diagnostic build only (PROF)
+    unsigned long long tph[12] = {}, tstamp = 0;  // diagnostic build only (PROF)
     const unsigned long long c_start = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long r_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
     auto stamp = [&](int ph) {
@@ -342,34 +372,23 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     };
     for (;; ++it) {
         stamp(-1);
-        // S. selection (cKL.cpp:341-355), redundantly in every wave
-        // the waves split the chunk keys (lanes 0-31: remain[0], 32-63:
-        // remain[1]; 32 chunks per wave and pass, unconditional reads of the
-        // zero-padded arrays), reduce per half-wave, and meet at one barrier;
-        // then every wave reduces the NW partials itself
-        const int half = lane >> 5, hl = lane & 31;
+        // S. selection (cKL.cpp:341-355): lanes 0-31 reduce remain[0]'s keys,
+        // 32-63 remain[1]'s; identical in every wave
+        u64 k = 0ull;
         {
             const u64* ck = half ? ck1 : ck0;
-            u64 k = 0ull;
-            for (int c = wv * 32 + hl; c < nckp; c += NW * 32) k = ck[c] > k ? ck[c] : k;
+            for (int c = hl; c < nsel; c += 32) k = ck[c] > k ? ck[c] : k;
             k = half_max_u64(k);
-            if (hl == 0) sel_part[half * NW + wv] = k;
         }
-        __syncthreads();  // (0) selection partials
-        u64 k0, k1;
-        {
-            u64 k = hl < NW ? sel_part[half * NW + hl] : 0ull;
-            k = half_max_u64(k);
-            k0 = __shfl(k, 0, 64);
-            k1 = __shfl(k, 32, 64);
-        }
+        const u64 k0 = readlane_u64(k, 0), k1 = readlane_u64(k, 32);
         if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
         const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
-        const KLInfo ia = ci0[posA / KL_CHUNK], ib = ci1[posB / KL_CHUNK];
+        const int cA = posA / KL_CHUNK, cB = posB / KL_CHUNK;
+        const KLInfo ia = ci0[cA], ib = ci1[cB];
         const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
         stamp(0);
-        // W. swap + erase (swip, cKL.cpp:274-286): each wave applies the
-        // (idempotent) bitmap flips itself, so no barrier is needed before G
+        // swap + erase (swip, cKL.cpp:274-286): each wave applies the
+        // (idempotent) bitmap flips itself, so no barrier is needed before G1
         if (lane == 0) {
             atomicOr(&s_side[A >> 5], 1u << (A & 31));
             atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
@@ -377,8 +396,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
             atomicOr(&s_lock[B >> 5], 1u << (B & 31));
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        if (wv == NW - 1) {  // w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386);
-                             // the last wave, so the gain items (from wave 0 up) start at once
+        const int tot = la + lb;
+        const int tag = int(it);
+        if (wv == W_W) {
+            // W. w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
             float gA = 0.f, gB = 0.f;
             if (lane == 0) {
                 gA = d.gp0[posA];
@@ -396,8 +417,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
             if (lane == 0) {
                 d.gp0[posA] = __builtin_nanf("");
                 d.gp1[posB] = __builtin_nanf("");
-                dtag0[posA / KL_CHUNK] = int(it);  // A and B were their chunks' winners
-                dtag1[posB / KL_CHUNK] = int(it);
                 const float gain = gA - gB - 2.0f * wab;
                 cut -= gain;
                 if (cut < best) {
@@ -415,85 +434,119 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
                 if (it + 1 >= d.n0 || it + 1 >= d.n1) stop = 1;  // a remain[] list is exhausted
                 s_stop[it & 1] = stop;
             }
-        }
-        stamp(1);
-        // G1. gains of N(A) u N(B) (updateAffectedNodeGains, cKL.cpp:253-272),
-        //     keeping the chunk keys exact incrementally: a risen key is merged
-        //     with an LDS atomicMax (its descriptor is written in G2 if it won);
-        //     a chunk whose winner fell (or was erased: A's, B's) is tagged for a
-        //     full rescan.  Chunks keys are exact at every iteration start, so
-        //     max(old key, risen keys) is exact for untagged chunks.
-        const int tot = la + lb;
-        const int tag = int(it);
-        // one lane per affected row: the neighbour's descriptor {node,
-        // rowptr, len, plist} (aux) and its first 16 {col, w} entries (seg)
-        // are both addressed by the CSR position alone, so every load of the
-        // row is issued at once; the sums run strictly in row order, the
-        // zero-weight padding of short segments adds exact zeros
-        for (int i = tid; i < tot; i += KL_LOOP_THREADS) {
-            const int p = i < la ? pa + i : pb + i - la;
-            const int4 a = *reinterpret_cast<const int4*>(d.aux + p);
-            int4 sg[KL_SEG_LANES];
-            if (d.seg) {
-#pragma unroll
-                for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = *reinterpret_cast<const int4*>(d.seg + size_t(p) * KL_SEG_LANES + j);
+        } else if (wv == W_EA || wv == W_EB) {
+            // E. early rescan of the chunk node1 (node2) leaves
+            const int s = wv == W_EB ? 1 : 0;
+            KLInfo info;
+            bool mine;
+            const u64 kk = s ? chunk_rescan(d.gp1, d.pinfo1, 1, cB, posB, lane, &info, &mine)
+                             : chunk_rescan(d.gp0, d.pinfo0, 0, cA, posA, lane, &info, &mine);
+            if (mine) {
+                er_key[s] = kk;
+                er_info[s] = info;
             }
-            const int u = a.x, rp = a.y, len = a.z;
-            const bool act = !((s_lock[u >> 5] >> (u & 31)) & 1u);
-            stamp(2);
-            float internal = 0.0f, external = 0.0f;
-            if (act) {
-                int q = 0;
+        } else {
+            // G1. gains of N(A) u N(B) (updateAffectedNodeGains, cKL.cpp:253-272):
+            // one lane per row; the neighbour's descriptor {node, rowptr, len,
+            // plist} (aux) and its first 32 {col, w} entries (seg) are both
+            // addressed by the CSR position alone, so every load of the row is
+            // issued at once; the sums run strictly in row order, the
+            // zero-weight padding of short segments adds exact zeros
+            int4* stage = sg_stage + wv * 8 * KL_SEG_LANES;  // this wave's 8 rows x KL_SEG_LANES pieces
+            for (int i0 = wv * 8; i0 < tot; i0 += NG * 8) {
+                // 8 lanes per row, each loading 16-B pieces j8, j8 + 8, ... of the
+                // row's inline segment: each instruction touches each 128-B line
+                // once.  (One lane loading all pieces of a line issues them as
+                // separate instructions on the same line, and each waits for the
+                // previous one's miss: serial L2 trips.)
+                constexpr int PPL = KL_SEG_LANES / 8;  // pieces per lane
+                const int gi = i0 + (lane >> 3), j8 = lane & 7;
+                const int pg = gi < tot ? (gi < la ? pa + gi : pb + gi - la) : pa;
+                int4 piece[PPL];
+#pragma unroll
+                for (int r = 0; r < PPL; ++r)
+                    piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
+                                     : make_int4(0, 0, 0, 0);
+                const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
                 if (d.seg) {
 #pragma unroll
-                    for (int j = 0; j < KL_SEG_LANES; ++j) {
-                        const float w0 = __int_as_float(sg[j].y), w1 = __int_as_float(sg[j].w);
-                        const bool e0 = (s_side[sg[j].x >> 5] >> (sg[j].x & 31)) & 1u;
-                        const bool e1 = (s_side[sg[j].z >> 5] >> (sg[j].z & 31)) & 1u;
-                        internal += e0 ? 0.0f : w0;
-                        external += e0 ? w0 : 0.0f;
-                        internal += e1 ? 0.0f : w1;
-                        external += e1 ? w1 : 0.0f;
-                    }
-                    q = 2 * KL_SEG_LANES;
+                    for (int r = 0; r < PPL; ++r) stage[(lane >> 3) * KL_SEG_LANES + j8 + 8 * r] = piece[r];
                 }
-                for (; q < len; q += 16) {  // beyond the inline segment: 16 loads in flight per pass
-                    int cc[16];
-                    float ww[16];
+                if (j8 != 0 || gi >= tot) continue;  // the row's first lane sums it
+                const int i = gi, p = pg;
+                int4 sg[KL_SEG_LANES];
+                if (d.seg) {
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) {  // col/w carry 16 zero entries of tail padding
-                        cc[k] = d.col[rp + q + k];
-                        ww[k] = q + k < len ? d.w[rp + q + k] : 0.0f;
+                    for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_SEG_LANES + j];
+                }
+                const int u = a.x, rp = a.y, len = a.z;
+                const bool act = !((s_lock[u >> 5] >> (u & 31)) & 1u);
+                stamp(6);
+                float internal = 0.0f, external = 0.0f;
+                {  // summed whether or not u is locked: a branch on `act` would let the
+                   // compiler sink the segment loads behind the descriptor's round trip
+                    int q = 0;
+                    if (d.seg) {
+#pragma unroll
+                        for (int j = 0; j < KL_SEG_LANES; ++j) {
+                            const float w0 = __int_as_float(sg[j].y), w1 = __int_as_float(sg[j].w);
+                            const bool e0 = (s_side[sg[j].x >> 5] >> (sg[j].x & 31)) & 1u;
+                            const bool e1 = (s_side[sg[j].z >> 5] >> (sg[j].z & 31)) & 1u;
+                            internal += e0 ? 0.0f : w0;
+                            external += e0 ? w0 : 0.0f;
+                            internal += e1 ? 0.0f : w1;
+                            external += e1 ? w1 : 0.0f;
+                        }
+                        q = 2 * KL_SEG_LANES;
                     }
+                    if constexpr (PROF) {
+                        if (q < len) atomicAdd(&s_stop[2], 1);
+                    }
+                    for (; q < len; q += 16) {  // beyond the inline segment: 16 loads in flight per pass
+                        int cc[16];
+                        float ww[16];
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        cc[k] = q + k < len ? cc[k] : 0;
-                        const bool e = (s_side[cc[k] >> 5] >> (cc[k] & 31)) & 1u;
-                        internal += e ? 0.0f : ww[k];
-                        external += e ? ww[k] : 0.0f;
+                        for (int k2 = 0; k2 < 16; ++k2) {  // col/w carry 16 zero entries of tail padding
+                            cc[k2] = d.col[rp + q + k2];
+                            ww[k2] = q + k2 < len ? d.w[rp + q + k2] : 0.0f;
+                        }
+#pragma unroll
+                        for (int k2 = 0; k2 < 16; ++k2) {
+                            cc[k2] = q + k2 < len ? cc[k2] : 0;
+                            const bool e = (s_side[cc[k2] >> 5] >> (cc[k2] & 31)) & 1u;
+                            internal += e ? 0.0f : ww[k2];
+                            external += e ? ww[k2] : 0.0f;
+                        }
                     }
                 }
-            }
-            stamp(3);
-            {
+                if constexpr (PROF) {
+                    if (tid == 0 && internal == -1.0f) s_stop[2] = 0;  // keeps the sums ahead of the stamp
+                }
+                stamp(7);
                 int cs = -1;
                 u64 kn = 0ull;
                 KLInfo inf{0, 0, 0, 0};
                 if (act) {
                     const float g = external - internal;
                     const uint32_t pl = uint32_t(a.w);
-                    const int s = int(pl >> 31), p = int(pl & 0x7fffffffu), c = p / KL_CHUNK;
-                    (s ? d.gp1 : d.gp0)[p] = g;
-                    kn = s ? key_min(g, p) : key_max(g, p);
-                    const u64 K = (s ? ck1 : ck0)[c];  // stable during the iteration (other waves may still select)
-                    if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(p) && kn < K) {
-                        (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
-                    } else if (kn > K) {
-                        atomicMax(&(s ? ckn1 : ckn0)[c], kn);
-                        if (i >= KL_ITEM_CAP) (s ? dtag1 : dtag0)[c] = tag;  // no LDS slot for its descriptor
+                    const int s = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / KL_CHUNK;
+                    (s ? d.gp1 : d.gp0)[pp] = g;
+                    kn = s ? key_min(g, pp) : key_max(g, pp);
+                    if (!(s ? c == cB : c == cA)) {  // node1's / node2's chunk: resolved in G2
+                        const u64 K = (s ? ck1 : ck0)[c];  // stable until the barrier
+                        if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(pp) && kn < K) {
+                            (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
+                            s_stop[3] = tag;
+                        } else if (kn > K) {
+                            atomicMax(&(s ? ckn1 : ckn0)[c], kn);
+                            if (i >= KL_ITEM_CAP) {  // no LDS slot for its descriptor
+                                (s ? dtag1 : dtag0)[c] = tag;
+                                s_stop[3] = tag;
+                            }
+                        }
                     }
                     cs = int((pl & 0x80000000u) | uint32_t(c));
-                    inf = KLInfo{u, rp, len, 0};
+                    inf = KLInfo{u, rp, len, pp};
                 }
                 if (i < KL_ITEM_CAP) {
                     it_key[i] = kn;
@@ -502,50 +555,115 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
                 }
             }
         }
-        stamp(4);
-        __syncthreads();  // (1) gains, merged keys and rescan tags visible
-        stamp(5);
-        // G2. publish merged keys of untagged chunks (every item of the chunk
-        // writes the same value) and the descriptor of the item that won ...
+        stamp(1);
+        __syncthreads();  // (1) gains, early rescans, merged keys and tags visible
+        stamp(2);
+        // G2a. node1's and node2's chunks: one wave (lanes 0-31 list 0, 32-63
+        // list 1), beside G2b/G2c in the others
+        if (wv == W_EA) {
+            const int s = half, cS = s ? cB : cA;
+            const u64 R = er_key[s];
+            const int Rpos = int(~uint32_t(R & 0xffffffffull));  // meaningless when R == 0 (never matched)
+            u64 bk = 0ull;
+            int bi = 0;
+            bool stale = false;
+            const int ni = tot < KL_ITEM_CAP ? tot : KL_ITEM_CAP;
+            for (int i = hl; i < ni; i += 32) {
+                const int cs = it_cs[i];
+                if (cs == -1 || int(uint32_t(cs) >> 31) != s || (cs & 0x7fffffff) != cS) continue;
+                const u64 kn = it_key[i];
+                if (R != 0ull && it_info[i].d == Rpos && kn < R) stale = true;
+                if (kn > bk) {
+                    bk = kn;
+                    bi = i;
+                }
+            }
+            const u64 m = half_max_u64(bk);
+            const u64 hmask = s ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+            const bool st = (__ballot(stale) & hmask) != 0ull || tot > KL_ITEM_CAP;
+            // readlane needs a wave-uniform lane: take both halves' winners, then pick
+            const u64 wb = __ballot(m != 0ull && bk == m);
+            const u64 wb0 = wb & 0x00000000ffffffffull, wb1 = wb & 0xffffffff00000000ull;
+            const int wbi0 = __builtin_amdgcn_readlane(bi, wb0 ? __ffsll((long long)wb0) - 1 : 0);
+            const int wbi1 = __builtin_amdgcn_readlane(bi, wb1 ? __ffsll((long long)wb1) - 1 : 32);
+            const int wbi = s ? wbi1 : wbi0;
+            if (hl == 0 && !st) {
+                u64 nk;
+                KLInfo nf;
+                if (m > R) {
+                    nk = m;
+                    nf = it_info[wbi];
+                } else {
+                    nk = R;
+                    nf = er_info[s];
+                }
+                (s ? ck1 : ck0)[cS] = nk;
+                (s ? ckn1 : ckn0)[cS] = nk;
+                (s ? ci1 : ci0)[cS] = nf;
+            }
+            // a stale early rescan (or a hub beyond the item list): full
+            // rescan now that every new gain (and node1/node2's NaN) is stored
+            const bool stA = __builtin_amdgcn_readlane(int(st), 0) != 0, stB = __builtin_amdgcn_readlane(int(st), 32) != 0;
+            if constexpr (PROF) {
+                if (lane == 0) atomicAdd(&s_stop[2], 1000000 * (int(stA) + int(stB)));  // stale counts in the high digits
+            }
+            for (int q = 0; q < 2; ++q) {
+                if (!(q ? stB : stA)) continue;
+                KLInfo info;
+                bool mine;
+                const u64 kk = q ? chunk_rescan(d.gp1, d.pinfo1, 1, cB, -1, lane, &info, &mine)
+                                 : chunk_rescan(d.gp0, d.pinfo0, 0, cA, -1, lane, &info, &mine);
+                if (mine) {
+                    (q ? ck1 : ck0)[q ? cB : cA] = kk;
+                    (q ? ckn1 : ckn0)[q ? cB : cA] = kk;
+                    (q ? ci1 : ci0)[q ? cB : cA] = info;
+                }
+            }
+        }
+        stamp(3);
+        // G2b. publish merged keys of the other untagged chunks (every item of
+        // a chunk writes the same value) and the descriptor of the item that won
         for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
             const int cs = it_cs[i];
             if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
             const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
-            if ((s ? dtag1 : dtag0)[c] == tag) continue;
+            if ((s ? c == cB : c == cA) || (s ? dtag1 : dtag0)[c] == tag) continue;
             const u64 kmerged = (s ? ckn1 : ckn0)[c];
             (s ? ck1 : ck0)[c] = kmerged;
             if (kmerged == it_key[i]) (s ? ci1 : ci0)[c] = it_info[i];
         }
-        // ... and full rescans of the tagged chunks (one wave each, claimed once)
-        for (int i = wv; i < tot + 2; i += NW) {
+        // G2c. full rescans of the tagged chunks (one wave each, claimed once);
+        // s_stop[3] holds the last iteration that tagged any
+        for (int i = wv; i < tot && s_stop[3] == tag; i += NW) {
             int cs;
-            if (i == tot) cs = posA / KL_CHUNK;
-            else if (i == tot + 1) cs = int(0x80000000u | uint32_t(posB / KL_CHUNK));
-            else if (i < KL_ITEM_CAP) cs = it_cs[i];
+            if (i < KL_ITEM_CAP) cs = it_cs[i];
             else {  // beyond the LDS item list (hubs): rederive
                 const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
                 cs = ((s_lock[u >> 5] >> (u & 31)) & 1u) ? -1 : int((uint32_t(d.nd[u].c) & 0x80000000u) |
                                                                      ((uint32_t(d.nd[u].c) & 0x7fffffffu) / KL_CHUNK));
             }
-            if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
+            if (cs == -1) continue;
             const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
-            if ((s ? dtag1 : dtag0)[c] != tag) continue;
+            if ((s ? dtag1 : dtag0)[c] != tag) continue;  // node1's / node2's chunks are never tagged
             int claimed = 0;
             if (lane == 0) claimed = atomicMax(&(s ? ctag1 : ctag0)[c], tag) < tag;
             if (!__shfl(claimed, 0, 64)) continue;
+            if constexpr (PROF) {
+                if (lane == 0) atomicAdd(&s_stop[2], 1);  // late rescans in the low digits
+            }
             KLInfo info;
             bool mine;
-            const u64 k = s ? chunk_best(d.gp1, d.pinfo1, 1, c, lane, &info, &mine)
-                            : chunk_best(d.gp0, d.pinfo0, 0, c, lane, &info, &mine);
+            const u64 kk = s ? chunk_rescan(d.gp1, d.pinfo1, 1, c, -1, lane, &info, &mine)
+                             : chunk_rescan(d.gp0, d.pinfo0, 0, c, -1, lane, &info, &mine);
             if (mine) {
-                (s ? ck1 : ck0)[c] = k;
-                (s ? ckn1 : ckn0)[c] = k;
+                (s ? ck1 : ck0)[c] = kk;
+                (s ? ckn1 : ckn0)[c] = kk;
                 (s ? ci1 : ci0)[c] = info;
             }
         }
-        stamp(6);
+        stamp(4);
         __syncthreads();  // (2) keys visible to the next selection
-        stamp(7);
+        stamp(5);
         if (s_stop[it & 1]) {
             ++it;
             break;
@@ -553,7 +671,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
     }
     __syncthreads();
     for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
-    if (wlead) {
+    if (wv == W_W && lane == 0) {
         out->iterations = it;
         out->best_iter = best_it;
         out->initial_cut = *d.cut0;
@@ -562,9 +680,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop_lds(KLDev d, int li
         out->status = 2u;
     }
     if (tid == 0) {  // phase stamps are taken by thread 0
-        for (int i = 0; i < 8; ++i) out->prof[i] = tph[i];
-        out->prof[8] = PROF ? __builtin_amdgcn_s_memtime() - c_start : 0ull;
-        out->prof[9] = PROF ? __builtin_amdgcn_s_memrealtime() - r_start : 0ull;
+        if constexpr (PROF) {
+            tph[8] = 100ull * (unsigned long long)(s_stop[2] / 1000000);
+            tph[9] = 100ull * (unsigned long long)(s_stop[2] % 1000000);
+        }
+        for (int i = 0; i < 12; ++i) out->prof[i] = tph[i];
+        out->prof[14] = PROF ? __builtin_amdgcn_s_memtime() - c_start : 0ull;
+        out->prof[15] = PROF ? __builtin_amdgcn_s_memrealtime() - r_start : 0ull;
     }
 }
 
@@ -721,6 +843,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
         out->final_cut = cut;
         out->status = SMEM ? 1u : 0u;
         for (int i = 0; i < 4; ++i) out->prof[i] = tph[i];  // global-state loop: 4 phases
+        for (int i = 4; i < 16; ++i) out->prof[i] = 0ull;
     }
 }
 
@@ -766,14 +889,14 @@ __global__ __launch_bounds__(256) void k_build_aux(long long nnz, const int32_t*
     *reinterpret_cast<int4*>(aux + p) = make_int4(v, x.x, x.y, x.z);
 }
 
-// seg[p*8 + j] = entries 2j, 2j+1 of row col[p] as {col, w bits, col, w bits} (0 past its end)
+// seg[p*KL_SEG_LANES + j] = entries 2j, 2j+1 of row col[p] as {col, w bits, col, w bits} (0 past its end)
 __global__ __launch_bounds__(256) void k_build_seg(long long nnz, const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col, const float* __restrict__ w,
                                                    KLInfo* __restrict__ seg) {
     const long long t = blockIdx.x * 256ll + threadIdx.x;
-    const long long p = t >> 3;
+    const long long p = t / KL_SEG_LANES;
     if (p >= nnz) return;
-    const int j = int(t & 7), v = col[p];
+    const int j = int(t % KL_SEG_LANES), v = col[p];
     const int rp = rowptr[v], len = rowptr[v + 1] - rp;
     const int e0 = 2 * j, e1 = 2 * j + 1;
     int4 o = make_int4(0, 0, 0, 0);
@@ -795,7 +918,7 @@ void kl_build_aux(hipStream_t s, int64_t nnz, const int32_t* col, const KLInfo* 
 
 void kl_build_seg(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* w, KLInfo* seg) {
     if (nnz <= 0) return;
-    hipLaunchKernelGGL(k_build_seg, dim3(unsigned((nnz * 8 + 255) / 256)), dim3(256), 0, s, (long long)nnz, rowptr,
+    hipLaunchKernelGGL(k_build_seg, dim3(unsigned((nnz * KL_SEG_LANES + 255) / 256)), dim3(256), 0, s, (long long)nnz, rowptr,
                        col, w, seg);
 }
 
@@ -812,9 +935,9 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
     const bool prof = std::getenv("EK_KL_PROF") != nullptr;  // phase stamps: diagnostic instantiation
     const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
     if (lds && !global_state && prof)
-        hipLaunchKernelGGL((k_kl_loop_lds<true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        hipLaunchKernelGGL((k_kl_swap_loop<true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
     else if (lds && !global_state)
-        hipLaunchKernelGGL((k_kl_loop_lds<false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        hipLaunchKernelGGL((k_kl_swap_loop<false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
     else if (prof)
         hipLaunchKernelGGL((k_kl_loop<false, true>), dim3(1), dim3(KL_LOOP_THREADS), 0, s, d, limit, log, cap, out);
     else

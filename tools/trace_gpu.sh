@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$TAG" -o "$TAG" \
-    -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/${TAG}.log" 2>&1
+    -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-sweep >"$OUT/${TAG}.log" 2>&1
 python3 - "$OUT/$TAG/${TAG}_kernel_stats.csv" <<'PY'
 import csv, sys
 for r in list(csv.DictReader(open(sys.argv[1])))[:14]:
