@@ -487,15 +487,22 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                    // compiler sink the segment loads behind the descriptor's round trip
                     int q = 0;
                     if (d.seg) {
+                        // 8 entries per block; a block no row of this wave reaches
+                        // is skipped as a whole (wave-uniform branch): the loop is
+                        // issue-bound, and the zero padding would add exact zeros
 #pragma unroll
-                        for (int j = 0; j < KL_SEG_LANES; ++j) {
-                            const float w0 = __int_as_float(sg[j].y), w1 = __int_as_float(sg[j].w);
-                            const bool e0 = (s_side[sg[j].x >> 5] >> (sg[j].x & 31)) & 1u;
-                            const bool e1 = (s_side[sg[j].z >> 5] >> (sg[j].z & 31)) & 1u;
-                            internal += e0 ? 0.0f : w0;
-                            external += e0 ? w0 : 0.0f;
-                            internal += e1 ? 0.0f : w1;
-                            external += e1 ? w1 : 0.0f;
+                        for (int b = 0; b < KL_SEG_LANES / 4; ++b) {
+                            if (!__ballot(len > 8 * b)) break;
+#pragma unroll
+                            for (int j = 4 * b; j < 4 * b + 4; ++j) {
+                                const float w0 = __int_as_float(sg[j].y), w1 = __int_as_float(sg[j].w);
+                                const bool e0 = (s_side[sg[j].x >> 5] >> (sg[j].x & 31)) & 1u;
+                                const bool e1 = (s_side[sg[j].z >> 5] >> (sg[j].z & 31)) & 1u;
+                                internal += e0 ? 0.0f : w0;
+                                external += e0 ? w0 : 0.0f;
+                                internal += e1 ? 0.0f : w1;
+                                external += e1 ? w1 : 0.0f;
+                            }
                         }
                         q = 2 * KL_SEG_LANES;
                     }
