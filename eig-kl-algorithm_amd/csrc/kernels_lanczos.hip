@@ -22,6 +22,22 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// thread-strided partial of sum(x[0:n)): x[t] + x[t+256] + ... in this order,
+// with the loads batched so they are in flight together (a plain strided loop
+// waits for each load before the next add)
+__device__ __forceinline__ double strided_sum256(const double* __restrict__ x, int n) {
+    double s = 0.0;
+    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 256) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = i0 + u * 256 < n ? x[i0 + u * 256] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * 256 < n) s += v[u];
+    }
+    return s;
+}
+
 // block of 256: returns the block sum in thread 0
 __device__ __forceinline__ double block_sum256(double v, double* lds4) {
     v = wave_sum(v);
@@ -77,8 +93,14 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
 // k_reduce_cols and by the fused update alike, so both give the same bits.
 __device__ __forceinline__ double col_sum(const double* __restrict__ pj, int nrb, int half) {
     double s = 0.0;
-#pragma unroll 4
-    for (int b = half; b < nrb; b += 2) s += pj[b];
+    for (int b0 = half; b0 < nrb; b0 += 32) {  // 16 loads in flight, then the adds in order
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = b0 + 2 * u < nrb ? pj[b0 + 2 * u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (b0 + 2 * u < nrb) s += v[u];
+    }
     return s + __shfl_xor(s, 1, 64);
 }
 
@@ -145,8 +167,7 @@ __global__ __launch_bounds__(256) void k_finalize_step(const double* __restrict_
                                                        const double* __restrict__ a3, const double* __restrict__ beff_i,
                                                        const double* __restrict__ bov_i) {
     __shared__ double lds4[4];
-    double s = 0.0;
-    for (int i = threadIdx.x; i < nb; i += 256) s += npart[i];
+    double s = strided_sum256(npart, nb);
     s = block_sum256(s, lds4);
     if (threadIdx.x == 0) {
         fn2_out[0] = s;
@@ -180,8 +201,7 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
     // beta_i = ||f_i||, or 0 after an injected restart vector (override not NaN)
     const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
     if (nparts > 0) {
-        double s = 0.0;
-        for (int i = threadIdx.x; i < nparts; i += 256) s += apart[i];
+        double s = strided_sum256(apart, nparts);
         s = block_sum256(s, lds4);
         if (threadIdx.x == 0) {
             s_alpha = s;

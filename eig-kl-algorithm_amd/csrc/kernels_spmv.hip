@@ -67,10 +67,23 @@ __device__ __forceinline__ void finalize_publish(const StepFin& f, double n2) {
     }
 }
 
-// sum of x[0:n) over the workgroup in a fixed tree; every thread gets it
-__device__ __forceinline__ double block_sum_all(const double* __restrict__ x, int n, double* wsum) {
+// thread-strided partial of sum(x[0:n)): x[t] + x[t+256] + ... in order (the
+// order of k_finalize_step), loads batched so they are in flight together
+__device__ __forceinline__ double strided_sum(const double* __restrict__ x, int n) {
     double s = 0.0;
-    for (int i = threadIdx.x; i < n; i += SPMV_THREADS) s += x[i];
+    for (int i0 = threadIdx.x; i0 < n; i0 += 4 * SPMV_THREADS) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i0 + u * SPMV_THREADS < n ? x[i0 + u * SPMV_THREADS] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + u * SPMV_THREADS < n) s += v[u];
+    }
+    return s;
+}
+
+// the fixed tree over the workgroup of the thread partials; every thread gets it
+__device__ __forceinline__ double block_sum_all(double s, double* wsum) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
@@ -100,11 +113,13 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     const int r0 = dsc.x, nr = dsc.y, p0 = dsc.z, cnt = dsc.w;
     // ||f||^2: folded finalize of the previous Lanczos step (every block sums
     // the same partials in the same order; block 0 publishes) or read.  The
-    // scale is only needed by the epilogue, so in stream mode the reduction
-    // runs after the block's loads are issued (see below).
+    // partials do not depend on the block descriptor, so their loads go out
+    // first; the tree (with its barriers) runs after the block's gathers are
+    // issued, and the scale is only needed by the epilogue.
+    const double npart_t = fin.npart ? strided_sum(fin.npart, fin.nb) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
-            const double n2 = block_sum_all(fin.npart, fin.nb, wsum);
+            const double n2 = block_sum_all(npart_t, wsum);
             if (blockIdx.x == 0 && t == 0) finalize_publish(fin, n2);
             return n2;
         }
