@@ -212,7 +212,7 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": spmv_bytes, "avg_launch_us": round(spmv_launch_ms * 1e3, 3),
-                     "timing": "kernel start/end timestamps (hipExtLaunchKernelGGL events) of every SpMV in the timed solves",
+                     "timing": "kernel start/end timestamps (hipExtLaunchKernelGGL events) of every 4th SpMV of each Lanczos cycle in the timed solves",
                      "sweep": sweep},
         "cpu_baseline": cpu,
         "result": {"lambda1": lam, "lanczos_matvecs": st["matvecs"], "lanczos_restarts": st["restarts"],
