@@ -100,6 +100,25 @@ def test_kl_random_init_synthetic(ek, oracle, ctx, mult, seed):
         assert res[k] == ores[k], k
 
 
+@pytest.mark.parametrize("mode", ["EK_KL_GLOBAL_STATE", "EK_KL_NOSEG"])
+@pytest.mark.parametrize("name", ["ibm01", "industry2"])
+def test_kl_fallback_paths_bitexact(ek, oracle, ctx, monkeypatch, name, mode):
+    # the global-state loop (graphs whose on-chip state does not fit LDS) and
+    # the LDS loop without inline neighbour rows (not enough memory for them)
+    # are forced here on shipped circuits; industry2 has rows of 910 entries
+    monkeypatch.setenv(mode, "1")
+    h = ek.Hypergraph.read(circuit_path(name))
+    _, _, _, _, o0, o1 = ek.eig_read(eig_path(name), h.nodes)
+    ctx.kl_graph_setup(h.kl_graph())
+    ctx.kl_nets_setup(*h.pins())
+    ctx.kl_set_partition(o0, o1)
+    log, res = ctx.kl_run()
+    olog, ores = oracle.Graph.read(circuit_path(name)).kl(o0, o1)
+    assert res["iterations"] == ores["iterations"] == NET_CUTS[name]["iterations"]
+    _swap_fields_equal(log, olog)
+    assert res["net_cut_best"] == NET_CUTS[name]["net_cut_best"]
+
+
 def test_kl_edge_cases(ek, oracle, ctx):
     # tiny graph with repeated pins in a net, a 1-pin net, an empty net and an isolated node
     net_ptr = np.array([0, 3, 4, 4, 6, 9, 11], np.int64)
