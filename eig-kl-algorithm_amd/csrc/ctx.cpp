@@ -79,6 +79,7 @@ struct ek_ctx {
         kl_ckey0, kl_ckey1, kl_aux, kl_seg, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
     bool kl_graph_ready = false, kl_part_ready = false, kl_seg_ok = false;
     std::vector<int32_t> kl_rowptr_h;  // host copy (row descriptors)
+    std::vector<hipEvent_t> spmv_ev;   // SpMV timing events, created once per context
 };
 
 namespace {
@@ -134,6 +135,7 @@ void ek_destroy(ek_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -557,16 +559,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     HIPCHK(hipMemsetAsync(c->Vn.p, 0, c->Vn.bytes, s));
     HIPCHK(hipMemsetAsync(c->w.p, 0, c->w.bytes, s));
     if (c->nranks > 1) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
-    if (L.time_spmv) {
-        L.ev.resize(size_t(2 * m));
-        for (auto& e : L.ev) HIPCHK(hipEventCreate(&e));
-    }
-    struct EvGuard {
-        std::vector<hipEvent_t>& ev;
-        ~EvGuard() {
-            for (auto e : ev) (void)hipEventDestroy(e);
+    if (L.time_spmv) {  // created once per context: ~200 creations per solve cost milliseconds
+        while (c->spmv_ev.size() < size_t(2 * m)) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            c->spmv_ev.push_back(e);
         }
-    } evguard{L.ev};
+        L.ev.assign(c->spmv_ev.begin(), c->spmv_ev.begin() + 2 * m);
+    }
 
     // start vector: Park-Miller LCG over GLOBAL indices (identical on every
     // rank), values in [-0.5, 0.5) like Spectra's SimpleRandom; deflated.
@@ -593,8 +593,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     int k = 0, restarts = 0, nconv = 0, breakdowns = 0;
     bool converged = false;
     const double beta_eps = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
+    double host_restart_ms = 0.0, device_cycle_ms = 0.0, host_qr_ms = 0.0;  // EK_LANCZOS_TRACE diagnostics
     for (;;) {
         HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
+        const auto tc = std::chrono::steady_clock::now();
         for (int from = k;;) {
             L.factorize(from);
             L.collect_spmv_times(from);
@@ -621,6 +623,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             L.inject(j1, breakdowns);
             from = j1;
         }
+        const auto th = std::chrono::steady_clock::now();
+        device_cycle_ms += std::chrono::duration<double, std::milli>(th - tc).count();
         if (!ek::tridiag_eig(m, d.data(), e.data(), theta.data(), zl.data(), nullptr))
             ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
         const double fnorm = std::sqrt(std::max(0.0, fn2_h[size_t(m)]));
@@ -642,7 +646,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         const int knew = nev_adjusted(nev, m, nconv, zl);
         std::vector<double> Q(size_t(m) * m, 0.0), dd(d), ee(e);
         for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
+        const auto tq0 = std::chrono::steady_clock::now();
         for (int i = knew; i < m; ++i) ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q.data());
+        host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
         const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
         const double hk = ee[size_t(knew - 1)];                         // H(knew, knew-1)
         HIPCHK(hipMemcpyAsync(c->Qd.p, Q.data(), size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
@@ -656,7 +662,11 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         for (int i = 0; i < knew; ++i) d[size_t(i)] = dd[size_t(i)];
         for (int i = 0; i + 1 < knew; ++i) e[size_t(i)] = ee[size_t(i)];
         k = knew;
+        host_restart_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
     }
+    if (trace)
+        std::fprintf(stderr, "[lanczos] factorization cycles %.3f ms, restarts %.3f ms (of which QR shifts %.3f ms)\n",
+                     device_cycle_ms, host_restart_ms, host_qr_ms);
     if (!converged)
         ek::fail(EK_ENOCONV, "Eigenvalue computation failed: %d of %d Ritz pairs converged after %d restarts", nconv,
                  nev, restarts);

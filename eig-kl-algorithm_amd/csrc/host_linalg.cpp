@@ -100,10 +100,12 @@ bool tridiag_eig(int m, const double* d_in, const double* e_in, double* evals, d
 // block, which is the one that carries the residual row (Q(m-1, :)).
 void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q) {
     if (m < 2) return;
-    // dense band scratch (row-major m x m, only |i-j| <= 2 ever non-zero)
-    std::vector<double> A(size_t(m) * m, 0.0);
+    // band scratch: only |i-j| <= 2 is ever non-zero (the chase's bulge), so
+    // row i keeps columns i-2 .. i+2 (5 entries; same operations, same order
+    // as a dense matrix, without zero-filling m x m per shift)
+    std::vector<double> A(size_t(m) * 5, 0.0);
     std::vector<char> split(size_t(m), 0);  // split[p]: a block starts at p
-    auto at = [&](int i, int j) -> double& { return A[size_t(i) * m + j]; };
+    auto at = [&](int i, int j) -> double& { return A[size_t(i) * 5 + size_t(j - i + 2)]; };
     for (int i = 0; i < m; ++i) at(i, i) = d[i];
     for (int i = 0; i + 1 < m; ++i) {
         const double ei = std::fabs(e[i]) <= DBL_EPSILON * (std::fabs(d[i]) + std::fabs(d[i + 1])) ? 0.0 : e[i];
