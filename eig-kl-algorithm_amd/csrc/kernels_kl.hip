@@ -282,6 +282,37 @@ __device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const 
     return m;
 }
 
+// chunk_rescan with every position's descriptor loaded beside its gain: one
+// round trip instead of two (the early rescans run beside the gain updates and
+// must not outlast them)
+__device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
+                                             int c, int skip, int lane, KLInfo* info, bool* mine) {
+    float g[KL_CHUNK / 64];
+    int4 pi[KL_CHUNK / 64];
+#pragma unroll
+    for (int q = 0; q < KL_CHUNK / 64; ++q) {
+        const int p = c * KL_CHUNK + q * 64 + lane;
+        g[q] = gp[p];
+        pi[q] = *reinterpret_cast<const int4*>(pinfo + p);
+    }
+    u64 k = 0ull;
+    int4 bi = make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < KL_CHUNK / 64; ++q) {
+        const int p = c * KL_CHUNK + q * 64 + lane;
+        const u64 kk = p == skip ? 0ull : (s ? key_min(g[q], p) : key_max(g[q], p));
+        if (kk > k) {
+            k = kk;
+            bi = pi[q];
+        }
+    }
+    const u64 m = wave_max_u64(k);
+    const u64 bal = __ballot(m != 0ull && k == m);
+    *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
+    *info = bal ? KLInfo{bi.x, bi.y, bi.z, bi.w} : KLInfo{0, 0, 0, 0};
+    return m;
+}
+
 // The swap loop (cKL.cpp:334-390) in ONE persistent 1024-thread workgroup,
 // its state on chip: LDS holds the side/locked bitmaps, every chunk's best key
 // and its winner's row descriptor {node, rowptr, rowlen}.  Per swap:
@@ -439,8 +470,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             const int s = wv == W_EB ? 1 : 0;
             KLInfo info;
             bool mine;
-            const u64 kk = s ? chunk_rescan(d.gp1, d.pinfo1, 1, cB, posB, lane, &info, &mine)
-                             : chunk_rescan(d.gp0, d.pinfo0, 0, cA, posA, lane, &info, &mine);
+            const u64 kk = s ? chunk_rescan1(d.gp1, d.pinfo1, 1, cB, posB, lane, &info, &mine)
+                             : chunk_rescan1(d.gp0, d.pinfo0, 0, cA, posA, lane, &info, &mine);
             if (mine) {
                 er_key[s] = kk;
                 er_info[s] = info;
@@ -469,12 +500,23 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                                      : make_int4(0, 0, 0, 0);
                 const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
                 if (d.seg) {
+                    // each lane looks up the sides of its own entries (4 LDS reads
+                    // per wave instead of 32 serial ones by the summing lane) and
+                    // stages every entry's (internal, external) contribution
 #pragma unroll
-                    for (int r = 0; r < PPL; ++r) stage[(lane >> 3) * KL_SEG_LANES + j8 + 8 * r] = piece[r];
+                    for (int r = 0; r < PPL; ++r) {
+                        const int4 pc = piece[r];
+                        const bool e0 = (s_side[pc.x >> 5] >> (pc.x & 31)) & 1u;
+                        const bool e1 = (s_side[pc.z >> 5] >> (pc.z & 31)) & 1u;
+                        const float w0 = __int_as_float(pc.y), w1 = __int_as_float(pc.w);
+                        stage[(lane >> 3) * KL_SEG_LANES + j8 + 8 * r] =
+                            make_int4(__float_as_int(e0 ? 0.0f : w0), __float_as_int(e0 ? w0 : 0.0f),
+                                      __float_as_int(e1 ? 0.0f : w1), __float_as_int(e1 ? w1 : 0.0f));
+                    }
                 }
                 if (j8 != 0 || gi >= tot) continue;  // the row's first lane sums it
-                const int i = gi, p = pg;
-                int4 sg[KL_SEG_LANES];
+                const int i = gi;
+                int4 sg[KL_SEG_LANES];  // per entry pair: (internal, external) contributions
                 if (d.seg) {
 #pragma unroll
                     for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_SEG_LANES + j];
@@ -494,14 +536,11 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                         for (int b = 0; b < KL_SEG_LANES / 4; ++b) {
                             if (!__ballot(len > 8 * b)) break;
 #pragma unroll
-                            for (int j = 4 * b; j < 4 * b + 4; ++j) {
-                                const float w0 = __int_as_float(sg[j].y), w1 = __int_as_float(sg[j].w);
-                                const bool e0 = (s_side[sg[j].x >> 5] >> (sg[j].x & 31)) & 1u;
-                                const bool e1 = (s_side[sg[j].z >> 5] >> (sg[j].z & 31)) & 1u;
-                                internal += e0 ? 0.0f : w0;
-                                external += e0 ? w0 : 0.0f;
-                                internal += e1 ? 0.0f : w1;
-                                external += e1 ? w1 : 0.0f;
+                            for (int j = 4 * b; j < 4 * b + 4; ++j) {  // strictly in row order
+                                internal += __int_as_float(sg[j].x);
+                                external += __int_as_float(sg[j].y);
+                                internal += __int_as_float(sg[j].z);
+                                external += __int_as_float(sg[j].w);
                             }
                         }
                         q = 2 * KL_SEG_LANES;
