@@ -243,8 +243,8 @@ __host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
-    const size_t b = (nck + KL_ITEM_CAP + 2 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_SEG_LANES) * sizeof(KLInfo) +
-                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 2) * 8 +
+    const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_SEG_LANES) * sizeof(KLInfo) +
+                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4) * 8 +
                      (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4;
     return b <= 152 * 1024 ? b : 0;
 }
@@ -285,21 +285,23 @@ __device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const 
 // chunk_rescan with every position's descriptor loaded beside its gain: one
 // round trip instead of two (the early rescans run beside the gain updates and
 // must not outlast them)
+// (over positions [p0, p0 + 64*NQ), one of the chunk's parts)
+template <int NQ>
 __device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
-                                             int c, int skip, int lane, KLInfo* info, bool* mine) {
-    float g[KL_CHUNK / 64];
-    int4 pi[KL_CHUNK / 64];
+                                             int p0, int skip, int lane, KLInfo* info, bool* mine) {
+    float g[NQ];
+    int4 pi[NQ];
 #pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) {
-        const int p = c * KL_CHUNK + q * 64 + lane;
+    for (int q = 0; q < NQ; ++q) {
+        const int p = p0 + q * 64 + lane;
         g[q] = gp[p];
         pi[q] = *reinterpret_cast<const int4*>(pinfo + p);
     }
     u64 k = 0ull;
     int4 bi = make_int4(0, 0, 0, 0);
 #pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) {
-        const int p = c * KL_CHUNK + q * 64 + lane;
+    for (int q = 0; q < NQ; ++q) {
+        const int p = p0 + q * 64 + lane;
         const u64 kk = p == skip ? 0ull : (s ? key_min(g[q], p) : key_max(g[q], p));
         if (kk > k) {
             k = kk;
@@ -338,7 +340,11 @@ template <bool PROF>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int limit, ek_swap* __restrict__ log,
                                                                   long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
-    constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = NW - 3, NG = NW - 3;  // waves 0 .. NG-1 run G1
+    // roles: W_W the pair gain; E_PARTS waves per chunk rescan node1's chunk
+    // (waves W_EA, W_EA-1, ...) and E_PARTS node2's (W_EB, W_EB-1, ...);
+    // waves 0 .. NG-1 run the gain updates
+    constexpr int E_PARTS = 2, NQ_E = KL_CHUNK / 64 / E_PARTS;
+    constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = lane >> 5, hl = lane & 31;
@@ -348,15 +354,15 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     KLInfo* ci0 = reinterpret_cast<KLInfo*>(smem);  // chunk winners' descriptors
     KLInfo* ci1 = ci0 + d.nck0;
     KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
-    KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2] early-rescan winners
-    int4* sg_stage = reinterpret_cast<int4*>(er_info + 2);  // [NG][8 rows][KL_SEG_LANES] G1 segment staging
+    KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2][E_PARTS] early-rescan winners
+    int4* sg_stage = reinterpret_cast<int4*>(er_info + 2 * E_PARTS);  // [NG][8 rows][KL_SEG_LANES] G1 staging
     u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * 8 * KL_SEG_LANES);  // chunk keys (zero-padded to nsel)
     u64* ck1 = ck0 + nsel;
     u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
     u64* ckn1 = ckn0 + d.nck0;
     u64* it_key = ckn1 + d.nck1;           // per updated row: its new key
-    u64* er_key = it_key + KL_ITEM_CAP;     // [2] early-rescan keys
-    int* dtag0 = reinterpret_cast<int*>(er_key + 2);  // iteration that tagged a late rescan
+    u64* er_key = it_key + KL_ITEM_CAP;     // [2][E_PARTS] early-rescan keys
+    int* dtag0 = reinterpret_cast<int*>(er_key + 2 * E_PARTS);  // iteration that tagged a late rescan
     int* dtag1 = dtag0 + d.nck0;
     int* ctag0 = dtag1 + d.nck1;  // iteration that claimed it
     int* ctag1 = ctag0 + d.nck0;
@@ -465,16 +471,18 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 if (it + 1 >= d.n0 || it + 1 >= d.n1) stop = 1;  // a remain[] list is exhausted
                 s_stop[it & 1] = stop;
             }
-        } else if (wv == W_EA || wv == W_EB) {
-            // E. early rescan of the chunk node1 (node2) leaves
-            const int s = wv == W_EB ? 1 : 0;
+        } else if (wv > W_EB - E_PARTS) {
+            // E. early rescan of the chunk node1 (node2) leaves, E_PARTS waves
+            // each taking a contiguous part of it
+            const int s = wv <= W_EB ? 1 : 0, part = (s ? W_EB : W_EA) - wv;
+            const int p0 = (s ? cB : cA) * KL_CHUNK + part * NQ_E * 64;
             KLInfo info;
             bool mine;
-            const u64 kk = s ? chunk_rescan1(d.gp1, d.pinfo1, 1, cB, posB, lane, &info, &mine)
-                             : chunk_rescan1(d.gp0, d.pinfo0, 0, cA, posA, lane, &info, &mine);
+            const u64 kk = s ? chunk_rescan1<NQ_E>(d.gp1, d.pinfo1, 1, p0, posB, lane, &info, &mine)
+                             : chunk_rescan1<NQ_E>(d.gp0, d.pinfo0, 0, p0, posA, lane, &info, &mine);
             if (mine) {
-                er_key[s] = kk;
-                er_info[s] = info;
+                er_key[s * E_PARTS + part] = kk;
+                er_info[s * E_PARTS + part] = info;
             }
         } else {
             // G1. gains of N(A) u N(B) (updateAffectedNodeGains, cKL.cpp:253-272):
@@ -608,7 +616,14 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         // list 1), beside G2b/G2c in the others
         if (wv == W_EA) {
             const int s = half, cS = s ? cB : cA;
-            const u64 R = er_key[s];
+            u64 R = 0ull;  // the early rescan's key: the best of its parts
+            int rpart = 0;
+#pragma unroll
+            for (int q = 0; q < E_PARTS; ++q)
+                if (er_key[s * E_PARTS + q] > R) {
+                    R = er_key[s * E_PARTS + q];
+                    rpart = q;
+                }
             const int Rpos = int(~uint32_t(R & 0xffffffffull));  // meaningless when R == 0 (never matched)
             u64 bk = 0ull;
             int bi = 0;
@@ -641,7 +656,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     nf = it_info[wbi];
                 } else {
                     nk = R;
-                    nf = er_info[s];
+                    nf = er_info[s * E_PARTS + rpart];
                 }
                 (s ? ck1 : ck0)[cS] = nk;
                 (s ? ckn1 : ckn0)[cS] = nk;
