@@ -424,15 +424,19 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         const KLInfo ia = ci0[cA], ib = ci1[cB];
         const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
         stamp(0);
-        // swap + erase (swip, cKL.cpp:274-286): each wave applies the
-        // (idempotent) bitmap flips itself, so no barrier is needed before G1
-        if (lane == 0) {
-            atomicOr(&s_side[A >> 5], 1u << (A & 31));
-            atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
-            atomicOr(&s_lock[A >> 5], 1u << (A & 31));
-            atomicOr(&s_lock[B >> 5], 1u << (B & 31));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        // swap + erase (swip, cKL.cpp:274-286): every G1 wave applies the
+        // (idempotent) bitmap flips itself once its row loads are in flight, so
+        // no barrier is needed before its side lookups (the other roles read
+        // no bitmap before the barrier)
+        auto flip = [&]() {
+            if (lane == 0) {
+                atomicOr(&s_side[A >> 5], 1u << (A & 31));
+                atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
+                atomicOr(&s_lock[A >> 5], 1u << (A & 31));
+                atomicOr(&s_lock[B >> 5], 1u << (B & 31));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        };
         const int tot = la + lb;
         const int tag = int(it);
         if (wv == W_W) {
@@ -492,6 +496,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // issued at once; the sums run strictly in row order, the
             // zero-weight padding of short segments adds exact zeros
             int4* stage = sg_stage + wv * 8 * KL_SEG_LANES;  // this wave's 8 rows x KL_SEG_LANES pieces
+            bool flipped = false;
             for (int i0 = wv * 8; i0 < tot; i0 += NG * 8) {
                 // 8 lanes per row, each loading 16-B pieces j8, j8 + 8, ... of the
                 // row's inline segment: each instruction touches each 128-B line
@@ -507,6 +512,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
                                      : make_int4(0, 0, 0, 0);
                 const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
+                if (!flipped) {
+                    flip();
+                    flipped = true;
+                }
                 if (d.seg) {
                     // each lane looks up the sides of its own entries (4 LDS reads
                     // per wave instead of 32 serial ones by the summing lane) and
@@ -608,6 +617,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     it_info[i] = inf;
                 }
             }
+            if (!flipped) flip();  // a wave without rows (node1 and node2 may have none)
         }
         stamp(1);
         __syncthreads();  // (1) gains, early rescans, merged keys and tags visible
