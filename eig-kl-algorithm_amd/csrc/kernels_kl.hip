@@ -540,6 +540,12 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 }
                 const int u = a.x, rp = a.y, len = a.z;
                 const bool act = !((s_lock[u >> 5] >> (u & 31)) & 1u);
+                // the row's list, position, chunk and that chunk's current key
+                // depend on the descriptor only: read ahead of the sums
+                const uint32_t pl = uint32_t(a.w);
+                const int ls = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / KL_CHUNK;
+                const bool ab = ls ? c == cB : c == cA;  // node1's / node2's chunk: resolved in G2
+                const u64 K = (ls ? ck1 : ck0)[c];       // stable until the barrier
                 stamp(6);
                 float internal = 0.0f, external = 0.0f;
                 {  // summed whether or not u is locked: a branch on `act` would let the
@@ -591,12 +597,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 KLInfo inf{0, 0, 0, 0};
                 if (act) {
                     const float g = external - internal;
-                    const uint32_t pl = uint32_t(a.w);
-                    const int s = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / KL_CHUNK;
+                    const int s = ls;
                     (s ? d.gp1 : d.gp0)[pp] = g;
                     kn = s ? key_min(g, pp) : key_max(g, pp);
-                    if (!(s ? c == cB : c == cA)) {  // node1's / node2's chunk: resolved in G2
-                        const u64 K = (s ? ck1 : ck0)[c];  // stable until the barrier
+                    if (!ab) {
                         if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(pp) && kn < K) {
                             (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
                             s_stop[3] = tag;
