@@ -183,7 +183,7 @@ struct KLDev {
     const KLInfo* seg = nullptr;
 };
 constexpr int KL_SEG_LANES = 16;  // 16-B pieces of 2 entries: 32 entries inline (all but 0.05% of touched rows)
-constexpr int KL_ITEM_CAP = 1024;  // affected rows whose new key/descriptor are kept in LDS
+constexpr int KL_ITEM_CAP = 256;  // updated rows whose new key/descriptor are kept in LDS (more: rederived, tagged)
 // LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
 // chunk winners on chip (0 when they do not fit: global-state mode).
 size_t kl_loop_lds_bytes(const KLDev& d);
