@@ -113,6 +113,18 @@ __device__ __forceinline__ uint32_t side_of(const uint32_t* s_side, const uint8_
     else return g_side[v];
 }
 
+// bitmap word i of the side bytes (bit j = node 32i+j on side 1): the 32
+// bytes are read together (a byte-at-a-time loop waits for every load)
+__device__ __forceinline__ uint32_t side_word(const uint8_t* __restrict__ side, int n, int i) {
+    uint8_t v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = i * 32 + j < n ? side[i * 32 + j] : 0;
+    uint32_t b = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) b |= uint32_t(v[j] == 1) << j;
+    return b;
+}
+
 // connections(node), cKL.cpp:225-251, over the cKL-ordered row: two
 // sequential fp32 accumulators, internal = neighbour on side 0.
 template <bool SMEM>
@@ -385,9 +397,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         dtag1[i] = ctag1[i] = -1;
     }
     for (int i = tid; i < words; i += KL_LOOP_THREADS) {
-        uint32_t b = 0;
-        for (int j = 0; j < 32 && i * 32 + j < d.n; ++j) b |= uint32_t(d.side_init[i * 32 + j] == 1) << j;
-        s_side[i] = b;
+        s_side[i] = side_word(d.side_init, d.n, i);
         s_lock[i] = 0u;
     }
     if (tid < 4) s_stop[tid] = tid == 3 ? -1 : 0;
@@ -790,9 +800,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_loop(KLDev d, int limit,
         for (int i = tid; i < d.nck0; i += KL_LOOP_THREADS) ck0[i] = d.ckey0[i];
         for (int i = tid; i < d.nck1; i += KL_LOOP_THREADS) ck1[i] = d.ckey1[i];
         for (int i = tid; i < words; i += KL_LOOP_THREADS) {
-            uint32_t b = 0;
-            for (int j = 0; j < 32 && i * 32 + j < d.n; ++j) b |= uint32_t(d.side_init[i * 32 + j] == 1) << j;
-            s_side[i] = b;
+            s_side[i] = side_word(d.side_init, d.n, i);
             s_lock[i] = 0u;
         }
     }
