@@ -100,8 +100,7 @@ def main():
         res = None
         if rank == 0:
             med, bits = ek.median_split(v)
-            idx = np.arange(n, dtype=np.int32)
-            ctx.kl_set_partition(idx[bits == 0], idx[bits == 1])
+            ctx.kl_set_partition_bits(bits)  # cKL -EIG split order (cKL.cpp:155-174)
             _, res = ctx.kl_run(cap=0)
         return lam, st, res
 

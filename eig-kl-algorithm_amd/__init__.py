@@ -102,6 +102,7 @@ _sig("ek_eig_read", ctypes.c_int, ctypes.c_char_p, _I64, ctypes.POINTER(ctypes.c
 _sig("ek_kl_graph_setup", ctypes.c_int, _P, _I64, _P, _P, _P)
 _sig("ek_kl_nets_setup", ctypes.c_int, _P, _I64, _P, _P)
 _sig("ek_kl_set_partition", ctypes.c_int, _P, _P, _I64, _P, _I64)
+_sig("ek_kl_set_partition_bits", ctypes.c_int, _P, _I64, _P)
 _sig("ek_kl_run", ctypes.c_int, _P, _I32, _P, _I64, ctypes.POINTER(KLResult))
 _sig("ek_kl_sides", ctypes.c_int, _P, _I32, _P)
 _sig("ek_cli_main", ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p))
@@ -351,13 +352,20 @@ class Context:
         _chk(_lib.ek_kl_nets_setup(self._c, len(net_ptr) - 1, _p(net_ptr), _p(pins)), "kl_nets_setup")
 
     def kl_set_partition(self, order0, order1):
-        self._o0 = np.ascontiguousarray(order0, np.int32)
-        self._o1 = np.ascontiguousarray(order1, np.int32)
-        _chk(_lib.ek_kl_set_partition(self._c, _p(self._o0), len(self._o0), _p(self._o1), len(self._o1)),
-             "kl_set_partition")
+        o0 = np.ascontiguousarray(order0, np.int32)
+        o1 = np.ascontiguousarray(order1, np.int32)
+        _chk(_lib.ek_kl_set_partition(self._c, _p(o0), len(o0), _p(o1), len(o1)), "kl_set_partition")
+        self._n01 = (len(o0), len(o1))
+
+    def kl_set_partition_bits(self, bits):
+        """cKL.cpp:155-174 (-EIG): node i to split[bits[i]], ascending node order."""
+        bits = np.ascontiguousarray(bits, np.uint8)
+        _chk(_lib.ek_kl_set_partition_bits(self._c, len(bits), _p(bits)), "kl_set_partition_bits")
+        n1 = int(np.count_nonzero(bits))
+        self._n01 = (len(bits) - n1, n1)
 
     def kl_run(self, limit=-1, cap=None):
-        cap = min(len(self._o0), len(self._o1)) if cap is None else cap
+        cap = min(self._n01) if cap is None else cap
         log = np.zeros(max(cap, 1), SWAP_DTYPE)
         r = KLResult()
         _chk(_lib.ek_kl_run(self._c, int(limit), _p(log), cap, ctypes.byref(r)), "kl_run")

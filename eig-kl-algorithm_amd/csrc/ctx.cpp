@@ -857,6 +857,20 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
     EK_CATCH
 }
 
+int ek_kl_set_partition_bits(ek_ctx* c, int64_t n, const uint8_t* bits) {
+    EK_TRY
+    if (n < 0 || (n && !bits)) ek::fail(EK_EINVAL, "ek_kl_set_partition_bits: bad argument");
+    std::vector<int32_t> o[2];
+    o[0].reserve(size_t(n) / 2 + 1);
+    o[1].reserve(size_t(n) / 2 + 1);
+    for (int64_t i = 0; i < n; ++i) {
+        if (bits[i] > 1) ek::fail(EK_EINVAL, "ek_kl_set_partition_bits: bit %d at node %lld", int(bits[i]), (long long)i);
+        o[bits[i]].push_back(int32_t(i));
+    }
+    return ek_kl_set_partition(c, o[0].data(), int64_t(o[0].size()), o[1].data(), int64_t(o[1].size()));
+    EK_CATCH
+}
+
 }  // extern "C"
 
 namespace {

@@ -206,6 +206,9 @@ int ek_kl_nets_setup(ek_ctx* ctx, int64_t nets, const int64_t* net_ptr, const in
 /* Initial remain[] lists (shuffleSparceMatrix, cKL.cpp:151-197): positions
  * are list order; the sides are split[0] = order0, split[1] = order1. */
 int ek_kl_set_partition(ek_ctx* ctx, const int32_t* order0, int64_t n0, const int32_t* order1, int64_t n1);
+/* The -EIG branch of shuffleSparceMatrix (cKL.cpp:155-174): node i goes to
+ * split[bits[i]] in ascending node order (the EIG file's line order). */
+int ek_kl_set_partition_bits(ek_ctx* ctx, int64_t n, const uint8_t* bits);
 /* Run the swap loop to termination on the device (one persistent
  * workgroup; no host round trip per iteration).  limit < 0: floor(log2 n)+5
  * (cKL.cpp:303).  log_out may be NULL. */

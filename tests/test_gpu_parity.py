@@ -119,6 +119,24 @@ def test_kl_fallback_paths_bitexact(ek, oracle, ctx, monkeypatch, name, mode):
     assert res["net_cut_best"] == NET_CUTS[name]["net_cut_best"]
 
 
+@pytest.mark.parametrize("name", ["fract", "ibm01"])
+def test_kl_partition_from_bits(ek, oracle, ctx, name):
+    # ek_kl_set_partition_bits is the -EIG branch of shuffleSparceMatrix
+    # (cKL.cpp:155-174): the same lists as the EIG file's line order
+    h = ek.Hypergraph.read(circuit_path(name))
+    _, _, bits, _, o0, o1 = ek.eig_read(eig_path(name), h.nodes)
+    assert np.array_equal(np.flatnonzero(bits == 0), o0) and np.array_equal(np.flatnonzero(bits == 1), o1)
+    ctx.kl_graph_setup(h.kl_graph())
+    ctx.kl_nets_setup(*h.pins())
+    ctx.kl_set_partition_bits(bits)
+    log, res = ctx.kl_run()
+    olog, ores = oracle.Graph.read(circuit_path(name)).kl(o0, o1)
+    assert res["iterations"] == ores["iterations"] == NET_CUTS[name]["iterations"]
+    _swap_fields_equal(log, olog)
+    with pytest.raises(ek.EKError):
+        ctx.kl_set_partition_bits(np.full(h.nodes, 2, np.uint8))
+
+
 def test_kl_edge_cases(ek, oracle, ctx):
     # tiny graph with repeated pins in a net, a 1-pin net, an empty net and an isolated node
     net_ptr = np.array([0, 3, 4, 4, 6, 9, 11], np.int64)
