@@ -434,19 +434,14 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         const KLInfo ia = ci0[cA], ib = ci1[cB];
         const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
         stamp(0);
-        // swap + erase (swip, cKL.cpp:274-286): every G1 wave applies the
-        // (idempotent) bitmap flips itself once its row loads are in flight, so
-        // no barrier is needed before its side lookups (the other roles read
-        // no bitmap before the barrier)
-        auto flip = [&]() {
-            if (lane == 0) {
-                atomicOr(&s_side[A >> 5], 1u << (A & 31));
-                atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
-                atomicOr(&s_lock[A >> 5], 1u << (A & 31));
-                atomicOr(&s_lock[B >> 5], 1u << (B & 31));
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        // swap + erase (swip, cKL.cpp:274-286): the bitmaps are flipped after
+        // the first barrier (G2, W wave); until then every lookup reads the
+        // pre-swap bitmaps and applies the swap itself: node1 and node2 (never
+        // equal) change side and become locked.
+        auto side_now = [&](int x) -> bool {
+            return (((s_side[x >> 5] >> (x & 31)) & 1u) != 0) ^ (x == A) ^ (x == B);
         };
+        auto locked_now = [&](int x) -> bool { return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B; };
         const int tot = la + lb;
         const int tag = int(it);
         if (wv == W_W) {
@@ -506,7 +501,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // issued at once; the sums run strictly in row order, the
             // zero-weight padding of short segments adds exact zeros
             int4* stage = sg_stage + wv * 8 * KL_SEG_LANES;  // this wave's 8 rows x KL_SEG_LANES pieces
-            bool flipped = false;
             for (int i0 = wv * 8; i0 < tot; i0 += NG * 8) {
                 // 8 lanes per row, each loading 16-B pieces j8, j8 + 8, ... of the
                 // row's inline segment: each instruction touches each 128-B line
@@ -522,10 +516,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
                                      : make_int4(0, 0, 0, 0);
                 const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
-                if (!flipped) {
-                    flip();
-                    flipped = true;
-                }
                 if (d.seg) {
                     // each lane looks up the sides of its own entries (4 LDS reads
                     // per wave instead of 32 serial ones by the summing lane) and
@@ -533,8 +523,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
 #pragma unroll
                     for (int r = 0; r < PPL; ++r) {
                         const int4 pc = piece[r];
-                        const bool e0 = (s_side[pc.x >> 5] >> (pc.x & 31)) & 1u;
-                        const bool e1 = (s_side[pc.z >> 5] >> (pc.z & 31)) & 1u;
+                        const bool e0 = side_now(pc.x);
+                        const bool e1 = side_now(pc.z);
                         const float w0 = __int_as_float(pc.y), w1 = __int_as_float(pc.w);
                         stage[(lane >> 3) * KL_SEG_LANES + j8 + 8 * r] =
                             make_int4(__float_as_int(e0 ? 0.0f : w0), __float_as_int(e0 ? w0 : 0.0f),
@@ -549,7 +539,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_SEG_LANES + j];
                 }
                 const int u = a.x, rp = a.y, len = a.z;
-                const bool act = !((s_lock[u >> 5] >> (u & 31)) & 1u);
+                const bool act = !locked_now(u);
                 // the row's list, position, chunk and that chunk's current key
                 // depend on the descriptor only: read ahead of the sums
                 const uint32_t pl = uint32_t(a.w);
@@ -592,7 +582,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
 #pragma unroll
                         for (int k2 = 0; k2 < 16; ++k2) {
                             cc[k2] = q + k2 < len ? cc[k2] : 0;
-                            const bool e = (s_side[cc[k2] >> 5] >> (cc[k2] & 31)) & 1u;
+                            const bool e = side_now(cc[k2]);
                             internal += e ? 0.0f : ww[k2];
                             external += e ? ww[k2] : 0.0f;
                         }
@@ -631,7 +621,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     it_info[i] = inf;
                 }
             }
-            if (!flipped) flip();  // a wave without rows (node1 and node2 may have none)
         }
         stamp(1);
         __syncthreads();  // (1) gains, early rescans, merged keys and tags visible
@@ -706,6 +695,12 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
         }
         stamp(3);
+        if (wv == W_W && lane == 0) {  // the swap itself, for the next swap's lookups (barrier 2)
+            s_side[A >> 5] |= 1u << (A & 31);
+            s_side[B >> 5] &= ~(1u << (B & 31));
+            s_lock[A >> 5] |= 1u << (A & 31);
+            s_lock[B >> 5] |= 1u << (B & 31);
+        }
         // G2b. publish merged keys of the other untagged chunks (every item of
         // a chunk writes the same value) and the descriptor of the item that won
         for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
@@ -724,7 +719,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             if (i < KL_ITEM_CAP) cs = it_cs[i];
             else {  // beyond the LDS item list (hubs): rederive
                 const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
-                cs = ((s_lock[u >> 5] >> (u & 31)) & 1u) ? -1 : int((uint32_t(d.nd[u].c) & 0x80000000u) |
+                cs = locked_now(u) ? -1 : int((uint32_t(d.nd[u].c) & 0x80000000u) |
                                                                      ((uint32_t(d.nd[u].c) & 0x7fffffffu) / KL_CHUNK));
             }
             if (cs == -1) continue;
