@@ -252,10 +252,14 @@ __host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
     return (m + 31) / 32 * 32;
 }
 
+// staging row stride in 16-B pieces: one piece of padding, so the 8 summing
+// lanes of a wave (one per row) read 8 different bank groups instead of one
+constexpr int KL_STAGE_ROW = KL_SEG_LANES + 1;
+
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
-    const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_SEG_LANES) * sizeof(KLInfo) +
+    const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_STAGE_ROW) * sizeof(KLInfo) +
                      (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4) * 8 +
                      (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4;
     return b <= 152 * 1024 ? b : 0;
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
     KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2][E_PARTS] early-rescan winners
     int4* sg_stage = reinterpret_cast<int4*>(er_info + 2 * E_PARTS);  // [NG][8 rows][KL_SEG_LANES] G1 staging
-    u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * 8 * KL_SEG_LANES);  // chunk keys (zero-padded to nsel)
+    u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * 8 * KL_STAGE_ROW);  // chunk keys (zero-padded to nsel)
     u64* ck1 = ck0 + nsel;
     u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
     u64* ckn1 = ckn0 + d.nck0;
@@ -500,7 +504,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // addressed by the CSR position alone, so every load of the row is
             // issued at once; the sums run strictly in row order, the
             // zero-weight padding of short segments adds exact zeros
-            int4* stage = sg_stage + wv * 8 * KL_SEG_LANES;  // this wave's 8 rows x KL_SEG_LANES pieces
+            int4* stage = sg_stage + wv * 8 * KL_STAGE_ROW;  // this wave's 8 rows x KL_SEG_LANES pieces (+1 pad)
             for (int i0 = wv * 8; i0 < tot; i0 += NG * 8) {
                 // 8 lanes per row, each loading 16-B pieces j8, j8 + 8, ... of the
                 // row's inline segment: each instruction touches each 128-B line
@@ -526,7 +530,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                         const bool e0 = side_now(pc.x);
                         const bool e1 = side_now(pc.z);
                         const float w0 = __int_as_float(pc.y), w1 = __int_as_float(pc.w);
-                        stage[(lane >> 3) * KL_SEG_LANES + j8 + 8 * r] =
+                        stage[(lane >> 3) * KL_STAGE_ROW + j8 + 8 * r] =
                             make_int4(__float_as_int(e0 ? 0.0f : w0), __float_as_int(e0 ? w0 : 0.0f),
                                       __float_as_int(e1 ? 0.0f : w1), __float_as_int(e1 ? w1 : 0.0f));
                     }
@@ -536,7 +540,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 int4 sg[KL_SEG_LANES];  // per entry pair: (internal, external) contributions
                 if (d.seg) {
 #pragma unroll
-                    for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_SEG_LANES + j];
+                    for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_STAGE_ROW + j];
                 }
                 const int u = a.x, rp = a.y, len = a.z;
                 const bool act = !locked_now(u);
