@@ -980,10 +980,10 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
         if (std::getenv("EK_KL_PROF")) {
-            static const char* names[10] = {"select", "G1-key", "bar1", "G2a", "G2bc", "bar2", "G1-aux", "G1-sum",
-                                            "n_stale", "n_late+tail"};
+            static const char* names[12] = {"select", "G1-key", "bar1", "G2a", "G2bc", "bar2", "G1-aux", "G1-sum",
+                                            "n_stale", "n_late+tail", "G1-load", "G1-look"};
             std::fprintf(stderr, "[kl] %lld swaps, us/swap:", (long long)ho.iterations);
-            for (int i = 0; i < 10; ++i)
+            for (int i = 0; i < 12; ++i)
                 std::fprintf(stderr, " %s %.3f", names[i], ho.prof[i] * 0.01 / std::max<long long>(1, ho.iterations));
             std::fprintf(stderr, "\n");
             if (ho.prof[15])

@@ -489,6 +489,9 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // each taking a contiguous part of it
             const int s = wv <= W_EB ? 1 : 0, part = (s ? W_EB : W_EA) - wv;
             const int p0 = (s ? cB : cA) * KL_CHUNK + part * NQ_E * 64;
+            // let the gain-update waves' few row loads enter the CU's memory
+            // pipeline ahead of these 16 KB (they are on the critical path)
+            __builtin_amdgcn_s_sleep(4);
             KLInfo info;
             bool mine;
             const u64 kk = s ? chunk_rescan1<NQ_E>(d.gp1, d.pinfo1, 1, p0, posB, lane, &info, &mine)
@@ -520,6 +523,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
                                      : make_int4(0, 0, 0, 0);
                 const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
+                if constexpr (PROF) {
+                    if (tid == 0 && (piece[0].x == -12345 || a.x == -12345)) s_stop[2] = 0;  // waits for the loads
+                }
+                stamp(10);
                 if (d.seg) {
                     // each lane looks up the sides of its own entries (4 LDS reads
                     // per wave instead of 32 serial ones by the summing lane) and
@@ -535,6 +542,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                                       __float_as_int(e1 ? 0.0f : w1), __float_as_int(e1 ? w1 : 0.0f));
                     }
                 }
+                stamp(11);
                 if (j8 != 0 || gi >= tot) continue;  // the row's first lane sums it
                 const int i = gi;
                 int4 sg[KL_SEG_LANES];  // per entry pair: (internal, external) contributions
