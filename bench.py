@@ -182,15 +182,16 @@ def main():
                "kl_iterations_match": ores["iterations"] == kres["iterations"]}
 
     # PMC traffic (committed rocprofv3 summary of this workload), per SpMV launch
-    traffic = None
+    traffic = rocprof_us = None
     pmc_path = os.path.join(REPO, "profiles", "spmv_pmc_bytes.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
             if pm.get("workload") == f"syn{args.mult:g}x-seed{args.seed}" and world == 1:
                 traffic = pm.get("hbm_bytes_per_launch")
+                rocprof_us = pm.get("rocprof_avg_launch_us")
         except Exception:
-            traffic = None
+            traffic = rocprof_us = None
 
     out = {
         "metric": "wall-clock to final cut (s) + cut size, ibm18.hgr; SpMV GB/s vs HBM peak",
@@ -212,6 +213,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": spmv_bytes, "avg_launch_us": round(spmv_launch_ms * 1e3, 3),
                      "timing": "kernel start/end timestamps (hipExtLaunchKernelGGL events) of every 4th SpMV of each Lanczos cycle in the timed solves",
+                     "rocprof_avg_launch_us": rocprof_us,  # committed kernel-trace summary of this workload
                      "sweep": sweep},
         "cpu_baseline": cpu,
         "result": {"lambda1": lam, "lanczos_matvecs": st["matvecs"], "lanczos_restarts": st["restarts"],
