@@ -118,6 +118,7 @@ def main():
     lam, st, kres = stats[-1]
     spmv_launch_ms = sum(s[1]["spmv_ms"] for s in stats) / max(1, sum(s[1]["spmv_timed"] for s in stats))
     spmv_bytes = ctx.spmv_bytes(fused=True)  # the Lanczos SpMV also reads f and writes the basis column
+    spmv_packed, spmv_stored = ctx.spmv_format(fused=True)  # what the kernel actually streams
     achieved = spmv_bytes / (spmv_launch_ms * 1e-3) / 1e9 if spmv_launch_ms > 0 else 0.0
     if rank != 0:
         return
@@ -126,17 +127,26 @@ def main():
     # launches on resident buffers for the 1x workload and the 2x / 10x configs
     sweep = []
     if world == 1 and not args.no_sweep:
-        for mult in (args.mult, 2.0, 10.0):
-            if mult == args.mult:
+        # (mult, storage): the shipped (dictionary-coded) form at each size, and
+        # the plain int32 col + fp64 val CSR at the bench size for comparison
+        for mult, plain in ((args.mult, False), (args.mult, True), (2.0, False), (10.0, False)):
+            if mult == args.mult and not plain:
                 c2, b2 = ctx, spmv_bytes
             else:
-                hs = ek.Hypergraph.generate(mult, int(mult))
-                Ls = hs.laplacian()
+                hs = h if mult == args.mult else ek.Hypergraph.generate(mult, int(mult))
+                Ls = L if mult == args.mult else hs.laplacian()
                 c2 = ek.Context(local_rank)
-                c2.spmv_setup(hs.nodes, 0, Ls.rowptr, Ls.col, Ls.val)
+                if plain:
+                    os.environ["EK_SPMV_PLAIN"] = "1"
+                try:
+                    c2.spmv_setup(hs.nodes, 0, Ls.rowptr, Ls.col, Ls.val)
+                finally:
+                    os.environ.pop("EK_SPMV_PLAIN", None)
                 b2 = c2.spmv_bytes(fused=True)
+            packed2, stored2 = c2.spmv_format(fused=True)
             us = c2.spmv_bench(200, fused=True)
-            sweep.append({"mult": mult, "bytes_per_launch": int(b2), "avg_launch_us": round(us, 3),
+            sweep.append({"mult": mult, "storage": "dict32" if packed2 else "csr", "bytes_per_launch": int(b2),
+                          "stored_bytes_per_launch": int(stored2), "avg_launch_us": round(us, 3),
                           "GB/s": round(b2 / us / 1e3, 1), "frac": round(b2 / us / 1e3 / HBM_PEAK_GBS, 4)})
             if c2 is not ctx:
                 c2.close()
@@ -208,10 +218,13 @@ def main():
         "data": "synthetic (seeded ISPD98-shaped generator; ibm18.hgr not shipped)",
         "config": {"workload": f"ibm18-shape synthetic {args.mult:g}x seed {args.seed}", "nodes": n, "nets": nets,
                    "pins": npins, "laplacian_nnz": L.nnz, "parallelism": f"lanczos row-shard x{world}, KL 1 GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_spmv_adaptive<512> (Lanczos CSR SpMV, fp64, fused epilogue)",
+        "roofline": {"bound": "hbm", "kernel": f"k_spmv_adaptive<512,{str(spmv_packed).lower()}> (Lanczos CSR SpMV, fp64, fused epilogue)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": spmv_bytes, "avg_launch_us": round(spmv_launch_ms * 1e3, 3),
+                     "storage": ("dictionary-coded CSR: 32-bit (code<<colbits | col) words + exact fp64 value table"
+                                 if spmv_packed else "CSR: int32 col + fp64 val"),
+                     "stored_bytes_per_launch": spmv_stored,
                      "timing": "kernel start/end timestamps (hipExtLaunchKernelGGL events) of every 4th SpMV of each Lanczos cycle in the timed solves",
                      "rocprof_avg_launch_us": rocprof_us,  # committed kernel-trace summary of this workload
                      "sweep": sweep},

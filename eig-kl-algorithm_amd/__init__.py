@@ -90,6 +90,7 @@ _sig("ek_spmv_setup", ctypes.c_int, _P, _I64, _I64, _I64, _P, _P, _P)
 _sig("ek_spmv", ctypes.c_int, _P, _P, _P, _P)
 _sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
 _sig("ek_spmv_bytes", _I64, _P)
+_sig("ek_spmv_format", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64))
 _sig("ek_spmv_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
 _sig("ek_lanczos_fiedler", ctypes.c_int, _P, ctypes.POINTER(LanczosOpts), ctypes.POINTER(ctypes.c_double), _P,
@@ -322,6 +323,12 @@ class Context:
     def spmv_bytes(self, fused=False):
         """Algorithmic bytes of one SpMV; fused: the Lanczos form (+ f read, basis column write)."""
         return _lib.ek_spmv_bytes(self._c) + (16 * self.nrows if fused else 0)
+
+    def spmv_format(self, fused=False):
+        """(packed, stored bytes per launch): the storage the SpMV reads (ek_spmv_format)."""
+        pk, b = ctypes.c_int32(0), _I64(0)
+        _chk(_lib.ek_spmv_format(self._c, ctypes.byref(pk), ctypes.byref(b)), "ek_spmv_format")
+        return bool(pk.value), int(b.value) + (16 * self.nrows if fused else 0)
 
     def spmv_bench(self, iters=200, fused=True):
         """Average microseconds per back-to-back SpMV launch on resident buffers."""

@@ -5,6 +5,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -70,7 +71,8 @@ struct ek_ctx {
     // Laplacian rows owned by this context
     int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
     int block_nnz = 1024, nrb_spmv = 0;
-    DBuf rb, rowptr, col, val;
+    DBuf rb, rowptr, col, val, pk, dict;
+    int colbits = 0;  // > 0: the dictionary-coded matrix (pk, dict) is the one the SpMV reads
     // Lanczos workspace
     DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, apart, Qd, scal, bov;
     // KL state
@@ -90,6 +92,23 @@ ek_ctx* check_ctx(ek_ctx* c) {
     if (!c) ek::fail(EK_EINVAL, "null ek_ctx");
     set_device(c);
     return c;
+}
+
+ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
+    ek::dev::SpmvMat m;
+    m.nblocks = c->nrb_spmv;
+    m.block_nnz = c->block_nnz;
+    m.desc = c->rb.as<int32_t>();
+    m.rowptr = c->rowptr.as<int32_t>();
+    if (c->colbits > 0) {
+        m.colbits = c->colbits;
+        m.pk = c->pk.as<uint32_t>();
+        m.dict = c->dict.as<double>();
+    } else {
+        m.col = c->col.as<int32_t>();
+        m.val = c->val.as<double>();
+    }
+    return m;
 }
 
 // In-place sum all-reduce of `count` doubles on the context stream.
@@ -206,8 +225,24 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     c->nrb_spmv = int(rbv.size() / 4);
     upload(c->rb, rbv.data(), rbv.size(), c->stream);
     upload(c->rowptr, rowptr, size_t(nrows) + 1, c->stream);
-    upload(c->col, col, size_t(nnz), c->stream);
-    upload(c->val, val, size_t(nnz), c->stream);
+    // dictionary-coded entries unless EK_SPMV_PLAIN is set or the values do not fit
+    std::vector<uint32_t> pkv;
+    std::vector<double> dictv;
+    int colbits = 0;
+    const char* plain = std::getenv("EK_SPMV_PLAIN");
+    const bool packed = !(plain && plain[0] && plain[0] != '0') && ek::dev::spmv_pack(n, nnz, col, val, pkv, dictv, colbits);
+    c->colbits = packed ? colbits : 0;
+    if (packed) {
+        upload(c->pk, pkv.data(), pkv.size(), c->stream);
+        upload(c->dict, dictv.data(), dictv.size(), c->stream);
+        c->col.reset();
+        c->val.reset();
+    } else {
+        upload(c->col, col, size_t(nnz), c->stream);
+        upload(c->val, val, size_t(nnz), c->stream);
+        c->pk.reset();
+        c->dict.reset();
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     return EK_OK;
     EK_CATCH
@@ -218,8 +253,7 @@ int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv before ek_spmv_setup");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-    ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                  c->val.as<double>(), x, y, nullptr, nullptr, nullptr, nullptr, c->block_nnz);
+    ek::dev::spmv(s, spmv_mat(c), x, y, nullptr, nullptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     return EK_OK;
     EK_CATCH
@@ -232,9 +266,7 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     DBuf dx, dy;
     upload(dx, x, size_t(c->n), c->stream);
     dy.ensure(size_t(std::max<int64_t>(c->nrows, 1)) * 8);
-    ek::dev::spmv(c->stream, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                  c->val.as<double>(), dx.as<double>(), dy.as<double>(), nullptr, nullptr, nullptr, nullptr,
-                  c->block_nnz);
+    ek::dev::spmv(c->stream, spmv_mat(c), dx.as<double>(), dy.as<double>(), nullptr, nullptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     if (c->nrows) HIPCHK(hipMemcpyAsync(y, dy.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -264,13 +296,10 @@ int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
     HIPCHK(hipMemcpyAsync(fn2.p, &nrm, 8, hipMemcpyHostToDevice, s));
     auto launch = [&] {
         if (fused)
-            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                          c->val.as<double>(), x.as<double>(), y.as<double>(), fn2.as<double>(), x.as<double>(),
-                          vcol.as<double>(), apart.as<double>(), c->block_nnz);
+            ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), fn2.as<double>(), x.as<double>(),
+                          vcol.as<double>(), apart.as<double>());
         else
-            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                          c->val.as<double>(), x.as<double>(), y.as<double>(), nullptr, nullptr, nullptr, nullptr,
-                          c->block_nnz);
+            ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), nullptr, nullptr, nullptr, nullptr);
     };
     for (int i = 0; i < 10; ++i) launch();
     hipEvent_t e0, e1;
@@ -293,6 +322,17 @@ int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
 int64_t ek_spmv_bytes(ek_ctx* c) {
     if (!c) return 0;
     return 12 * c->nnz + 4 * (c->nrows + 1) + 8 * c->n + 8 * c->nrows;
+}
+
+int ek_spmv_format(ek_ctx* c, int32_t* packed, int64_t* stored_bytes) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_format before ek_spmv_setup");
+    const int64_t entries = c->colbits > 0 ? 4 * c->nnz + int64_t(c->dict.bytes) : 12 * c->nnz;
+    if (packed) *packed = c->colbits > 0 ? 1 : 0;
+    if (stored_bytes) *stored_bytes = entries + 4 * (c->nrows + 1) + 8 * c->n + 8 * c->nrows;
+    return EK_OK;
+    EK_CATCH
 }
 
 // ---------------------------------------------------------------------------
@@ -366,9 +406,8 @@ struct Lanczos {
         for (int i = k; i < m; ++i) {
             const double* x = gather_f();
             const bool timed = spmv_timed_step(i, k);
-            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                          c->val.as<double>(), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
-                          reorth == 1 ? c->apart.as<double>() : nullptr, c->block_nnz, nullptr,
+            ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
+                          reorth == 1 ? c->apart.as<double>() : nullptr, nullptr,
                           timed ? ev[size_t(2 * (i - k))] : nullptr, timed ? ev[size_t(2 * (i - k) + 1)] : nullptr);
             ++matvecs;
             const int nc = i + 1, tot = nc + has_u0;
@@ -437,9 +476,8 @@ struct Lanczos {
                 fin.bov_i = bov + i - 1;
             }
             const bool timed = spmv_timed_step(i, k);
-            ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                          c->val.as<double>(), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
-                          c->apart.as<double>(), c->block_nnz, i > k ? &fin : nullptr,
+            ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
+                          c->apart.as<double>(), i > k ? &fin : nullptr,
                           timed ? ev[size_t(2 * (i - k))] : nullptr, timed ? ev[size_t(2 * (i - k) + 1)] : nullptr);
             ++matvecs;
             const int nc = i + 1;
@@ -687,8 +725,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     }
     HIPCHK(hipMemcpyAsync(v.data(), xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
     // residual ||L x - lambda x|| on the owned rows
-    ek::dev::spmv(s, c->nrb_spmv, c->rb.as<int32_t>(), c->rowptr.as<int32_t>(), c->col.as<int32_t>(),
-                  c->val.as<double>(), xg, c->w.as<double>(), nullptr, nullptr, nullptr, nullptr, c->block_nnz);
+    ek::dev::spmv(s, spmv_mat(c), xg, c->w.as<double>(), nullptr, nullptr, nullptr, nullptr);
     std::vector<double> y(size_t(std::max<int64_t>(c->nrows, 1)));
     if (c->nrows) HIPCHK(hipMemcpyAsync(y.data(), c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

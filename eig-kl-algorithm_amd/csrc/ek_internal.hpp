@@ -100,9 +100,29 @@ std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int b
 // desc: 4 ints per block {row0, nrows, nnz0, cnt} from spmv_row_blocks.
 // fin: the previous step's finalize folded in (then ||f||^2 comes from it, not *fn2).
 // ev_start/ev_stop: kernel start/end timestamps (hipExtLaunchKernelGGL), optional.
-void spmv(hipStream_t s, int nblocks, const int32_t* desc, const int32_t* rowptr, const int32_t* col,
-          const double* val, const double* x, double* y, const double* fn2, const double* f, double* vcol,
-          double* apart, int block_nnz, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
+//
+// Matrix storage: plain CSR (col int32 + val fp64, 12 B per entry) or the
+// value-dictionary form (pk != null): one 32-bit word per entry,
+// (code << colbits) | col, with val = dict[code].  A clique Laplacian holds few
+// distinct values (-2/|e| sums and the row sums: 840 at ibm18 shape, 4,890 in
+// ibm01), so the exact fp64 values come back from a table of a few KB that
+// stays in L1/L2, and each entry streams 4 B instead of 12.  Same products,
+// same summation order: results are bit-identical to the plain form.
+struct SpmvMat {
+    int nblocks = 0, block_nnz = 512, colbits = 0;
+    const int32_t* desc = nullptr;
+    const int32_t* rowptr = nullptr;
+    const int32_t* col = nullptr;
+    const double* val = nullptr;
+    const uint32_t* pk = nullptr;
+    const double* dict = nullptr;
+};
+// dictionary coding of (col, val): false (pk untouched) when the distinct
+// values do not fit the 32 - colbits code bits.  dict is ordered by frequency.
+bool spmv_pack(int64_t n, int64_t nnz, const int32_t* col, const double* val, std::vector<uint32_t>& pk,
+               std::vector<double>& dict, int& colbits);
+void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
+          double* vcol, double* apart, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
           hipEvent_t ev_stop = nullptr);
 
 // kernels_lanczos.hip

@@ -122,6 +122,15 @@ int ek_spmv_host(ek_ctx* ctx, const double* x, double* y);
  * §8d: 12*nnz (col+val) + 4*(nrows+1) (rowptr) + 8*n (x read once) +
  * 8*nrows (y).  Single GPU: 12 nnz + 4(n+1) + 16 n. */
 int64_t ek_spmv_bytes(ek_ctx* ctx);
+/* Storage form the SpMV reads (no reference counterpart; the reference keeps
+ * an Eigen CSC of fp64 values, cEIG.cpp:49-50).  *packed = 1 when the entries
+ * are dictionary-coded 32-bit words (column | code of the exact fp64 value in
+ * a per-matrix table; bit-identical products), 0 for plain CSR (int32 col +
+ * fp64 val; chosen when the distinct values overflow the code bits, or with
+ * EK_SPMV_PLAIN=1 at setup).  *stored_bytes = bytes of one launch as stored:
+ * entries + table + rowptr + 8*n (x) + 8*nrows (y).  Either pointer may be
+ * NULL. */
+int ek_spmv_format(ek_ctx* ctx, int32_t* packed, int64_t* stored_bytes);
 /* Back-to-back SpMV launches on context-owned buffers, timed with HIP events
  * around the batch: *avg_us = average per launch.  fused = 1 times the
  * Lanczos form (y scaled by 1/||x||, basis column + alpha partials written:

@@ -52,6 +52,49 @@ def test_spmv_matches_oracle(ek, oracle, ctx, which):
     assert np.abs(y1).max() <= 1e-12
 
 
+@pytest.mark.parametrize("which", ["ibm01", "syn1"])
+def test_spmv_dictionary_form_bit_identical(ek, ctx, monkeypatch, which):
+    """The dictionary-coded entries (32-bit col|code words + exact fp64 table)
+    must give the plain CSR kernel's products in the same order: y and the
+    whole Lanczos run bit for bit."""
+    h = ek.Hypergraph.generate(1.0, 1) if which == "syn1" else ek.Hypergraph.read(circuit_path(which))
+    L = h.laplacian()
+    x = np.random.default_rng(11).standard_normal(h.nodes)
+    out = {}
+    for plain in (False, True):
+        if plain:
+            monkeypatch.setenv("EK_SPMV_PLAIN", "1")
+        else:
+            monkeypatch.delenv("EK_SPMV_PLAIN", raising=False)
+        ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+        packed, stored = ctx.spmv_format()
+        assert packed == (not plain)
+        assert stored < ctx.spmv_bytes() if packed else stored == ctx.spmv_bytes()
+        y = ctx.spmv_host(x)
+        lam, v, st = ctx.lanczos_fiedler() if which == "ibm01" else (0.0, np.zeros(1), {"matvecs": 0})
+        out[plain] = (y, lam, v, st["matvecs"])
+    monkeypatch.delenv("EK_SPMV_PLAIN", raising=False)
+    assert np.array_equal(out[False][0].view(np.uint64), out[True][0].view(np.uint64))
+    assert out[False][1] == out[True][1] and out[False][3] == out[True][3]
+    assert np.array_equal(out[False][2], out[True][2])
+
+
+def test_spmv_dictionary_overflow_falls_back(ek, ctx):
+    """More distinct values than the code bits hold -> plain CSR, same result."""
+    n = 1 << 20  # colbits 20 -> 4096 codes; 6000 distinct values do not fit
+    rng = np.random.default_rng(5)
+    deg = 4
+    rowptr = (np.arange(n + 1) * deg).astype(np.int32)
+    col = rng.integers(0, n, n * deg).astype(np.int32)
+    val = np.round(rng.integers(1, 6001, n * deg) * 1e-3, 3)
+    ctx.spmv_setup(n, 0, rowptr, col, val)
+    assert ctx.spmv_format()[0] is False
+    x = rng.standard_normal(n)
+    y = ctx.spmv_host(x)
+    ref = np.add.reduceat(val * x[col], rowptr[:-1])
+    assert np.abs(y - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
 # ------------------------------------------------------- KL, bit-exact vs cKL
 @pytest.mark.parametrize("name", CIRCUITS)
 def test_kl_bitexact_golden(ek, oracle, ctx, name):
