@@ -71,8 +71,9 @@ struct ek_ctx {
     // Laplacian rows owned by this context
     int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
     int block_nnz = 1024, nrb_spmv = 0;
-    DBuf rb, rowptr, col, val, pk, dict;
+    DBuf rb, rowptr, col, val, pk, rel, dict;
     int colbits = 0;  // > 0: the dictionary-coded matrix (pk, dict) is the one the SpMV reads
+    int64_t mat_bytes = 0;  // bytes of the matrix arrays one SpMV reads, as stored
     // Lanczos workspace
     DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, apart, Qd, scal, bov;
     // KL state
@@ -103,6 +104,7 @@ ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
     if (c->colbits > 0) {
         m.colbits = c->colbits;
         m.pk = c->pk.as<uint32_t>();
+        m.rel = c->rel.as<uint16_t>();
         m.dict = c->dict.as<double>();
     } else {
         m.col = c->col.as<int32_t>();
@@ -220,29 +222,39 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     c->nrows = nrows;
     c->nloc = c->nranks > 1 ? nloc : n;
     c->nnz = nnz;
-    c->block_nnz = 512;  // lab (tools/spmv_lab.hip): 512-nnz blocks are the fastest at every size tried
-    const auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
-    c->nrb_spmv = int(rbv.size() / 4);
-    upload(c->rb, rbv.data(), rbv.size(), c->stream);
-    upload(c->rowptr, rowptr, size_t(nrows) + 1, c->stream);
     // dictionary-coded entries unless EK_SPMV_PLAIN is set or the values do not fit
     std::vector<uint32_t> pkv;
     std::vector<double> dictv;
     int colbits = 0;
     const char* plain = std::getenv("EK_SPMV_PLAIN");
     const bool packed = !(plain && plain[0] && plain[0] != '0') && ek::dev::spmv_pack(n, nnz, col, val, pkv, dictv, colbits);
+    // 512-nnz blocks (tools/spmv_lab.hip for plain CSR; for the coded form,
+    // 1024-nnz segments measured 14.3 against 12.7 us inside the solve)
+    c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
+    auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
+    c->nrb_spmv = int(rbv.size() / 4);
     c->colbits = packed ? colbits : 0;
     if (packed) {
-        upload(c->pk, pkv.data(), pkv.size(), c->stream);
+        std::vector<uint32_t> segv;
+        std::vector<uint16_t> relv;
+        ek::dev::spmv_segment(rbv, rowptr, pkv, c->block_nnz, segv, relv);  // long rows: desc nnz0 -> overflow area
+        upload(c->pk, segv.data(), segv.size(), c->stream);
+        upload(c->rel, relv.data(), relv.size(), c->stream);
         upload(c->dict, dictv.data(), dictv.size(), c->stream);
+        c->mat_bytes = int64_t(segv.size() * 4 + relv.size() * 2 + dictv.size() * 8 + rbv.size() * 4);
         c->col.reset();
         c->val.reset();
+        c->rowptr.reset();
     } else {
+        upload(c->rowptr, rowptr, size_t(nrows) + 1, c->stream);
         upload(c->col, col, size_t(nnz), c->stream);
         upload(c->val, val, size_t(nnz), c->stream);
+        c->mat_bytes = 12 * nnz + 4 * (nrows + 1);
         c->pk.reset();
+        c->rel.reset();
         c->dict.reset();
     }
+    upload(c->rb, rbv.data(), rbv.size(), c->stream);
     HIPCHK(hipStreamSynchronize(c->stream));
     return EK_OK;
     EK_CATCH
@@ -328,9 +340,10 @@ int ek_spmv_format(ek_ctx* c, int32_t* packed, int64_t* stored_bytes) {
     EK_TRY
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_format before ek_spmv_setup");
-    const int64_t entries = c->colbits > 0 ? 4 * c->nnz + int64_t(c->dict.bytes) : 12 * c->nnz;
+    // coded: segments (padding included) + row starts + table + descriptors; plain: CSR
+    const int64_t mat = c->mat_bytes;
     if (packed) *packed = c->colbits > 0 ? 1 : 0;
-    if (stored_bytes) *stored_bytes = entries + 4 * (c->nrows + 1) + 8 * c->n + 8 * c->nrows;
+    if (stored_bytes) *stored_bytes = mat + 8 * c->n + 8 * c->nrows;
     return EK_OK;
     EK_CATCH
 }

@@ -114,13 +114,19 @@ struct SpmvMat {
     const int32_t* rowptr = nullptr;
     const int32_t* col = nullptr;
     const double* val = nullptr;
-    const uint32_t* pk = nullptr;
+    const uint32_t* pk = nullptr;  // per-block segments of the coded words (spmv_segment)
+    const uint16_t* rel = nullptr;  // row starts inside each segment
     const double* dict = nullptr;
 };
+constexpr int SPMV_SEG_NNZ = 512;     // default block_nnz (segment size) of the coded form
+constexpr int SPMV_REL_STRIDE = 258;  // rel entries per block (nrows + 1 <= 257, padded)
 // dictionary coding of (col, val): false (pk untouched) when the distinct
 // values do not fit the 32 - colbits code bits.  dict is ordered by frequency.
 bool spmv_pack(int64_t n, int64_t nnz, const int32_t* col, const double* val, std::vector<uint32_t>& pk,
                std::vector<double>& dict, int& colbits);
+// desc (from spmv_row_blocks with SPMV_SEG_NNZ) is updated for long rows.
+void spmv_segment(std::vector<int32_t>& desc, const int32_t* rowptr, const std::vector<uint32_t>& pk, int seg_nnz,
+                  std::vector<uint32_t>& seg, std::vector<uint16_t>& rel);
 void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
           double* vcol, double* apart, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
           hipEvent_t ev_stop = nullptr);

@@ -121,6 +121,35 @@ bool spmv_pack(int64_t n, int64_t nnz, const int32_t* col, const double* val, st
     return true;
 }
 
+// Per-block segments of the coded entries: block b's entries at
+// [b*seg_nnz, +cnt), padded with word 0; a long row (vector mode) goes
+// to an overflow area after the segments and its descriptor's nnz0 points
+// there.  rel[b*SPMV_REL_STRIDE + t] = start of the block's row t inside the
+// segment for t <= nrows, cnt beyond.
+void spmv_segment(std::vector<int32_t>& desc, const int32_t* rowptr, const std::vector<uint32_t>& pk, int seg_nnz,
+                  std::vector<uint32_t>& seg, std::vector<uint16_t>& rel) {
+    const size_t SEG = size_t(seg_nnz);
+    const size_t nb = desc.size() / 4;
+    size_t over = 0;
+    for (size_t b = 0; b < nb; ++b)
+        if (size_t(desc[4 * b + 3]) > SEG) over += size_t(desc[4 * b + 3]);
+    seg.assign(nb * SEG + over, 0u);
+    rel.assign(nb * SPMV_REL_STRIDE, 0);
+    size_t off = nb * SEG;
+    for (size_t b = 0; b < nb; ++b) {
+        const int32_t r0 = desc[4 * b], nr = desc[4 * b + 1], p0 = desc[4 * b + 2], cnt = desc[4 * b + 3];
+        if (size_t(cnt) > SEG) {
+            std::copy(pk.begin() + p0, pk.begin() + p0 + cnt, seg.begin() + off);
+            desc[4 * b + 2] = int32_t(off);
+            off += size_t(cnt);
+            continue;
+        }
+        std::copy(pk.begin() + p0, pk.begin() + p0 + cnt, seg.begin() + b * SEG);
+        for (int t = 0; t < SPMV_REL_STRIDE; ++t)
+            rel[b * SPMV_REL_STRIDE + t] = uint16_t(t <= nr ? rowptr[r0 + t] - p0 : cnt);
+    }
+}
+
 __device__ __forceinline__ void finalize_publish(const StepFin& f, double n2) {
     f.fn2_out[0] = n2;
     if (f.step >= 0) {
@@ -144,7 +173,9 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ x, int 
     return s;
 }
 
-// the fixed tree over the workgroup of the thread partials; every thread gets it
+// the fixed tree over the workgroup of the thread partials; every thread gets it.
+// (A barrier-free form where every wave reduces all 1024 partials itself, same
+// bits, measured slower inside the solve: 15.3 vs 12.7 us per SpMV.)
 __device__ __forceinline__ double block_sum_all(double s, double* wsum) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -155,13 +186,18 @@ __device__ __forceinline__ double block_sum_all(double s, double* wsum) {
     return r;
 }
 
-// PK: entries are dictionary-coded 32-bit words (SpmvMat::pk); `col` then
-// holds the pk words and `val` the dictionary.
+// PK: entries are dictionary-coded 32-bit words in per-block segments
+// (SpmvMat::seg, spmv_segment); `col` then holds the segments, `val` the
+// dictionary and `rel` the row starts inside each segment.  Block b's entries
+// and row starts sit at addresses given by b alone, so their loads go out
+// together with the descriptor's instead of after it: the x gathers are two
+// dependent memory round trips from the kernel start, not three.
 template <int BLOCK_NNZ, bool PK>
 __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __restrict__ desc,
                                                                 const int32_t* __restrict__ rowptr,
                                                                 const int32_t* __restrict__ col,
                                                                 const double* __restrict__ val, int colbits,
+                                                                const uint16_t* __restrict__ rel,
                                                                 const double* __restrict__ x, double* __restrict__ y,
                                                                 const double* __restrict__ fn2,
                                                                 const double* __restrict__ f,
@@ -173,13 +209,24 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     __shared__ double yrow[SPMV_THREADS];
     __shared__ double wsum[SPMV_THREADS / 64];
     const int t = threadIdx.x;
+    uint32_t wd[PER];
+    int rb0 = 0, rb1 = 0;
+    if constexpr (PK) {  // speculative: a long-row block's segment is padding
+#pragma unroll
+        for (int u = 0; u < PER; ++u) wd[u] = uint32_t(col[size_t(blockIdx.x) * BLOCK_NNZ + t + u * SPMV_THREADS]);
+        rb0 = rel[size_t(blockIdx.x) * SPMV_REL_STRIDE + t];
+        if (t == 0) rb1 = rel[size_t(blockIdx.x) * SPMV_REL_STRIDE + SPMV_THREADS];
+    }
     const int4 dsc = desc[blockIdx.x];
     const int r0 = dsc.x, nr = dsc.y, p0 = dsc.z, cnt = dsc.w;
     // ||f||^2: folded finalize of the previous Lanczos step (every block sums
     // the same partials in the same order; block 0 publishes) or read.  The
     // partials do not depend on the block descriptor, so their loads go out
-    // first; the tree (with its barriers) runs after the block's gathers are
-    // issued, and the scale is only needed by the epilogue.
+    // early; the tree (with its barriers) runs after the block's gathers are
+    // issued, and the scale is only needed by the epilogue.  (Measured inside
+    // the solve: loading them in the segment's round trip, 13.1 us, or every
+    // wave reducing all of them without barriers, 15.3 us, were both slower
+    // than this form, 12.7 us.)
     const double npart_t = fin.npart ? strided_sum(fin.npart, fin.nb) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
@@ -224,19 +271,12 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     // use (fixed trip count), products to LDS, row boundaries to LDS
     int ci[PER];
     double vv[PER];
-    if constexpr (PK) {
-        uint32_t wd[PER];
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int i = t + u * SPMV_THREADS;
-            wd[u] = i < cnt ? uint32_t(col[p0 + i]) : 0u;
-        }
+    if constexpr (PK) {  // padding entries are (col 0, code 0): valid loads, never summed
         const uint32_t cmask = (1u << colbits) - 1u;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int i = t + u * SPMV_THREADS;
-            ci[u] = i < cnt ? int(wd[u] & cmask) : -1;
-            vv[u] = i < cnt ? val[wd[u] >> colbits] : 0.0;
+            ci[u] = int(wd[u] & cmask);
+            vv[u] = val[wd[u] >> colbits];
         }
     } else {
 #pragma unroll
@@ -246,8 +286,10 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
             vv[u] = i < cnt ? val[p0 + i] : 0.0;
         }
     }
-    const int rb0 = t <= nr ? rowptr[r0 + t] - p0 : 0;
-    const int rb1 = (t == 0 && nr == SPMV_THREADS) ? rowptr[r0 + SPMV_THREADS] - p0 : 0;
+    if constexpr (!PK) {
+        rb0 = t <= nr ? rowptr[r0 + t] - p0 : 0;
+        rb1 = (t == 0 && nr == SPMV_THREADS) ? rowptr[r0 + SPMV_THREADS] - p0 : 0;
+    }
     const double fr = (vcol && t < nr) ? f[r0 + t] : 0.0;  // prefetched for the epilogue
     double xv[PER];
 #pragma unroll
@@ -304,12 +346,9 @@ void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const dou
     // rocprofv3 reports), not event packets around it
 #define EK_SPMV_LAUNCH(BN, PK)                                                                                 \
     hipExtLaunchKernelGGL(k_spmv_adaptive<BN, PK>, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, ev_start, ev_stop, 0, \
-                          d, m.rowptr, c, v, m.colbits, x, y, fn2, f, vcol, apart, fv)
+                          d, m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv)
     if (m.pk) {
-        switch (m.block_nnz) {
-            case 512: EK_SPMV_LAUNCH(512, true); break;
-            default: EK_SPMV_LAUNCH(1024, true); break;
-        }
+        EK_SPMV_LAUNCH(SPMV_SEG_NNZ, true);
     } else {
         switch (m.block_nnz) {
             case 512: EK_SPMV_LAUNCH(512, false); break;
