@@ -268,6 +268,16 @@ __global__ __launch_bounds__(256) void kFlush(const double4* __restrict__ p, siz
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += 256ull * gridDim.x) acc += p[i].x + p[i].w;
     if (acc == 12345.678) sink[0] = acc;
 }
+// the same stream with nontemporal loads (LAB_NT=1): does the basis traffic
+// still evict the SpMV's matrix and x?
+__global__ __launch_bounds__(256) void kFlushNT(const double4* __restrict__ p, size_t n, double* __restrict__ sink) {
+    double acc = 0.0;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += 256ull * gridDim.x) {
+        const double* q = reinterpret_cast<const double*>(p + i);
+        acc += __builtin_nontemporal_load(q) + __builtin_nontemporal_load(q + 3);
+    }
+    if (acc == 12345.678) sink[0] = acc;
+}
 
 static std::vector<int> row_blocks(const std::vector<int>& rp, int64_t n, int bn, int rows_cap) {
     std::vector<int> starts{0};
@@ -382,6 +392,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     // launch(ev0, ev1) must use hipExtLaunchKernelGGL with the two events
+    const bool lab_nt = std::getenv("LAB_NT") && std::getenv("LAB_NT")[0] == '1';
     auto run = [&](const char* name, int nblocks, auto launch, bool check) {
         CK(hipMemsetAsync(d_y, 0, size_t(n) * 8, s));
         for (int i = 0; i < 10; ++i) launch(nullptr, nullptr);
@@ -402,8 +413,8 @@ int main(int argc, char** argv) {
             double tot = 0.0;
             for (int i = 0; i < iters; ++i) {
                 if (cold)
-                    hipLaunchKernelGGL(kFlush, dim3(2048), dim3(256), 0, s, (const double4*)d_flush,
-                                       flush_bytes / sizeof(double4), d_sink);
+                    hipLaunchKernelGGL(lab_nt ? kFlushNT : kFlush, dim3(2048), dim3(256), 0, s,
+                                       (const double4*)d_flush, flush_bytes / sizeof(double4), d_sink);
                 launch(e0, e1);
                 CK(hipEventSynchronize(e1));
                 float ms = 0.f;
