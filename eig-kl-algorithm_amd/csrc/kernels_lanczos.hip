@@ -62,15 +62,30 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
 #pragma unroll
     for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
     const size_t nr = size_t(nreal);
+    // every load of the block's tile is issued before the first use (column
+    // index clamped to a valid column: no branch around a load, which would
+    // make each load wait for the previous one); the arithmetic and its order
+    // are unchanged
+    constexpr int KR = GT_ROWS / 512;
+    const int jmax = ncols > 0 ? ncols - 1 : 0;
+    double2 xs[KR], vs[KR][GT_COLS];
 #pragma unroll
-    for (int k = 0; k < GT_ROWS / 512; ++k) {
+    for (int k = 0; k < KR; ++k) {
         const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
-        const double2 x = *reinterpret_cast<const double2*>(w + r);
+        xs[k] = *reinterpret_cast<const double2*>(w + r);
+#pragma unroll
+        for (int jj = 0; jj < GT_COLS; ++jj)
+            vs[k][jj] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+    }
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+        const double2 x = xs[k];
 #pragma unroll
         for (int jj = 0; jj < GT_COLS; ++jj) {
             const int j = j0 + jj;
             if (j < ncols) {
-                const double2 v = *reinterpret_cast<const double2*>(V + size_t(j) * ldv + r);
+                const double2 v = vs[k][jj];
                 acc[jj] += v.x * x.x + v.y * x.y;
             } else if (has_u0 && j == ncols) {
                 acc[jj] += u0val * ((r < nr ? x.x : 0.0) + (r + 1 < nr ? x.y : 0.0));
@@ -91,15 +106,19 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
 // The canonical order of a column sum over the projection partials: lane
 // pair (2j, 2j+1) sums the even / odd blocks in order, then one add.  Used by
 // k_reduce_cols and by the fused update alike, so both give the same bits.
+// 32 loads in flight, then the adds in order.  The loads are unconditional
+// (clamped index) and so are the adds (0.0 past the end): a load behind a
+// branch waits for the loads before it.  s + 0.0 == s here because s starts
+// at +0 and a sum of these partials never becomes -0.0.
 __device__ __forceinline__ double col_sum(const double* __restrict__ pj, int nrb, int half) {
+    constexpr int CB = 32;
     double s = 0.0;
-    for (int b0 = half; b0 < nrb; b0 += 32) {  // 16 loads in flight, then the adds in order
-        double v[16];
+    for (int b0 = half; b0 < nrb; b0 += 2 * CB) {
+        double v[CB];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = b0 + 2 * u < nrb ? pj[b0 + 2 * u] : 0.0;
+        for (int u = 0; u < CB; ++u) v[u] = pj[min(b0 + 2 * u, nrb - 1)];
 #pragma unroll
-        for (int u = 0; u < 16; ++u)
-            if (b0 + 2 * u < nrb) s += v[u];
+        for (int u = 0; u < CB; ++u) s += b0 + 2 * u < nrb ? v[u] : 0.0;
     }
     return s + __shfl_xor(s, 1, 64);
 }
@@ -125,6 +144,24 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     __shared__ double hs[MAX_NCV + 2];
     __shared__ double lds4[4];
     const int tot = ncols + has_u0;
+    // Basis columns in batches of UB, double-buffered: batch b+1's loads are
+    // issued before batch b is used, and batch 0's (with src) before h is
+    // reduced, so the projection reduce and every batch overlap a round trip.
+    // Clamped column index and unconditional subtractions (a column past
+    // ncols is subtracted with coefficient 0): a load or a use behind a branch
+    // makes the load wait for the ones before it.  The subtractions keep their
+    // sequential order; x - v*0 == x for every x but -0.0, which these sums do
+    // not produce (a difference of equal values rounds to +0).
+    constexpr int UB = 8;
+    const int jmax = ncols > 0 ? ncols - 1 : 0;
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    auto load_batch = [&](double2* vb, int j0) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u) vb[u] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + u, jmax)) * ldv + r);
+    };
+    double2 cur[UB], nxt[UB];
+    double2 x = *reinterpret_cast<const double2*>(src + r);
+    load_batch(cur, 0);
     if constexpr (RED) {
         for (int j0 = 0; j0 < tot; j0 += 128) {
             const int j = j0 + (threadIdx.x >> 1);
@@ -138,12 +175,16 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
         for (int j = threadIdx.x; j < tot; j += 256) hs[j] = h[j];
     }
     __syncthreads();
-    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
-    double2 x = *reinterpret_cast<const double2*>(src + r);
-    for (int j = 0; j < ncols; ++j) {
-        const double2 v = *reinterpret_cast<const double2*>(V + size_t(j) * ldv + r);
-        x.x -= v.x * hs[j];
-        x.y -= v.y * hs[j];
+    for (int j0 = 0; j0 < ncols; j0 += UB) {
+        load_batch(nxt, j0 + UB);  // past the end: clamped re-reads of column jmax (cache hits)
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            const double hj = j0 + u < ncols ? hs[min(j0 + u, jmax)] : 0.0;
+            x.x -= cur[u].x * hj;
+            x.y -= cur[u].y * hj;
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u) cur[u] = nxt[u];
     }
     if (has_u0) {
         const double c = u0val * hs[ncols];
