@@ -25,15 +25,19 @@ __device__ __forceinline__ double wave_sum(double v) {
 // thread-strided partial of sum(x[0:n)): x[t] + x[t+256] + ... in this order,
 // with the loads batched so they are in flight together (a plain strided loop
 // waits for each load before the next add)
+// (16 per batch, unconditional clamped loads and adds of 0.0 past the end: a
+// load behind a branch waits for the loads before it; s + 0.0 == s because s
+// starts at +0 and these sums never become -0.0)
 __device__ __forceinline__ double strided_sum256(const double* __restrict__ x, int n) {
+    constexpr int SB = 16;
     double s = 0.0;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 256) {
-        double v[8];
+    if (n <= 0) return s;
+    for (int i0 = threadIdx.x; i0 < n; i0 += SB * 256) {
+        double v[SB];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = i0 + u * 256 < n ? x[i0 + u * 256] : 0.0;
+        for (int u = 0; u < SB; ++u) v[u] = x[min(i0 + u * 256, n - 1)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (i0 + u * 256 < n) s += v[u];
+        for (int u = 0; u < SB; ++u) s += i0 + u * 256 < n ? v[u] : 0.0;
     }
     return s;
 }
