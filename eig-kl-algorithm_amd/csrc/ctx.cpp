@@ -533,10 +533,12 @@ struct Lanczos {
 
     // The SpMV's kernel timestamps are taken on every 4th step of a cycle: a
     // launch with timing events costs the host ~7 us more, which the timed
-    // solve would otherwise carry on every step.
+    // solve would otherwise carry on every step.  The sample starts at the
+    // cycle's second step: the first SpMV after a restart (1 in 100 of the
+    // launches) follows the V <- VQ stream and would be 1 in 25 of the sample.
     static constexpr int SPMV_SAMPLE = 4;
     bool spmv_timed_step(int i, int k) const {
-        return time_spmv && (i - k) % SPMV_SAMPLE == 0 && size_t(2 * (i - k) + 1) < ev.size();
+        return time_spmv && (i - k) % SPMV_SAMPLE == 1 && size_t(2 * (i - k) + 1) < ev.size();
     }
 
     void collect_spmv_times(int k) {
