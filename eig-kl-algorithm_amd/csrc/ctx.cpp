@@ -700,7 +700,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         std::vector<double> Q(size_t(m) * m, 0.0), dd(d), ee(e);
         for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
         const auto tq0 = std::chrono::steady_clock::now();
-        for (int i = knew; i < m; ++i) ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q.data());
+        for (int i = knew; i < m; ++i)  // Q starts as the identity: lower bandwidth i - knew
+            ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q.data(), i - knew);
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
         const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
         const double hk = ee[size_t(knew - 1)];                         // H(knew, knew-1)

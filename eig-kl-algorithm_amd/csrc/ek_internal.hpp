@@ -60,8 +60,10 @@ uint64_t hashtable_next_buckets(uint64_t cur);  // bucket count after the rehash
 // eigenvalues (ascending) of the symmetric tridiagonal (d, e), e[i] = T(i+1,i);
 // zlast[j] = last component of eigenvector j; full Z (m x m col-major) if Z != null.
 bool tridiag_eig(int m, const double* d, const double* e, double* evals, double* zlast, double* Z);
-// one implicit symmetric QR step with shift mu on (d, e); accumulates Q (m x m col-major) <- Q G
-void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q);
+// one implicit symmetric QR step with shift mu on (d, e); accumulates Q (m x m col-major) <- Q G.
+// band >= 0: Q's lower bandwidth before this step (0 for the identity, +1 per
+// step), so rows below it are skipped; -1: full columns.
+void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int band = -1);
 }  // namespace ek
 
 // ---------------------------------------------------------------------------

@@ -4,6 +4,7 @@
 // steps of Spectra's SymEigsSolver (the solver cEIG.cpp:195-198 calls):
 // TridiagEigen of the projected H and the shifted QR sweeps of its restart.
 #include <cfloat>
+#include <algorithm>
 #include <cmath>
 #include <numeric>
 
@@ -98,7 +99,7 @@ bool tridiag_eig(int m, const double* d_in, const double* e_in, double* evals, d
 // blocks and the chase restarts at the top of every block — a chase that
 // simply ran through a split would stop there and never shift the trailing
 // block, which is the one that carries the residual row (Q(m-1, :)).
-void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q) {
+void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int band) {
     if (m < 2) return;
     // band scratch: only |i-j| <= 2 is ever non-zero (the chase's bulge), so
     // row i keeps columns i-2 .. i+2 (5 entries; same operations, same order
@@ -140,7 +141,10 @@ void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q) {
         if (!split[size_t(p)]) at(q, p - 1) = at(p - 1, q) = 0.0;  // bulge annihilated
         double* qp = Q + size_t(p) * m;
         double* qq = Q + size_t(q) * m;
-        for (int i = 0; i < m; ++i) {
+        // Q has lower bandwidth `band` before this sweep, so columns p and q
+        // are zero below row q + band: the rotation leaves those rows alone
+        const int iend = band >= 0 ? std::min(m, q + band + 1) : m;
+        for (int i = 0; i < iend; ++i) {
             const double a = qp[i], b = qq[i];
             qp[i] = c * a + s * b;
             qq[i] = -s * a + c * b;
