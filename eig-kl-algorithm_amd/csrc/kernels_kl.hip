@@ -113,15 +113,29 @@ __device__ __forceinline__ uint32_t side_of(const uint32_t* s_side, const uint8_
     else return g_side[v];
 }
 
-// bitmap word i of the side bytes (bit j = node 32i+j on side 1): the 32
-// bytes are read together (a byte-at-a-time loop waits for every load)
+// bitmap word i of the side bytes (bit j = node 32i+j on side 1): a whole
+// word is two 16-B loads (the byte array is hipMalloc'd, so 32i is 16-B
+// aligned); the last, partial word reads clamped bytes unconditionally.  (A
+// load behind a per-byte bounds branch waits for every load before it: the
+// byte-at-a-time form issued 32 dependent round trips per word.)
 __device__ __forceinline__ uint32_t side_word(const uint8_t* __restrict__ side, int n, int i) {
-    uint8_t v[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = i * 32 + j < n ? side[i * 32 + j] : 0;
+    const int base = i * 32;
     uint32_t b = 0;
+    if (base + 32 <= n) {
+        const uint4 a = *reinterpret_cast<const uint4*>(side + base);
+        const uint4 c = *reinterpret_cast<const uint4*>(side + base + 16);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
 #pragma unroll
-    for (int j = 0; j < 32; ++j) b |= uint32_t(v[j] == 1) << j;
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b |= uint32_t(((w[k] >> (8 * q)) & 0xffu) == 1u) << (4 * k + q);
+    } else {
+        uint8_t v[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) v[j] = side[min(base + j, n - 1)];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) b |= uint32_t(base + j < n && v[j] == 1) << j;
+    }
     return b;
 }
 
