@@ -1034,8 +1034,29 @@ void kl_prepare(hipStream_t s, const KLDev& d) {
     hipLaunchKernelGGL(k_chunk_init, dim3((waves + 3) / 4), dim3(256), 0, s, d);
 }
 
+// Streams `n16` 16-B pieces through the caches (nothing kept): after it the
+// array's lines sit in the Infinity Cache (MALL) as far as it holds them.
+__global__ __launch_bounds__(256) void k_touch(const int4* __restrict__ p, long long n16, int* __restrict__ sink) {
+    int acc = 0;
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n16; i += 256ll * gridDim.x) acc ^= p[i].x;
+    if (acc == 0x7fffabcd) sink[0] = acc;
+}
+
 void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out) {
     const size_t lds = kl_loop_lds_bytes(d);
+    // Warm the Infinity Cache with the per-entry arrays the swap loop reads at
+    // random (inline segments, then descriptors, so the descriptors are the
+    // most recent): most of its one dependent round trip per swap then hits
+    // the MALL instead of HBM.  ibm18 shape: 59.3 -> 57.9 ms for the swap
+    // loop, the two streams included (~50 us).  EK_KL_NOTOUCH=1: off (A/B).
+    if (!std::getenv("EK_KL_NOTOUCH")) {
+        int* sink = reinterpret_cast<int*>(&out->prof[13]);  // never written in practice
+        if (d.seg)
+            hipLaunchKernelGGL(k_touch, dim3(4096), dim3(256), 0, s, reinterpret_cast<const int4*>(d.seg),
+                               (long long)d.nnz * KL_SEG_LANES, sink);
+        hipLaunchKernelGGL(k_touch, dim3(1024), dim3(256), 0, s, reinterpret_cast<const int4*>(d.aux), (long long)d.nnz,
+                           sink);
+    }
     const bool prof = std::getenv("EK_KL_PROF") != nullptr;  // phase stamps: diagnostic instantiation
     const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
     if (lds && !global_state && prof)
