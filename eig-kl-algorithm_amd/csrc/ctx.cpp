@@ -80,7 +80,9 @@ struct ek_ctx {
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
         kl_ckey0, kl_ckey1, kl_aux, kl_seg, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
-    bool kl_graph_ready = false, kl_part_ready = false, kl_seg_ok = false;
+    bool kl_graph_ready = false, kl_part_ready = false, kl_seg_ok = false, kl_segc_ok = false;
+    DBuf kl_segc, kl_wdict;
+    int kl_nwd = 0, kl_wcolbits = 0;
     std::vector<int32_t> kl_rowptr_h;  // host copy (row descriptors)
     std::vector<hipEvent_t> spmv_ev;   // SpMV timing events, created once per context
 };
@@ -805,9 +807,32 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     HIPCHK(hipMemsetAsync(c->kl_w.as<float>() + nnz, 0, 16 * 4, s));
     if (nnz) HIPCHK(hipMemcpyAsync(c->kl_col.p, col, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
     if (nnz) HIPCHK(hipMemcpyAsync(c->kl_w.p, w, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
-    // inline neighbour-row segments for the swap loop (128 B per entry; skipped past 32 GB)
-    c->kl_seg_ok = size_t(nnz) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30);
+    // inline neighbour-row segments for the swap loop: weight-coded (128 B per
+    // entry) when the distinct weights fit the code bits and the LDS table,
+    // else plain (256 B per entry); skipped past 32 GB.  EK_KL_NOSEGC=1 at
+    // setup: plain (A/B, tests).
+    std::vector<uint32_t> kw;
+    std::vector<float> wdict;
+    int wcolbits = 0;
+    c->kl_segc_ok = !std::getenv("EK_KL_NOSEGC") &&
+                    size_t(nnz) * ek::dev::KL_SEGC_PIECES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30) &&
+                    ek::dev::kl_weight_codes(n, nnz, col, w, kw, wdict, wcolbits);
+    c->kl_seg_ok = !c->kl_segc_ok && size_t(nnz) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30);
+    if (c->kl_segc_ok) {
+        DBuf dkw;
+        upload(dkw, kw.data(), kw.size(), s);
+        upload(c->kl_wdict, wdict.data(), wdict.size(), s);
+        c->kl_nwd = int(wdict.size());
+        c->kl_wcolbits = wcolbits;
+        c->kl_seg.reset();
+        c->kl_segc.ensure(size_t(std::max<int64_t>(nnz, 1)) * ek::dev::KL_SEGC_PIECES * sizeof(ek::dev::KLInfo));
+        ek::dev::kl_build_segc(s, nnz, c->kl_rowptr.as<int32_t>(), c->kl_col.as<int32_t>(), dkw.as<uint32_t>(),
+                               c->kl_segc.as<ek::dev::KLInfo>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(s));  // dkw is freed at scope end
+    }
     if (c->kl_seg_ok) {
+        c->kl_segc.reset();
         c->kl_seg.ensure(size_t(std::max<int64_t>(nnz, 1)) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo));
         ek::dev::kl_build_seg(s, nnz, c->kl_rowptr.as<int32_t>(), c->kl_col.as<int32_t>(), c->kl_w.as<float>(),
                               c->kl_seg.as<ek::dev::KLInfo>());
@@ -949,7 +974,12 @@ ek::dev::KLDev kl_dev(ek_ctx* c) {
     d.cinfo0 = c->kl_cinfo0.as<ek::dev::KLInfo>();
     d.cinfo1 = c->kl_cinfo1.as<ek::dev::KLInfo>();
     d.aux = c->kl_aux.as<ek::dev::KLInfo>();
-    d.seg = c->kl_seg_ok && !std::getenv("EK_KL_NOSEG") ? c->kl_seg.as<ek::dev::KLInfo>() : nullptr;  // env: A/B
+    const bool noseg = std::getenv("EK_KL_NOSEG") != nullptr;  // env: A/B, no inline segments at all
+    d.seg = c->kl_seg_ok && !noseg ? c->kl_seg.as<ek::dev::KLInfo>() : nullptr;
+    d.segc = c->kl_segc_ok && !noseg ? c->kl_segc.as<ek::dev::KLInfo>() : nullptr;
+    d.wdict = c->kl_wdict.as<float>();
+    d.nwd = c->kl_nwd;
+    d.wcolbits = c->kl_wcolbits;
     d.n0 = int(c->kl_n0);
     d.n1 = int(c->kl_n1);
     d.nck0 = int((c->kl_n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK);

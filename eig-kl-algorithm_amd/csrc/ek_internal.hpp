@@ -209,7 +209,16 @@ struct KLDev {
     // per CSR entry p: the first 2*KL_SEG_LANES {col, w} entries of row col[p]
     // as KL_SEG_LANES 16-B pieces (zero-padded); null when it would not fit
     const KLInfo* seg = nullptr;
+    // the same 32 entries weight-coded (preferred; seg is then null): one
+    // 32-bit word (code << wcolbits) | col per entry, 4 per 16-B piece,
+    // KL_SEGC_PIECES pieces per p; word 0 pads (wdict[0] == 0.0f).  Half the
+    // bytes, so the segments and descriptors fit the Infinity Cache together.
+    const KLInfo* segc = nullptr;
+    const float* wdict = nullptr;  // exact fp32 weight of each code (nwd entries)
+    int nwd = 0, wcolbits = 0;
 };
+constexpr int KL_SEGC_PIECES = 8;
+constexpr int KL_WDICT_CAP = 4096;  // codes kept in LDS; more distinct weights: plain segments
 constexpr int KL_SEG_LANES = 16;  // 16-B pieces of 2 entries: 32 entries inline (all but 0.05% of touched rows; 16 inline: 70 vs 59 ms swap loop at ibm18 shape)
 constexpr int KL_ITEM_CAP = 256;  // updated rows whose new key/descriptor are kept in LDS (more: rederived, tagged)
 // LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
@@ -228,6 +237,12 @@ void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk ke
 // aux[p] = {col[p], nd[col[p]].{rowptr, len, plist}} for p < nnz (after the partition is set)
 void kl_build_aux(hipStream_t s, int64_t nnz, const int32_t* col, const KLInfo* nd, KLInfo* aux);
 void kl_build_seg(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* w, KLInfo* seg);
+// segc from the coded words kw[p] = (code << wcolbits) | col[p]
+void kl_build_segc(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const uint32_t* kw,
+                   KLInfo* segc);
+// weight dictionary of the KL graph (code 0 = 0.0f); false when it does not fit
+bool kl_weight_codes(int64_t n, int64_t nnz, const int32_t* col, const float* w, std::vector<uint32_t>& kw,
+                     std::vector<float>& wdict, int& wcolbits);
 void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out);
 // sides_out = side_init with the first `count` swaps of `log` applied (count on device: *best or *iters)
 void kl_replay(hipStream_t s, int n, const uint8_t* side_init, const ek_swap* log, const long long* count,

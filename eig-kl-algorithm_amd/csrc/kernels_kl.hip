@@ -31,7 +31,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "ek_internal.hpp"
 
@@ -275,7 +277,7 @@ size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
     const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_STAGE_ROW) * sizeof(KLInfo) +
                      (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4) * 8 +
-                     (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4;
+                     (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
     return b <= 152 * 1024 ? b : 0;
 }
 
@@ -366,7 +368,10 @@ __device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const
 // such a row, the chunk's key is exactly max(R, new keys of the updated rows
 // in the chunk); if R is one whose new key is below R, R was a stale value and
 // the chunk is rescanned after the barrier.
-template <bool PROF>
+// SEGC: the rows' inline segments are the weight-coded ones (KLDev::segc),
+// decoded through the weight table in LDS; the staged contributions and the
+// sums are the same as from the plain segments.
+template <bool PROF, bool SEGC>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int limit, ek_swap* __restrict__ log,
                                                                   long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
@@ -400,6 +405,9 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     int* s_stop = it_cs + KL_ITEM_CAP;  // [4], by iteration parity
     uint32_t* s_side = reinterpret_cast<uint32_t*>(s_stop + 4);
     uint32_t* s_lock = s_side + words;
+    float* s_wd = reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
+    if constexpr (SEGC)
+        for (int i = tid; i < d.nwd; i += KL_LOOP_THREADS) s_wd[i] = d.wdict[i];
     for (int i = tid; i < nsel; i += KL_LOOP_THREADS) {
         ck0[i] = i < d.nck0 ? d.ckey0[i] : 0ull;
         ck1[i] = i < d.nck1 ? d.ckey1[i] : 0ull;
@@ -532,16 +540,39 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 const int gi = i0 + (lane >> 3), j8 = lane & 7;
                 const int pg = gi < tot ? (gi < la ? pa + gi : pb + gi - la) : pa;
                 int4 piece[PPL];
+                if constexpr (SEGC) {  // one piece of 4 coded entries per lane (KL_SEGC_PIECES == 8 lanes)
+                    piece[0] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8);
+                } else {
 #pragma unroll
-                for (int r = 0; r < PPL; ++r)
-                    piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
-                                     : make_int4(0, 0, 0, 0);
+                    for (int r = 0; r < PPL; ++r)
+                        piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
+                                         : make_int4(0, 0, 0, 0);
+                }
                 const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
                 if constexpr (PROF) {
                     if (tid == 0 && (piece[0].x == -12345 || a.x == -12345)) s_stop[2] = 0;  // waits for the loads
                 }
                 stamp(10);
-                if (d.seg) {
+                if constexpr (SEGC) {
+                    // entries 4*j8 .. 4*j8+3: the same (internal, external) pairs the
+                    // plain segments stage, in pieces 2*j8 and 2*j8+1
+                    const uint32_t cmask = (1u << d.wcolbits) - 1u;
+                    const uint32_t wv4[4] = {uint32_t(piece[0].x), uint32_t(piece[0].y), uint32_t(piece[0].z),
+                                             uint32_t(piece[0].w)};
+                    float wk[4];
+                    bool ek4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        wk[k] = s_wd[wv4[k] >> d.wcolbits];
+                        ek4[k] = side_now(int(wv4[k] & cmask));
+                    }
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2)
+                        stage[(lane >> 3) * KL_STAGE_ROW + 2 * j8 + h2] = make_int4(
+                            __float_as_int(ek4[2 * h2] ? 0.0f : wk[2 * h2]), __float_as_int(ek4[2 * h2] ? wk[2 * h2] : 0.0f),
+                            __float_as_int(ek4[2 * h2 + 1] ? 0.0f : wk[2 * h2 + 1]),
+                            __float_as_int(ek4[2 * h2 + 1] ? wk[2 * h2 + 1] : 0.0f));
+                } else if (d.seg) {
                     // each lane looks up the sides of its own entries (4 LDS reads
                     // per wave instead of 32 serial ones by the summing lane) and
                     // stages every entry's (internal, external) contribution
@@ -560,7 +591,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 if (j8 != 0 || gi >= tot) continue;  // the row's first lane sums it
                 const int i = gi;
                 int4 sg[KL_SEG_LANES];  // per entry pair: (internal, external) contributions
-                if (d.seg) {
+                if (SEGC || d.seg) {
 #pragma unroll
                     for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_STAGE_ROW + j];
                 }
@@ -577,7 +608,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 {  // summed whether or not u is locked: a branch on `act` would let the
                    // compiler sink the segment loads behind the descriptor's round trip
                     int q = 0;
-                    if (d.seg) {
+                    if (SEGC || d.seg) {
                         // 8 entries per block; a block no row of this wave reaches
                         // is skipped as a whole (wave-uniform branch): the loop is
                         // issue-bound, and the zero padding would add exact zeros
@@ -1026,6 +1057,67 @@ void kl_build_seg(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32
                        col, w, seg);
 }
 
+// segc[p*KL_SEGC_PIECES + j] = coded entries 4j .. 4j+3 of row col[p] (word 0 past its end)
+__global__ __launch_bounds__(256) void k_build_segc(long long nnz, const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ col, const uint32_t* __restrict__ kw,
+                                                    KLInfo* __restrict__ segc) {
+    const long long t = blockIdx.x * 256ll + threadIdx.x;
+    const long long p = t / KL_SEGC_PIECES;
+    if (p >= nnz) return;
+    const int j = int(t % KL_SEGC_PIECES), v = col[p];
+    const int rp = rowptr[v], len = rowptr[v + 1] - rp;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = 4 * j + k < len ? kw[rp + 4 * j + k] : 0u;
+    segc[t] = KLInfo{int32_t(o[0]), int32_t(o[1]), int32_t(o[2]), int32_t(o[3])};
+}
+
+void kl_build_segc(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const uint32_t* kw,
+                   KLInfo* segc) {
+    if (nnz <= 0) return;
+    hipLaunchKernelGGL(k_build_segc, dim3(unsigned((nnz * KL_SEGC_PIECES + 255) / 256)), dim3(256), 0, s,
+                       (long long)nnz, rowptr, col, kw, segc);
+}
+
+// Exact fp32 weights by bit pattern: code 0 is 0.0f (the padding), the rest
+// in first-seen order.  Open addressing over the few distinct values (sums of
+// 1/(k-1) over shared nets: tens at ibm18 shape).
+bool kl_weight_codes(int64_t n, int64_t nnz, const int32_t* col, const float* w, std::vector<uint32_t>& kw,
+                     std::vector<float>& wdict, int& wcolbits) {
+    wcolbits = 1;
+    while (wcolbits < 31 && (int64_t(1) << wcolbits) < n) ++wcolbits;
+    if (wcolbits > 28) return false;
+    const size_t max_codes = std::min<size_t>(size_t(1) << (32 - wcolbits), size_t(KL_WDICT_CAP));
+    const size_t cap = 2 * size_t(KL_WDICT_CAP);  // power of two, at least twice the codes
+    std::vector<uint32_t> keys(cap);
+    std::vector<int32_t> slot(cap, -1);
+    auto find = [&](uint32_t k) -> size_t {
+        size_t h = size_t((k * 0x9E3779B1u) >> 19) & (cap - 1);
+        while (slot[h] >= 0 && keys[h] != k) h = (h + 1) & (cap - 1);
+        return h;
+    };
+    wdict.assign(1, 0.0f);
+    {
+        const size_t h = find(0u);
+        slot[h] = 0;
+        keys[h] = 0u;
+    }
+    kw.resize(size_t(std::max<int64_t>(nnz, 0)));
+    for (int64_t p = 0; p < nnz; ++p) {
+        uint32_t k;
+        std::memcpy(&k, &w[p], 4);
+        const size_t h = find(k);
+        if (slot[h] < 0) {
+            if (wdict.size() >= max_codes) return false;
+            slot[h] = int32_t(wdict.size());
+            keys[h] = k;
+            wdict.push_back(w[p]);
+        }
+        kw[size_t(p)] = (uint32_t(slot[h]) << wcolbits) | uint32_t(col[p]);
+    }
+    return true;
+}
+
 void kl_prepare(hipStream_t s, const KLDev& d) {
     const int nb = (d.n + 255) / 256;
     hipLaunchKernelGGL(k_gain_scan, dim3(nb), dim3(256), 0, s, d);
@@ -1051,7 +1143,10 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
     // loop, the two streams included (~50 us).  EK_KL_NOTOUCH=1: off (A/B).
     if (!std::getenv("EK_KL_NOTOUCH")) {
         int* sink = reinterpret_cast<int*>(&out->prof[13]);  // never written in practice
-        if (d.seg)
+        if (d.segc)
+            hipLaunchKernelGGL(k_touch, dim3(4096), dim3(256), 0, s, reinterpret_cast<const int4*>(d.segc),
+                               (long long)d.nnz * KL_SEGC_PIECES, sink);
+        else if (d.seg)
             hipLaunchKernelGGL(k_touch, dim3(4096), dim3(256), 0, s, reinterpret_cast<const int4*>(d.seg),
                                (long long)d.nnz * KL_SEG_LANES, sink);
         hipLaunchKernelGGL(k_touch, dim3(1024), dim3(256), 0, s, reinterpret_cast<const int4*>(d.aux), (long long)d.nnz,
@@ -1059,10 +1154,16 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
     }
     const bool prof = std::getenv("EK_KL_PROF") != nullptr;  // phase stamps: diagnostic instantiation
     const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
-    if (lds && !global_state && prof)
-        hipLaunchKernelGGL((k_kl_swap_loop<true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+    if (lds && !global_state && prof && d.segc)
+        hipLaunchKernelGGL((k_kl_swap_loop<true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+    else if (lds && !global_state && prof)
+        hipLaunchKernelGGL((k_kl_swap_loop<true, false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+    else if (lds && !global_state && d.segc)
+        hipLaunchKernelGGL((k_kl_swap_loop<false, true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap,
+                           out);
     else if (lds && !global_state)
-        hipLaunchKernelGGL((k_kl_swap_loop<false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        hipLaunchKernelGGL((k_kl_swap_loop<false, false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap,
+                           out);
     else if (prof)
         hipLaunchKernelGGL((k_kl_loop<false, true>), dim3(1), dim3(KL_LOOP_THREADS), 0, s, d, limit, log, cap, out);
     else
