@@ -1140,7 +1140,8 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
     // random (inline segments, then descriptors, so the descriptors are the
     // most recent): most of its one dependent round trip per swap then hits
     // the MALL instead of HBM.  ibm18 shape: 59.3 -> 57.9 ms for the swap
-    // loop, the two streams included (~50 us).  EK_KL_NOTOUCH=1: off (A/B).
+    // loop, the two streams included (~50 us); the chunk scans' descriptors
+    // as well: no further gain.  EK_KL_NOTOUCH=1: off (A/B).
     if (!std::getenv("EK_KL_NOTOUCH")) {
         int* sink = reinterpret_cast<int*>(&out->prof[13]);  // never written in practice
         if (d.segc)
