@@ -449,8 +449,16 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         // 32-63 remain[1]'s; identical in every wave
         u64 k = 0ull;
         {
+            // 8 keys per lane read together (clamped index: duplicates do not
+            // change a max); one read per trip waited for each LDS round trip
             const u64* ck = half ? ck1 : ck0;
-            for (int c = hl; c < nsel; c += 32) k = ck[c] > k ? ck[c] : k;
+            for (int c0 = hl; c0 < nsel; c0 += 8 * 32) {
+                u64 kv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) kv[u] = ck[min(c0 + 32 * u, nsel - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) k = kv[u] > k ? kv[u] : k;
+            }
             k = half_max_u64(k);
         }
         const u64 k0 = readlane_u64(k, 0), k1 = readlane_u64(k, 32);
