@@ -42,6 +42,9 @@ __device__ __forceinline__ double strided_sum256(const double* __restrict__ x, i
     return s;
 }
 
+constexpr int TT_ROWS = 1024;  // rows per three-term block (ldv is a multiple of GT_ROWS = 1024)
+static_assert(GT_ROWS % TT_ROWS == 0, "ldv must be a multiple of TT_ROWS");
+
 // block of 256: returns the block sum in thread 0
 __device__ __forceinline__ double block_sum256(double v, double* lds4) {
     v = wave_sum(v);
@@ -237,12 +240,18 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
                                                     double* __restrict__ fp) {
     __shared__ double lds4[4];
     __shared__ double s_alpha;
-    // the row loads go out first: they do not depend on alpha and overlap
-    // the reduction of its partials
-    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
-    double2 x = *reinterpret_cast<const double2*>(w + r);
-    const double2 v = *reinterpret_cast<const double2*>(vi + r);
-    const double2 u = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
+    // TT_ROWS rows per block (2 double2 per thread): fewer blocks re-reduce the
+    // alpha partials.  The row loads go out first: they do not depend on
+    // alpha and overlap the reduction of its partials.
+    constexpr int KR = TT_ROWS / 512;
+    double2 x[KR], v[KR], u[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const size_t r = size_t(blockIdx.x) * TT_ROWS + size_t(k) * 512 + 2 * size_t(threadIdx.x);
+        x[k] = *reinterpret_cast<const double2*>(w + r);
+        v[k] = *reinterpret_cast<const double2*>(vi + r);
+        u[k] = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
+    }
     // beta_i = ||f_i||, or 0 after an injected restart vector (override not NaN)
     const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
     if (nparts > 0) {
@@ -257,13 +266,18 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
     }
     __syncthreads();
     const double a = s_alpha;
-    x.x -= a * v.x;
-    x.y -= a * v.y;
-    if (vim1) {
-        x.x -= b * u.x;
-        x.y -= b * u.y;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const size_t r = size_t(blockIdx.x) * TT_ROWS + size_t(k) * 512 + 2 * size_t(threadIdx.x);
+        double2 y = x[k];
+        y.x -= a * v[k].x;
+        y.y -= a * v[k].y;
+        if (vim1) {
+            y.x -= b * u[k].x;
+            y.y -= b * u[k].y;
+        }
+        *reinterpret_cast<double2*>(fp + r) = y;
     }
-    *reinterpret_cast<double2*>(fp + r) = x;
 }
 
 // out[:, j] = sum_{i<m} V[:, i] Q[i, j], j < kk; grid (ldv/512, ceil(kk/8)).
@@ -361,7 +375,7 @@ void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, 
 
 void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,
                 const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp) {
-    hipLaunchKernelGGL(k_three_term, dim3(ldv / UPD_ROWS), dim3(256), 0, s, apart, nparts, alpha_io, w, vi, vim1, fn2_i,
+    hipLaunchKernelGGL(k_three_term, dim3(ldv / TT_ROWS), dim3(256), 0, s, apart, nparts, alpha_io, w, vi, vim1, fn2_i,
                        bov_i, fp);
 }
 
