@@ -159,6 +159,8 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     // makes the load wait for the ones before it.  The subtractions keep their
     // sequential order; x - v*0 == x for every x but -0.0, which these sums do
     // not produce (a difference of equal values rounds to +0).
+    // (One row per thread with 8-B loads in 512-thread blocks, twice the
+    // waves: 28 vs 20 us per step.)
     constexpr int UB = 8;
     const int jmax = ncols > 0 ? ncols - 1 : 0;
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
