@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     // not produce (a difference of equal values rounds to +0).
     // (One row per thread with 8-B loads in 512-thread blocks, twice the
     // waves: 28 vs 20 us per step.)
-    constexpr int UB = 8;
+    constexpr int UB = 8;  // 16: 21.5 vs 20.3 us
     const int jmax = ncols > 0 ? ncols - 1 : 0;
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
     auto load_batch = [&](double2* vb, int j0) {
