@@ -894,25 +894,19 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
     upload(c->kl_order1, order1, size_t(n1), s);
     upload(c->kl_side_init, side.data(), size_t(n), s);
     upload(c->kl_plist, plist.data(), size_t(n), s);
-    // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr, rowlen, plist}
+    // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr,
+    // rowlen, plist}, built on the device from the lists just uploaded (the
+    // by-position arrays are padded to whole chunks with zero descriptors, and
+    // the gains with NaN = invalid keys, so the chunk scans load unconditionally)
     {
-        const auto& rp = c->kl_rowptr_h;
-        // by-position arrays are padded to whole chunks (zero descriptors, NaN
-        // gains = invalid keys) so the chunk scans load unconditionally
-        std::vector<ek::dev::KLInfo> p0(size_t(chunk_pad(n0))), p1(size_t(chunk_pad(n1))), nd(static_cast<size_t>(n));
-        for (int64_t i = 0; i < n0; ++i) {
-            const int32_t u = order0[i];
-            p0[size_t(i)] = {u, rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], 0};
-        }
-        for (int64_t i = 0; i < n1; ++i) {
-            const int32_t u = order1[i];
-            p1[size_t(i)] = {u, rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], 0};
-        }
-        for (int64_t u = 0; u < n; ++u)
-            nd[size_t(u)] = {rp[size_t(u)], rp[size_t(u) + 1] - rp[size_t(u)], int32_t(plist[size_t(u)]), 0};
-        upload(c->kl_pinfo0, p0.data(), p0.size(), s);
-        upload(c->kl_pinfo1, p1.data(), p1.size(), s);
-        upload(c->kl_nd, nd.data(), nd.size(), s);
+        c->kl_pinfo0.ensure(size_t(chunk_pad(n0)) * sizeof(ek::dev::KLInfo));
+        c->kl_pinfo1.ensure(size_t(chunk_pad(n1)) * sizeof(ek::dev::KLInfo));
+        c->kl_nd.ensure(size_t(std::max<int64_t>(n, 1)) * sizeof(ek::dev::KLInfo));
+        ek::dev::kl_build_desc(s, int(n), int(n0), int(n1), int(chunk_pad(n0)), int(chunk_pad(n1)),
+                               c->kl_order0.as<int32_t>(), c->kl_order1.as<int32_t>(), c->kl_plist.as<uint32_t>(),
+                               c->kl_rowptr.as<int32_t>(), c->kl_pinfo0.as<ek::dev::KLInfo>(),
+                               c->kl_pinfo1.as<ek::dev::KLInfo>(), c->kl_nd.as<ek::dev::KLInfo>());
+        HIPCHK(hipGetLastError());
         const int64_t nnz = c->kl_rowptr_h[size_t(n)];
         c->kl_aux.ensure(size_t(std::max<int64_t>(nnz, 1)) * sizeof(ek::dev::KLInfo));
         ek::dev::kl_build_aux(s, nnz, c->kl_col.as<int32_t>(), c->kl_nd.as<ek::dev::KLInfo>(),
@@ -920,7 +914,7 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
         HIPCHK(hipGetLastError());
         c->kl_cinfo0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
         c->kl_cinfo1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
-        HIPCHK(hipStreamSynchronize(s));  // host staging vectors go out of scope
+        HIPCHK(hipStreamSynchronize(s));  // side / plist (host temporaries) have been copied
     }
     c->kl_gp0.ensure(size_t(chunk_pad(n0)) * 4);
     c->kl_gp1.ensure(size_t(chunk_pad(n1)) * 4);

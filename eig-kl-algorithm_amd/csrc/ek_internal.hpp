@@ -237,6 +237,10 @@ void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk ke
 // aux[p] = {col[p], nd[col[p]].{rowptr, len, plist}} for p < nnz (after the partition is set)
 void kl_build_aux(hipStream_t s, int64_t nnz, const int32_t* col, const KLInfo* nd, KLInfo* aux);
 void kl_build_seg(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* w, KLInfo* seg);
+// pinfo0/pinfo1 (by position, zero-padded to pad0/pad1) and nd (by node) of a partition
+void kl_build_desc(hipStream_t s, int n, int n0, int n1, int pad0, int pad1, const int32_t* order0,
+                   const int32_t* order1, const uint32_t* plist, const int32_t* rowptr, KLInfo* p0, KLInfo* p1,
+                   KLInfo* nd);
 // segc from the coded words kw[p] = (code << wcolbits) | col[p]
 void kl_build_segc(hipStream_t s, int64_t nnz, const int32_t* rowptr, const int32_t* col, const uint32_t* kw,
                    KLInfo* segc);

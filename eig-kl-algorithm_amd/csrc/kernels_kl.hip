@@ -1126,6 +1126,44 @@ bool kl_weight_codes(int64_t n, int64_t nnz, const int32_t* col, const float* w,
     return true;
 }
 
+// Row descriptors of a partition, from the uploaded lists (integers only):
+// by position in each list {node, rowptr, rowlen, 0}, zero past the list up to
+// the chunk padding; by node {rowptr, rowlen, plist, 0}.
+__global__ __launch_bounds__(256) void k_build_desc(int n, int n0, int n1, int pad0, int pad1,
+                                                    const int32_t* __restrict__ order0,
+                                                    const int32_t* __restrict__ order1,
+                                                    const uint32_t* __restrict__ plist,
+                                                    const int32_t* __restrict__ rowptr, KLInfo* __restrict__ p0,
+                                                    KLInfo* __restrict__ p1, KLInfo* __restrict__ nd) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < pad0) {
+        KLInfo v{0, 0, 0, 0};
+        if (i < n0) {
+            const int u = order0[i];
+            v = KLInfo{u, rowptr[u], rowptr[u + 1] - rowptr[u], 0};
+        }
+        p0[i] = v;
+    }
+    if (i < pad1) {
+        KLInfo v{0, 0, 0, 0};
+        if (i < n1) {
+            const int u = order1[i];
+            v = KLInfo{u, rowptr[u], rowptr[u + 1] - rowptr[u], 0};
+        }
+        p1[i] = v;
+    }
+    if (i < n) nd[i] = KLInfo{rowptr[i], rowptr[i + 1] - rowptr[i], int32_t(plist[i]), 0};
+}
+
+void kl_build_desc(hipStream_t s, int n, int n0, int n1, int pad0, int pad1, const int32_t* order0,
+                   const int32_t* order1, const uint32_t* plist, const int32_t* rowptr, KLInfo* p0, KLInfo* p1,
+                   KLInfo* nd) {
+    const int m = std::max(n, std::max(pad0, pad1));
+    if (m <= 0) return;
+    hipLaunchKernelGGL(k_build_desc, dim3((m + 255) / 256), dim3(256), 0, s, n, n0, n1, pad0, pad1, order0, order1,
+                       plist, rowptr, p0, p1, nd);
+}
+
 void kl_prepare(hipStream_t s, const KLDev& d) {
     const int nb = (d.n + 255) / 256;
     hipLaunchKernelGGL(k_gain_scan, dim3(nb), dim3(256), 0, s, d);
