@@ -271,11 +271,12 @@ __host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
 // staging row stride in 16-B pieces: one piece of padding, so the 8 summing
 // lanes of a wave (one per row) read 8 different bank groups instead of one
 constexpr int KL_STAGE_ROW = KL_SEG_LANES + 1;
+constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded, 8 plain)
 
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
-    const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * 8 * KL_STAGE_ROW) * sizeof(KLInfo) +
+    const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
                      (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4) * 8 +
                      (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
     return b <= 152 * 1024 ? b : 0;
@@ -390,8 +391,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     KLInfo* ci1 = ci0 + d.nck0;
     KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
     KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2][E_PARTS] early-rescan winners
-    int4* sg_stage = reinterpret_cast<int4*>(er_info + 2 * E_PARTS);  // [NG][8 rows][KL_SEG_LANES] G1 staging
-    u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * 8 * KL_STAGE_ROW);  // chunk keys (zero-padded to nsel)
+    int4* sg_stage = reinterpret_cast<int4*>(er_info + 2 * E_PARTS);  // [NG][KL_STAGE_ROWS][KL_STAGE_ROW] G1 staging
+    u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * KL_STAGE_ROWS * KL_STAGE_ROW);  // chunk keys (zero-padded to nsel)
     u64* ck1 = ck0 + nsel;
     u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
     u64* ckn1 = ckn0 + d.nck0;
@@ -537,23 +538,30 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // addressed by the CSR position alone, so every load of the row is
             // issued at once; the sums run strictly in row order, the
             // zero-weight padding of short segments adds exact zeros
-            int4* stage = sg_stage + wv * 8 * KL_STAGE_ROW;  // this wave's 8 rows x KL_SEG_LANES pieces (+1 pad)
-            for (int i0 = wv * 8; i0 < tot; i0 += NG * 8) {
-                // 8 lanes per row, each loading 16-B pieces j8, j8 + 8, ... of the
-                // row's inline segment: each instruction touches each 128-B line
-                // once.  (One lane loading all pieces of a line issues them as
-                // separate instructions on the same line, and each waits for the
-                // previous one's miss: serial L2 trips.)
-                constexpr int PPL = KL_SEG_LANES / 8;  // pieces per lane
-                const int gi = i0 + (lane >> 3), j8 = lane & 7;
+            // lanes per row: 8 for plain segments (2 pieces each), 4 for coded
+            // ones (2 pieces each): 16 rows per wave, 48 per pass over the
+            // three gain waves, so 0.1 % of the swaps (tot > 48) need a second
+            // pass instead of 11 % (tot > 24) at ibm18 shape
+            constexpr int LPR = SEGC ? 4 : 8, RPW = 64 / LPR;
+            int4* stage = sg_stage + wv * KL_STAGE_ROWS * KL_STAGE_ROW;  // this wave's rows x KL_SEG_LANES pieces (+1 pad)
+            for (int i0 = wv * RPW; i0 < tot; i0 += NG * RPW) {
+                // LPR lanes per row, each loading 16-B pieces j8, j8 + LPR, ... of
+                // the row's inline segment: each instruction touches each 128-B
+                // line once.  (One lane loading all pieces of a line issues them
+                // as separate instructions on the same line, and each waits for
+                // the previous one's miss: serial L2 trips.)
+                constexpr int PPL = (SEGC ? KL_SEGC_PIECES : KL_SEG_LANES) / LPR;  // pieces per lane
+                const int gi = i0 + lane / LPR, j8 = lane % LPR, srow = lane / LPR;
                 const int pg = gi < tot ? (gi < la ? pa + gi : pb + gi - la) : pa;
                 int4 piece[PPL];
-                if constexpr (SEGC) {  // one piece of 4 coded entries per lane (KL_SEGC_PIECES == 8 lanes)
-                    piece[0] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8);
+                if constexpr (SEGC) {  // pieces of 4 coded entries
+#pragma unroll
+                    for (int r = 0; r < PPL; ++r)
+                        piece[r] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8 + LPR * r);
                 } else {
 #pragma unroll
                     for (int r = 0; r < PPL; ++r)
-                        piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + 8 * r)
+                        piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + LPR * r)
                                          : make_int4(0, 0, 0, 0);
                 }
                 const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
@@ -562,24 +570,30 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 }
                 stamp(10);
                 if constexpr (SEGC) {
-                    // entries 4*j8 .. 4*j8+3: the same (internal, external) pairs the
-                    // plain segments stage, in pieces 2*j8 and 2*j8+1
+                    // piece q = j8 + LPR*r holds entries 4q .. 4q+3: the same
+                    // (internal, external) pairs the plain segments stage, in
+                    // staging pieces 2q and 2q+1
                     const uint32_t cmask = (1u << d.wcolbits) - 1u;
-                    const uint32_t wv4[4] = {uint32_t(piece[0].x), uint32_t(piece[0].y), uint32_t(piece[0].z),
-                                             uint32_t(piece[0].w)};
-                    float wk[4];
-                    bool ek4[4];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        wk[k] = s_wd[wv4[k] >> d.wcolbits];
-                        ek4[k] = side_now(int(wv4[k] & cmask));
+                    for (int r = 0; r < PPL; ++r) {
+                        const int q = j8 + LPR * r;
+                        const uint32_t wv4[4] = {uint32_t(piece[r].x), uint32_t(piece[r].y), uint32_t(piece[r].z),
+                                                 uint32_t(piece[r].w)};
+                        float wk[4];
+                        bool ek4[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            wk[k] = s_wd[wv4[k] >> d.wcolbits];
+                            ek4[k] = side_now(int(wv4[k] & cmask));
+                        }
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2)
+                            stage[srow * KL_STAGE_ROW + 2 * q + h2] = make_int4(
+                                __float_as_int(ek4[2 * h2] ? 0.0f : wk[2 * h2]),
+                                __float_as_int(ek4[2 * h2] ? wk[2 * h2] : 0.0f),
+                                __float_as_int(ek4[2 * h2 + 1] ? 0.0f : wk[2 * h2 + 1]),
+                                __float_as_int(ek4[2 * h2 + 1] ? wk[2 * h2 + 1] : 0.0f));
                     }
-#pragma unroll
-                    for (int h2 = 0; h2 < 2; ++h2)
-                        stage[(lane >> 3) * KL_STAGE_ROW + 2 * j8 + h2] = make_int4(
-                            __float_as_int(ek4[2 * h2] ? 0.0f : wk[2 * h2]), __float_as_int(ek4[2 * h2] ? wk[2 * h2] : 0.0f),
-                            __float_as_int(ek4[2 * h2 + 1] ? 0.0f : wk[2 * h2 + 1]),
-                            __float_as_int(ek4[2 * h2 + 1] ? wk[2 * h2 + 1] : 0.0f));
                 } else if (d.seg) {
                     // each lane looks up the sides of its own entries (4 LDS reads
                     // per wave instead of 32 serial ones by the summing lane) and
@@ -590,7 +604,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                         const bool e0 = side_now(pc.x);
                         const bool e1 = side_now(pc.z);
                         const float w0 = __int_as_float(pc.y), w1 = __int_as_float(pc.w);
-                        stage[(lane >> 3) * KL_STAGE_ROW + j8 + 8 * r] =
+                        stage[srow * KL_STAGE_ROW + j8 + LPR * r] =
                             make_int4(__float_as_int(e0 ? 0.0f : w0), __float_as_int(e0 ? w0 : 0.0f),
                                       __float_as_int(e1 ? 0.0f : w1), __float_as_int(e1 ? w1 : 0.0f));
                     }
@@ -601,7 +615,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 int4 sg[KL_SEG_LANES];  // per entry pair: (internal, external) contributions
                 if (SEGC || d.seg) {
 #pragma unroll
-                    for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[(lane >> 3) * KL_STAGE_ROW + j];
+                    for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[srow * KL_STAGE_ROW + j];
                 }
                 const int u = a.x, rp = a.y, len = a.z;
                 const bool act = !locked_now(u);
