@@ -171,6 +171,8 @@ void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x
 // x = x / sqrt(*n2) ... and deflate helpers
 void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* mean_sum, double inv_n);
 void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares);
+// x[0:ldv) = Park-Miller start vector over global rows row0.. (0 past nreal)
+void start_vector(hipStream_t s, int ldv, long long row0, int nreal, double* x);
 
 // kernels_kl.hip
 constexpr int KL_LOOP_THREADS = 512;  // 8 waves: 256 VGPRs per lane, no spills in the swap loop

@@ -389,6 +389,31 @@ void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x
     hipLaunchKernelGGL(k_axpby_norm, dim3(ldv / UPD_ROWS), dim3(256), 0, s, f, sigma, x, hk, npart);
 }
 
+// Lanczos start vector: x[r] = st_{row0+r+1} / (2^31 - 1) - 0.5 for the
+// Park-Miller sequence st_k = 16807^k mod (2^31 - 1) (Spectra SimpleRandom's
+// range), 0 on padded rows.  Each element by square-and-multiply: exact
+// integers, so the same doubles as the sequential host loop.
+__global__ __launch_bounds__(256) void k_start_vector(double* __restrict__ x, int ldv, long long row0, int nreal) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= ldv) return;
+    double v = 0.0;
+    if (r < nreal) {
+        constexpr unsigned long long P = 2147483647ull;
+        unsigned long long e = (unsigned long long)(row0 + r + 1), b = 16807ull, st = 1ull;
+        while (e) {
+            if (e & 1ull) st = (st * b) % P;
+            b = (b * b) % P;
+            e >>= 1;
+        }
+        v = double(st) / 2147483647.0 - 0.5;
+    }
+    x[r] = v;
+}
+
+void start_vector(hipStream_t s, int ldv, long long row0, int nreal, double* x) {
+    hipLaunchKernelGGL(k_start_vector, dim3((ldv + 255) / 256), dim3(256), 0, s, x, ldv, row0, nreal);
+}
+
 void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares) {
     hipLaunchKernelGGL(k_sum_partial, dim3(ldv / UPD_ROWS), dim3(256), 0, s, x, nreal, npart, squares);
 }
