@@ -85,6 +85,8 @@ struct ek_ctx {
     int kl_nwd = 0, kl_wcolbits = 0;
     std::vector<int32_t> kl_rowptr_h;  // host copy (row descriptors)
     std::vector<hipEvent_t> spmv_ev;   // SpMV timing events, created once per context
+    double* pin = nullptr;             // pinned host staging (Ritz vector + residual rows)
+    size_t pin_doubles = 0;
 };
 
 namespace {
@@ -159,6 +161,7 @@ void ek_destroy(ek_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
+    if (c->pin) (void)hipHostFree(c->pin);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -730,24 +733,33 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     HIPCHK(hipMemcpyAsync(c->Qd.p, Z.data() + size_t(want) * m, size_t(m) * 8, hipMemcpyHostToDevice, s));
     double* xloc = c->Vn.as<double>();
     ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), 1, xloc);
-    // full vector on every rank
-    std::vector<double> v(static_cast<size_t>(n));
+    // full vector on every rank; copied out through pinned staging kept by the
+    // context (pageable copies of these 2 x 8n bytes cost ~0.5 ms a solve)
+    const size_t need = size_t(n) + size_t(std::max<int64_t>(c->nrows, 1));
+    if (c->pin_doubles < need) {
+        if (c->pin) HIPCHK(hipHostFree(c->pin));
+        c->pin = nullptr;
+        c->pin_doubles = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pin), need * 8, hipHostMallocDefault));
+        c->pin_doubles = need;
+    }
+    double* v = c->pin;
+    double* y = c->pin + n;
     double* xg = xloc;
     if (c->nranks > 1) {
         NCCLCHK(ncclAllGather(xloc, c->xfull.as<double>(), size_t(c->nloc), ncclDouble, c->comm, s));
         xg = c->xfull.as<double>();
     }
-    HIPCHK(hipMemcpyAsync(v.data(), xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(v, xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
     // residual ||L x - lambda x|| on the owned rows
     ek::dev::spmv(s, spmv_mat(c), xg, c->w.as<double>(), nullptr, nullptr, nullptr, nullptr);
-    std::vector<double> y(size_t(std::max<int64_t>(c->nrows, 1)));
-    if (c->nrows) HIPCHK(hipMemcpyAsync(y.data(), c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
+    if (c->nrows) HIPCHK(hipMemcpyAsync(y, c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     double r2 = 0.0, nx2 = 0.0;
-    for (int64_t i = 0; i < n; ++i) nx2 += v[size_t(i)] * v[size_t(i)];
+    for (int64_t i = 0; i < n; ++i) nx2 += v[i] * v[i];
     const double inv = 1.0 / std::sqrt(nx2);
     for (int64_t i = 0; i < c->nrows; ++i) {
-        const double t = (y[size_t(i)] - lambda * v[size_t(c->row0 + i)]) * inv;
+        const double t = (y[i] - lambda * v[c->row0 + i]) * inv;
         r2 += t * t;
     }
     if (c->nranks > 1) {
@@ -758,13 +770,13 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         HIPCHK(hipStreamSynchronize(s));
     }
     // deterministic sign: the entry of largest magnitude (first on ties) is positive
-    size_t imax = 0;
-    for (size_t i = 1; i < v.size(); ++i)
+    int64_t imax = 0;
+    for (int64_t i = 1; i < n; ++i)
         if (std::fabs(v[i]) > std::fabs(v[imax])) imax = i;
     const double sgn = v[imax] < 0 ? -inv : inv;
-    for (double& t : v) t *= sgn;
     if (lambda_out) *lambda_out = lambda;
-    if (v_out) std::copy(v.begin(), v.end(), v_out);
+    if (v_out)
+        for (int64_t i = 0; i < n; ++i) v_out[i] = v[i] * sgn;
     if (stats) {
         stats->restarts = restarts;
         stats->matvecs = L.matvecs;
