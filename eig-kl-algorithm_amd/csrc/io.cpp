@@ -15,12 +15,41 @@ extern "C" {
 int ek_median_split(int64_t n, const double* v, double* median_out, uint8_t* bits_out) {
     EK_TRY
     if (n <= 0 || !v) ek::fail(EK_EINVAL, "ek_median_split: empty vector");
-    std::vector<double> s(v, v + n);
-    const size_t hi = size_t(n / 2);
-    std::nth_element(s.begin(), s.begin() + std::ptrdiff_t(hi), s.end());
-    double med = s[hi];
+    // The values at ranks hi = n/2 (and hi-1 for even n, whose mean is the
+    // median) are the ones nth_element over all of v returns.  Large n: a
+    // fixed-stride sample brackets them between two pivots, one pass counts
+    // the values below the lower pivot and keeps those inside the bracket,
+    // and nth_element runs on that ~2 % only; a bracket that misses (or a NaN
+    // in v) falls back to the whole vector.
+    const size_t hi = size_t(n / 2), rlo = n % 2 == 0 ? hi - 1 : hi;
+    std::vector<double> s;
+    size_t below = 0;
+    bool bracketed = false;
+    if (n >= (int64_t(1) << 16)) {
+        constexpr size_t NS = 4096, MARGIN = 96;  // sample size; pivots +-MARGIN samples around the median's
+        std::vector<double> smp(NS);
+        for (size_t k = 0; k < NS; ++k) smp[k] = v[size_t(k * size_t(n) / NS)];
+        std::sort(smp.begin(), smp.end());
+        const double plo = smp[NS / 2 - MARGIN], phi = smp[NS / 2 + MARGIN];
+        s.reserve(size_t(n) / 16);
+        bool nan = false;
+        for (int64_t i = 0; i < n; ++i) {
+            const double x = v[i];
+            if (x < plo) ++below;
+            else if (x <= phi) s.push_back(x);
+            else nan |= x != x;
+        }
+        bracketed = !nan && below <= rlo && hi < below + s.size();
+    }
+    if (!bracketed) {
+        s.assign(v, v + n);
+        below = 0;
+    }
+    const size_t h = hi - below;
+    std::nth_element(s.begin(), s.begin() + std::ptrdiff_t(h), s.end());
+    double med = s[h];
     if (n % 2 == 0) {  // mean of the two middle values
-        const double lo = *std::max_element(s.begin(), s.begin() + std::ptrdiff_t(hi));
+        const double lo = *std::max_element(s.begin(), s.begin() + std::ptrdiff_t(h));
         med = (lo + med) / 2.0;
     }
     if (median_out) *median_out = med;
