@@ -189,6 +189,28 @@ def test_median_split_rule(ek, n):
     assert np.array_equal(bits, (ref > v).astype(np.uint8))  # cEIG.cpp:218
 
 
+@pytest.mark.parametrize("n", [65535, 65536, 65537, 201920, 201921])
+@pytest.mark.parametrize("dist", ["normal", "sorted", "reversed", "constant", "half_zero", "few_values"])
+def test_median_split_large_bracketed(ek, n, dist):
+    """Past 64K values the median comes from a sample-bracketed selection
+    (falling back to the whole vector when the bracket misses): the same
+    value as a full sort for every shape of input."""
+    rng = np.random.default_rng(n)
+    v = {
+        "normal": lambda: rng.standard_normal(n) * 1e-3,
+        "sorted": lambda: np.sort(rng.standard_normal(n)),
+        "reversed": lambda: -np.sort(rng.standard_normal(n)),
+        "constant": lambda: np.full(n, 0.25),
+        "half_zero": lambda: np.concatenate([np.zeros(n // 2 + 1), rng.standard_normal(n - n // 2 - 1)]),
+        "few_values": lambda: rng.integers(0, 5, n).astype(np.float64) - 2.0,
+    }[dist]()
+    med, bits = ek.median_split(v)
+    s = np.sort(v)
+    ref = s[n // 2] if n % 2 else (s[n // 2 - 1] + s[n // 2]) / 2.0
+    assert med == ref
+    assert np.array_equal(bits, (ref > v).astype(np.uint8))
+
+
 # ------------------------------------------------------------- shard map
 @pytest.mark.parametrize("n,ranks", [(1000, 3), (201920, 8), (64, 8), (7, 2)])
 def test_shard_rows_tile_the_matrix(ek, n, ranks):
