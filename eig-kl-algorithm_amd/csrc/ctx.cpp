@@ -665,8 +665,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             double anorm = 1.0;
             for (int i = 0; i < m; ++i)
                 anorm = std::max(anorm, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
+            // from `from` itself: after an implicit restart the residual f_k
+            // can collapse (the kept Ritz space is invariant, seen on the 2x
+            // synthetic), and a zero column k would leave a spurious exact-zero
+            // Ritz pair whose vector is zero
             int j1 = -1;
-            for (int i = from + 1; i < m; ++i)
+            for (int i = std::max(from, 1); i < m; ++i)
                 if (!(std::sqrt(std::max(0.0, fn2_h[size_t(i)])) > beta_eps * anorm)) {
                     j1 = i;
                     break;
@@ -757,6 +761,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     HIPCHK(hipStreamSynchronize(s));
     double r2 = 0.0, nx2 = 0.0;
     for (int64_t i = 0; i < n; ++i) nx2 += v[i] * v[i];
+    if (!(nx2 > 0.0) || !std::isfinite(nx2))
+        ek::fail(EK_ENOCONV, "Lanczos: the Ritz vector is zero or not finite (|x|^2 = %g)", nx2);
     const double inv = 1.0 / std::sqrt(nx2);
     for (int64_t i = 0; i < c->nrows; ++i) {
         const double t = (y[i] - lambda * v[c->row0 + i]) * inv;

@@ -276,7 +276,9 @@ constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
-    const size_t b = (nck + KL_ITEM_CAP + 4 + (KL_LOOP_THREADS / 64 - 3) * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
+    // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * 2 (early rescans), as carved by the kernel
+    constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
+    const size_t b = (nck + KL_ITEM_CAP + 4 + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
                      (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4) * 8 +
                      (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
     return b <= 152 * 1024 ? b : 0;
@@ -381,6 +383,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     // waves 0 .. NG-1 run the gain updates
     constexpr int E_PARTS = 2, NQ_E = KL_CHUNK / 64 / E_PARTS;
     constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
+    static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * 2, "kl_loop_lds_bytes reserves staging for NG gain waves");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = lane >> 5, hl = lane & 31;

@@ -260,6 +260,20 @@ def test_lanczos_ibm10_unconverged_golden(ek, ctx):
     assert (bits != bits_ref).sum() <= 100  # survey: a converged solver differs on 48 bits
 
 
+def test_lanczos_synthetic_2x_restart_breakdown(ek, ctx):
+    """2x synthetic (configs[3]): after an implicit restart the residual
+    collapses to zero (the kept Ritz space is invariant); the run must
+    continue from a fresh vector, not return a zero Ritz vector."""
+    h = ek.Hypergraph.generate(2.0, 2)
+    L = h.laplacian()
+    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    lam, v, st = ctx.lanczos_fiedler()
+    assert np.all(np.isfinite(v)) and abs(np.linalg.norm(v) - 1) < 1e-10  # host fp64 norm over 404K values
+    assert st["converged"] and st["residual"] < 1e-8 and abs(lam) < 1e-8
+    _, bits = ek.median_split(v)
+    assert 0 < int(bits.sum()) < h.nodes
+
+
 def test_lanczos_deterministic_and_synthetic(ek, ctx):
     h = ek.Hypergraph.generate(0.25, 5)
     L = h.laplacian()
