@@ -37,6 +37,10 @@
 
 #include "ek_internal.hpp"
 
+#ifndef EK_E_SLEEP
+#define EK_E_SLEEP 4  // early-rescan waves: s_sleep units before their loads (2: same, 8: +0.9 ms per solve)
+#endif
+
 namespace ek {
 namespace dev {
 
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             const int p0 = (s ? cB : cA) * KL_CHUNK + part * NQ_E * 64;
             // let the gain-update waves' few row loads enter the CU's memory
             // pipeline ahead of these 16 KB (they are on the critical path)
-            __builtin_amdgcn_s_sleep(4);
+            __builtin_amdgcn_s_sleep(EK_E_SLEEP);
             KLInfo info;
             bool mine;
             const u64 kk = s ? chunk_rescan1<NQ_E>(d.gp1, d.pinfo1, 1, p0, posB, lane, &info, &mine)
