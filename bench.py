@@ -1,32 +1,53 @@
 #!/usr/bin/env python3
-"""bench.py — EIG+KL solve on MI355X (BASELINE.json metric).
+"""bench.py — wall-clock to the final cut on MI355X (BASELINE.json metric).
 
-One "step" = one full solve of the hot path on one synthetic ISPD98-shaped
-circuit whose CSR inputs are already resident in HBM: GPU Lanczos Fiedler
-vector (row-sharded over the ranks, RCCL all-reduce/all-gather over xGMI when
-N > 1) -> median split -> GPU KL swap loop to termination (rank 0; the swap
-loop is a sequential dependency chain) -> integer net cut.
+One step = one in-process run of the whole hot path on a .hgr file, the body
+of `gKL2 <file> -EIG` (ek_solve_file): parse -> clique Laplacian -> GPU
+Lanczos Fiedler vector (rows sharded over the ranks, RCCL all-gather /
+all-reduce over xGMI when N > 1) -> median split -> KL adjacency (host, built
+while the GPU solves) -> GPU KL swap loop to termination (rank 0: the loop is a
+sequential dependency chain) -> results/<base>_KL_CutSize_EIG_output.txt.
 
-N = 1 workload: ibm18-shape = build generator at 1.0x, seed 1 (BASELINE
-configs[2]; ibm18.hgr itself is not shipped).  `value` = seconds per solve
-(lower is better).  N > 1: the SAME circuit, Lanczos rows sharded across the
-ranks (strong scaling of the sharded phase; KL stays on rank 0).
+N = 1 workload: configs[2] "ibm18.hgr EIG+KL on 1 MI355X".  ibm18.hgr is not
+shipped, so the stand-in is the seeded ISPD98-shaped synthetic at 1.0x, seed 1
+(201,920 nodes), written to a file in the untimed setup.  `value` = seconds
+per step (lower is better), the GPU context staying up across steps like a
+service (a fresh process also pays HIP start-up: `e2e_fresh_process_s`).
+N > 1: the same file; the Lanczos rows are sharded (strong scaling of the
+sharded phase), the KL loop stays on rank 0.  `--gpus N` without WORLD_SIZE
+starts the N ranks itself (torch.distributed.run, before any GPU call).
 
-Also reported: `roofline` of the dominant-by-contract kernel (the Lanczos CSR
-SpMV, HIP events around every launch in the timed steps), `cpu_baseline`
-(the oracle port on this host, bounded sample), the end-to-end wall time of
-the file-based path (parse + build + upload + solve) and cut sizes.
+Also reported: `roofline` of the Lanczos SpMV (HIP kernel timestamps of the
+SpMVs of the timed steps; SURVEY §8d algorithmic bytes; PMC traffic from
+rocprofv3 passes over a resident solve run as child processes before the
+GPU is touched here), `cpu_baseline` (the oracle restatement on this host's
+cores, 1 core and all cores, whole solve, swap log compared), per-config
+sub-results (ibm01, ibm10, 2x, the 1x synthetic's largest connected
+component), the resident-input solve time and the syn10 sharded Lanczos phase.
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GOLD = os.path.join(REPO, "tests", "golden", "circuit")
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def load_pkg():
@@ -38,206 +59,376 @@ def load_pkg():
     return mod
 
 
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def pmc_traffic(mult, seed, work):
+    """FETCH_SIZE / WRITE_SIZE of the Lanczos SpMV, one rocprofv3 pass each over
+    tools/spmv_probe.py (a resident solve), run BEFORE this process touches the
+    GPU.  Per dispatch, kB -> bytes.  Returns a dict or None."""
+    if not shutil.which("rocprofv3"):
+        return None
+    out = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(work, f"pmc_{ctr}")
+        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o",
+               "p", "--", sys.executable, os.path.join(REPO, "tools", "spmv_probe.py"), str(mult), str(seed)]
+        env = dict(os.environ, TMPDIR="/tmp")
+        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            log(f"rocprofv3 {ctr} pass failed (rc {r.returncode}): {r.stderr[-300:]}")
+            return None
+        vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(files[0]))
+                if "k_spmv_adaptive" in row["Kernel_Name"]]
+        if not vals:
+            return None
+        out[ctr] = sum(vals) / len(vals) * 1024.0
+        out[ctr + "_dispatches"] = len(vals)
+    return out
+
+
+def cpu_baseline(hgr, split_npz, threads):
+    """oracle/cpu_baseline.py in a child process (CPU only), pinned to `threads` cores."""
+    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), hgr, split_npz, str(threads)]
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="true")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mult", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--ncv", type=int, default=0)
+    ap.add_argument("--comm", choices=["auto", "rccl", "host"], default="auto",
+                    help="multi-rank exchange: RCCL over xGMI, or host-staged (several ranks per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-sweep", action="store_true", help="skip the SpMV size sweep")
-    ap.add_argument("--cpu-matvecs", type=int, default=40, help="oracle Lanczos matvecs timed for the CPU baseline")
+    ap.add_argument("--no-extras", action="store_true", help="skip sub-configs, sweep, PMC and syn10 legs")
+    ap.add_argument("--no-pmc", action="store_true")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started before any GPU call or package import
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    ek = load_pkg()
-    dist = None
+    if world != args.gpus:
+        log(f"WORLD_SIZE {world} != --gpus {args.gpus}: reporting the {world} ranks that run")
+    work = tempfile.mkdtemp(prefix=f"ekbench_r{rank}_")
+    extras = not args.no_extras and world == 1
+
+    # PMC passes first: child processes, before this process touches the GPU
+    pmc = None
+    if extras and not args.no_pmc:
+        t = time.time()
+        pmc = pmc_traffic(args.mult, args.seed, work)
+        log(f"PMC passes {time.time() - t:.1f} s: {pmc}")
+
+    import torch.distributed as dist
     if world > 1:
-        import torch
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo")
-        dist = tdist
+        dist.init_process_group("gloo")
 
     def barrier():
-        if dist:
+        if world > 1:
             dist.barrier()
 
     def max_over_ranks(x):
-        if not dist:
+        if world == 1:
             return x
         import torch
         t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # ---------------- setup (untimed): inputs resident in HBM
-    t_setup = time.time()
+    ek = load_pkg()
+    ndev = ek.device_count()
+    comm = args.comm
+    if world > 1 and comm == "auto":
+        comm = "rccl" if ndev >= world else "host"
+    ctx = ek.Context(local_rank % max(ndev, 1))
+    if world > 1:
+        if comm == "rccl":
+            uid = [ek.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            ctx.comm_init(world, rank, uid[0])
+        else:
+            import torch
+
+            def allgather(x):
+                parts = [torch.empty(len(x), dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(parts, torch.from_numpy(x))
+                return torch.cat(parts).numpy()
+
+            def allreduce(x):
+                t = torch.from_numpy(x)  # shares memory: in place
+                dist.all_reduce(t)
+
+            ctx.comm_init_host(world, rank, allgather, allreduce)
+
+    # ---------------- untimed setup: the workload file
     h = ek.Hypergraph.generate(args.mult, args.seed)
     nets, n, npins = h.dims()
-    L = h.laplacian()
-    ctx = ek.Context(local_rank)
-    if world > 1:
-        import torch
-        uid = [ek.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(world, rank, uid[0])
-    row0, nrows, _ = ek.shard_rows(n, world, rank)
-    rp = L.rowptr[row0: row0 + nrows + 1].astype(np.int64)
-    ctx.spmv_setup(n, row0, (rp - rp[0]).astype(np.int32), L.col[rp[0]: rp[-1]], L.val[rp[0]: rp[-1]])
-    if rank == 0:
-        G = h.kl_graph()
-        net_ptr, pins = h.pins()
-        ctx.kl_graph_setup(G)
-        ctx.kl_nets_setup(net_ptr, pins)
-    setup_s = time.time() - t_setup
+    path = os.path.join(work, f"syn{args.mult:g}x_seed{args.seed}.hgr")
+    h.write(path)
+    out_dir = os.path.join(work, "out")
+    os.makedirs(out_dir, exist_ok=True)
 
-    def solve(time_spmv):
-        lam, v, st = ctx.lanczos_fiedler(ncv=args.ncv, time_spmv=time_spmv)
-        res = None
-        if rank == 0:
-            med, bits = ek.median_split(v)
-            ctx.kl_set_partition_bits(bits)  # cKL -EIG split order (cKL.cpp:155-174)
-            _, res = ctx.kl_run(cap=0)
-        return lam, st, res
+    def step(time_spmv=False):
+        return ctx.solve_file(path, eig=1, out_dir=out_dir, write_results=(rank == 0), time_spmv=time_spmv,
+                              log_cap=(n // 2 if rank == 0 else 0))
 
     for _ in range(args.warmup):
-        solve(False)
+        step()
     barrier()
+    ctx.synchronize()
     t0 = time.time()
-    stats = []
+    results = []
     for _ in range(args.steps):
-        stats.append(solve(True))
+        results.append(step(time_spmv=True))
+    ctx.synchronize()
     barrier()
     elapsed = max_over_ranks(time.time() - t0)
-    sec_per_solve = elapsed / args.steps
+    sec_per_step = elapsed / args.steps
+    last, swap_log = results[-1]
+    lz = [r[0]["lanczos"] for r in results]
+    spmv_timed = sum(x["spmv_timed"] for x in lz)
+    spmv_us = 1e3 * sum(x["spmv_ms"] for x in lz) / max(1, spmv_timed)
+    comm_ms = sum(x["comm_ms"] for x in lz) / len(lz)
+    phases = {k: round(float(np.median([r[0][k] for r in results])), 4) for k in
+              ("t_read", "t_laplacian", "t_lanczos", "t_split", "t_kl_graph_wait", "t_kl_setup", "t_kl", "t_write",
+               "t_total")}
+    row0, nrows, _ = ek.shard_rows(n, world, rank)
+    alg_bytes = ctx.spmv_bytes(fused=False)  # SURVEY §8d: 12 nnz + 4(nrows+1) + 8n (x) + 8 nrows (y)
+    fused_bytes = ctx.spmv_bytes(fused=True)  # + the fused epilogue's f read and basis-column write
+    packed, stored = ctx.spmv_format(fused=True)
+    # the same for every rank: every rank's SpMV is timed; report rank 0's and the max
+    spmv_us_max = max_over_ranks(spmv_us)
+    nnz_local = int((alg_bytes - 4 * (nrows + 1) - 8 * n - 8 * nrows) // 12)
 
-    lam, st, kres = stats[-1]
-    spmv_launch_ms = sum(s[1]["spmv_ms"] for s in stats) / max(1, sum(s[1]["spmv_timed"] for s in stats))
-    spmv_bytes = ctx.spmv_bytes(fused=True)  # the Lanczos SpMV also reads f and writes the basis column
-    spmv_packed, spmv_stored = ctx.spmv_format(fused=True)  # what the kernel actually streams
-    achieved = spmv_bytes / (spmv_launch_ms * 1e-3) / 1e9 if spmv_launch_ms > 0 else 0.0
+    # ---------------- resident-input solve (inputs already in HBM): the solve alone
+    L_rows = None
+    resident = None
+    res_bits = res_log = None
+    if rank == 0 or world > 1:
+        Lr = h.laplacian()
+        rp = Lr.rowptr[row0: row0 + nrows + 1].astype(np.int64)
+        ctx.spmv_setup(n, row0, (rp - rp[0]).astype(np.int32), Lr.col[rp[0]: rp[-1]], Lr.val[rp[0]: rp[-1]])
+        L_rows = Lr
+        if rank == 0:
+            ctx.kl_graph_setup(h.kl_graph())
+            ctx.kl_nets_setup(*h.pins())
+        times, kres, klog, bits_r = [], None, None, None
+        for i in range(4):
+            barrier()
+            t = time.time()
+            lam_r, v_r, st_r = ctx.lanczos_fiedler()
+            if rank == 0:
+                _, bits_r = ek.median_split(v_r)
+                ctx.kl_set_partition_bits(bits_r)
+                klog, kres = ctx.kl_run()
+            ctx.synchronize()
+            barrier()
+            if i:
+                times.append(max_over_ranks(time.time() - t))
+        resident = {"solve_s": round(float(np.median(times)), 5), "lanczos_ms": round(st_r["total_ms"], 3),
+                    "lanczos_matvecs": st_r["matvecs"]}
+        if rank == 0:
+            res_bits, res_log = bits_r, klog
+            resident.update({"kl_loop_ms": round(kres["loop_ms"], 3), "kl_iterations": kres["iterations"],
+                             "us_per_swap": round(1e3 * kres["loop_ms"] / max(1, kres["iterations"]), 3),
+                             "swap_log_equals_timed_steps": bool(world == 1 and len(klog) == len(swap_log) and
+                                                                 klog.tobytes() == swap_log.tobytes())})
+
+    # ---------------- syn10 (configs[4]): the sharded Lanczos phase at this N
+    syn10 = None
+    if not args.no_extras:
+        h10 = ek.Hypergraph.generate(10.0, 10)
+        n10 = h10.nodes
+        r0, nr, _ = ek.shard_rows(n10, world, rank)
+        c10 = ctx
+        L10 = h10.laplacian_rows(r0, r0 + nr)
+        c10.spmv_setup(n10, r0, L10.rowptr, L10.col, L10.val)
+        del L10
+        st10 = None
+        tt = []
+        for i in range(2):
+            barrier()
+            t = time.time()
+            _, _, st10 = c10.lanczos_fiedler(time_spmv=(i == 1))
+            c10.synchronize()
+            barrier()
+            tt.append(max_over_ranks(time.time() - t))
+        b10 = c10.spmv_bytes(fused=False)
+        us10 = 1e3 * st10["spmv_ms"] / max(1, st10["spmv_timed"])
+        us10_max = max_over_ranks(us10)
+        syn10 = {"workload": "synthetic 10x seed 10", "nodes": n10, "ranks": world, "lanczos_s": round(tt[-1], 4),
+                 "matvecs": st10["matvecs"], "spmv_us_per_launch_max_rank": round(us10_max, 3),
+                 "spmv_bytes_per_rank": int(b10),
+                 "spmv_GBps_per_gpu": round(b10 / us10_max / 1e3, 1),
+                 "spmv_frac_per_gpu": round(b10 / us10_max / 1e3 / HBM_PEAK_GBS, 4),
+                 "spmv_GBps_aggregate": round(world * b10 / us10_max / 1e3, 1),
+                 "comm_ms_per_solve": round(max_over_ranks(st10["comm_ms"]), 3), "comm": comm if world > 1 else None}
+        del h10
+
     if rank != 0:
+        ctx.close()
+        if world > 1:
+            dist.destroy_process_group()
         return
 
-    # ---------------- SpMV size sweep (untimed, informational): back-to-back
-    # launches on resident buffers for the 1x workload and the 2x / 10x configs
+    # ---------------- sub-configs (N = 1): the file path on other inputs
+    subs = {}
+    if extras:
+        hl, _ = h.largest_component()
+        inputs = [("ibm01", os.path.join(GOLD, "ibm01.hgr"), "configs[1] ibm01.hgr (shipped)"),
+                  ("ibm10", os.path.join(GOLD, "ibm10.hgr"), "ibm10.hgr: the largest shipped ISPD98 circuit, connected"),
+                  ("syn1_lcc", None, "largest connected component of the 1x seed-1 synthetic (non-degenerate Fiedler)"),
+                  ("syn2", None, "configs[3] circuit_generator 2.0x shape, seed 2")]
+        for name, p, what in inputs:
+            if p is None:
+                p = os.path.join(work, f"{name}.hgr")
+                (hl if name == "syn1_lcc" else ek.Hypergraph.generate(2.0, 2)).write(p)
+            walls, rr = [], None
+            for i in range(3):
+                t = time.time()
+                rr, _ = ctx.solve_file(p, eig=1, out_dir=out_dir)
+                walls.append(time.time() - t)
+            subs[name] = {"what": what, "nodes": rr["nodes"], "wall_s": round(float(np.median(walls[1:])), 4),
+                          "lambda1": rr["lambda"], "matvecs": rr["lanczos"]["matvecs"],
+                          "restarts": rr["lanczos"]["restarts"], "lanczos_s": round(rr["t_lanczos"], 4),
+                          "kl_iterations": rr["kl"]["iterations"], "kl_s": round(rr["t_kl"], 4),
+                          "best_cut": rr["kl"]["best_cut"], "net_cut_best": rr["kl"]["net_cut_best"],
+                          "best_iter": rr["kl"]["best_iter"]}
+            log(f"sub-config {name}: {subs[name]}")
+
+    # ---------------- SpMV size sweep (informational, back-to-back launches)
     sweep = []
-    if world == 1 and not args.no_sweep:
-        # (mult, storage): the shipped (dictionary-coded) form at each size, and
-        # the plain int32 col + fp64 val CSR at the bench size for comparison
-        for mult, plain in ((args.mult, False), (args.mult, True), (2.0, False), (10.0, False)):
-            if mult == args.mult and not plain:
-                c2, b2 = ctx, spmv_bytes
-            else:
-                hs = h if mult == args.mult else ek.Hypergraph.generate(mult, int(mult))
-                Ls = L if mult == args.mult else hs.laplacian()
-                c2 = ek.Context(local_rank)
-                if plain:
-                    os.environ["EK_SPMV_PLAIN"] = "1"
-                try:
-                    c2.spmv_setup(hs.nodes, 0, Ls.rowptr, Ls.col, Ls.val)
-                finally:
-                    os.environ.pop("EK_SPMV_PLAIN", None)
-                b2 = c2.spmv_bytes(fused=True)
-            packed2, stored2 = c2.spmv_format(fused=True)
-            us = c2.spmv_bench(200, fused=True)
-            sweep.append({"mult": mult, "storage": "dict32" if packed2 else "csr", "bytes_per_launch": int(b2),
-                          "stored_bytes_per_launch": int(stored2), "avg_launch_us": round(us, 3),
+    if extras:
+        for mult, seed in ((args.mult, args.seed), (2.0, 2)):
+            hs = h if mult == args.mult else ek.Hypergraph.generate(mult, seed)
+            Ls = L_rows if mult == args.mult else hs.laplacian()
+            c2 = ek.Context(0)
+            c2.spmv_setup(hs.nodes, 0, Ls.rowptr, Ls.col, Ls.val)
+            us = c2.spmv_bench(200, fused=False)
+            b2 = c2.spmv_bytes(fused=False)
+            sweep.append({"mult": mult, "bytes_per_launch": int(b2), "avg_launch_us": round(us, 3),
                           "GB/s": round(b2 / us / 1e3, 1), "frac": round(b2 / us / 1e3 / HBM_PEAK_GBS, 4)})
-            if c2 is not ctx:
-                c2.close()
+            c2.close()
 
-    # ---------------- end-to-end wall of the file-based drop-in path (untimed above)
-    e2e = None
-    try:
-        import subprocess
-        import tempfile
-        with tempfile.TemporaryDirectory() as tmp:
-            hp = os.path.join(tmp, "ibm18_shape.hgr")
-            h.write(hp)
-            tool = os.path.join(REPO, "eig-kl-algorithm_amd", "build", "bin", "gKL2")
-            t1 = time.time()
-            subprocess.run([tool, hp, "-EIG", "--quiet"], cwd=tmp, check=True, timeout=300)
-            e2e = time.time() - t1
-    except Exception as exc:  # report, do not hide
-        e2e = f"failed: {exc}"
+    # ---------------- fresh-process wall of the drop-in tool (HIP start-up included)
+    fresh = None
+    if extras:
+        tool = os.path.join(REPO, "eig-kl-algorithm_amd", "build", "bin", "gKL2")
+        walls = []
+        for _ in range(5):
+            t = time.time()
+            r = subprocess.run([tool, path, "-EIG", "--quiet"], cwd=out_dir, capture_output=True, timeout=300)
+            walls.append(time.time() - t)
+            if r.returncode != 0:
+                walls = [f"failed rc {r.returncode}: {r.stderr[-200:]!r}"]
+                break
+        fresh = round(float(np.median(walls)), 4) if isinstance(walls[0], float) else walls[0]
 
-    # ---------------- CPU baseline: the oracle port on this host (bounded sample)
+    # ---------------- CPU baseline: oracle restatement on this host, 1 core and all cores
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle as O  # test/baseline infrastructure only
-        net_ptr, pins = h.pins()
-        g = O.Graph.from_pins(n, net_ptr, pins)
-        t1 = time.time()
-        _, _, ost = g.lanczos(deflate=True, max_matvec=args.cpu_matvecs)
-        t_eig_sample = time.time() - t1
-        per_mv = t_eig_sample / max(1, ost["matvecs"])
-        eig_est = per_mv * st["matvecs"]
-        _, v_gpu, _ = ctx.lanczos_fiedler(ncv=args.ncv)
-        med, bits = ek.median_split(v_gpu)
-        idx = np.arange(n, dtype=np.int32)
-        t1 = time.time()
-        _, ores = g.kl(idx[bits == 0], idx[bits == 1], cap=0)
-        t_kl = time.time() - t1
-        cpu = {"value": round(eig_est + t_kl, 3), "unit": "s", "cores": 1, "kind": "port",
-               "sample": (f"oracle thick-restart Lanczos timed for its first {ost['matvecs']} matvecs "
-                          f"({t_eig_sample:.2f} s, extrapolated x{st['matvecs'] / max(1, ost['matvecs']):.1f} to the "
-                          f"GPU solve's {st['matvecs']} matvecs) + full oracle cKL swap loop from the GPU split "
-                          f"({t_kl:.2f} s, {ores['iterations']} swaps, bit-identical result)"),
-               "kl_iterations_match": ores["iterations"] == kres["iterations"]}
+    if extras and not args.no_cpu_baseline:
+        # the resident leg's split and swap log (bit-identical to the timed steps': checked below)
+        bits = res_bits
+        split_npz = os.path.join(work, "split.npz")
+        np.savez(split_npz, bits=bits, log=res_log)
+        ncpu = len(os.sched_getaffinity(0))
+        all_cores = min(16, ncpu)  # the GPU box grants each job a 16-CPU share
+        legs = {}
+        for t in sorted({1, all_cores}):
+            tt = time.time()
+            legs[t] = cpu_baseline(path, split_npz, t)
+            log(f"cpu baseline {t} thread(s): {time.time() - tt:.1f} s: {legs[t]}")
+        best = legs[all_cores]
+        if "error" not in best:
+            cpu = {"value": round(best["total_s"], 3), "unit": "s", "cores": best["threads"], "kind": "port",
+                   "sample": ("whole solve on the oracle restatement of cEIG+cKL (oracle/eko_eig.cpp, eko_kl.cpp), "
+                              f"OpenMP on {best['threads']} pinned host cores: parse, Laplacian + Lanczos to "
+                              f"convergence ({best['lanczos_matvecs']} matvecs), KL() from the GPU run's split "
+                              f"({best['kl_iterations']} swaps, swap log compared with the GPU's)"),
+                   "parse_s": best["parse_s"], "lanczos_s": best["lanczos_s"], "kl_s": best["kl_s"],
+                   "swap_log_match": best["swap_log_match"], "first_mismatch": best["first_mismatch"],
+                   "net_cut_match": best["net_cut_best"] == last["kl"]["net_cut_best"] and
+                   best["net_cut_final"] == last["kl"]["net_cut_final"],
+                   "one_core": legs[1] if all_cores != 1 else None,
+                   "reference_cKL_note": "real cKL (oracle/_ref, built from /root/reference) is O(n^2) in setup and "
+                                         "per swap (cKL.cpp:53-72, 225-251): see BASELINE.md for its measured times"}
+        else:
+            cpu = {"error": best["error"]}
 
-    # PMC traffic (committed rocprofv3 summary of this workload), per SpMV launch
-    traffic = rocprof_us = None
-    pmc_path = os.path.join(REPO, "profiles", "spmv_pmc_bytes.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("workload") == f"syn{args.mult:g}x-seed{args.seed}" and world == 1:
-                traffic = pm.get("hbm_bytes_per_launch")
-                rocprof_us = pm.get("rocprof_avg_launch_us")
-        except Exception:
-            traffic = rocprof_us = None
+    roof = {"bound": "hbm", "kernel": f"k_spmv_adaptive<512,{str(packed).lower()}> (Lanczos CSR SpMV, fp64)",
+            "achieved": round(alg_bytes / spmv_us / 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg_bytes / spmv_us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": int(alg_bytes),
+            "bytes_rule": "SURVEY §8d: 12 nnz + 4 (n+1) + 8 n (x) + 8 n (y)",
+            "avg_launch_us": round(spmv_us, 3), "launches_timed": spmv_timed,
+            "timing": "HIP kernel start/end timestamps (hipExtLaunchKernelGGL events on the context stream) of every "
+                      "4th SpMV of each Lanczos cycle, inside the timed steps",
+            "fused_bytes_per_launch": int(fused_bytes),
+            "fused_frac": round(fused_bytes / spmv_us / 1e3 / HBM_PEAK_GBS, 4),
+            "stored_bytes_per_launch": int(stored),
+            "storage": ("dictionary-coded CSR: 32-bit (code<<colbits | col) words + exact fp64 value table"
+                        if packed else "CSR: int32 col + fp64 val"),
+            "sweep_back_to_back": sweep}
+    if pmc:
+        f_raw, w_raw = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
+        roof["traffic"] = round(2 * f_raw + w_raw)
+        roof["traffic_detail"] = {
+            "fetch_raw_bytes": round(f_raw), "write_bytes": round(w_raw), "dispatches": pmc["FETCH_SIZE_dispatches"],
+            "correction": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide reads, "
+                          "MI355X_MICROARCH.md HBM; this kernel's widths: see profiles/r02/pmc_calib.txt); "
+                          "L2 memory-side requests, Infinity-Cache hits included",
+            "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over tools/spmv_probe.py in this run"}
 
     out = {
         "metric": "wall-clock to final cut (s) + cut size, ibm18.hgr; SpMV GB/s vs HBM peak",
-        "value": round(sec_per_solve, 6),
+        "value": round(sec_per_step, 6),
         "unit": "s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(sec_per_solve * 1e3, 4),
+        "ms_per_step": round(sec_per_step * 1e3, 4),
         "higher_is_better": False,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64 (Lanczos) + f32 (KL gains, bit-exact with cKL)",
-        "data": "synthetic (seeded ISPD98-shaped generator; ibm18.hgr not shipped)",
-        "config": {"workload": f"ibm18-shape synthetic {args.mult:g}x seed {args.seed}", "nodes": n, "nets": nets,
-                   "pins": npins, "laplacian_nnz": L.nnz, "parallelism": f"lanczos row-shard x{world}, KL 1 GPU"},
-        "roofline": {"bound": "hbm", "kernel": f"k_spmv_adaptive<512,{str(spmv_packed).lower()}> (Lanczos CSR SpMV, fp64, fused epilogue)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_per_launch": spmv_bytes, "avg_launch_us": round(spmv_launch_ms * 1e3, 3),
-                     "storage": ("dictionary-coded CSR: 32-bit (code<<colbits | col) words + exact fp64 value table"
-                                 if spmv_packed else "CSR: int32 col + fp64 val"),
-                     "stored_bytes_per_launch": spmv_stored,
-                     "timing": "kernel start/end timestamps (hipExtLaunchKernelGGL events) of every 4th SpMV of each Lanczos cycle in the timed solves",
-                     "rocprof_avg_launch_us": rocprof_us,  # committed kernel-trace summary of this workload
-                     "sweep": sweep},
+        "data": "synthetic (seeded ISPD98-shaped generator written to .hgr; ibm18.hgr not shipped)",
+        "config": {"workload": f"ibm18-shape synthetic {args.mult:g}x seed {args.seed}: .hgr file -> results file",
+                   "nodes": n, "nets": nets, "pins": npins, "laplacian_nnz": nnz_local if world == 1 else None,
+                   "parallelism": f"lanczos row-shard x{world} ({comm if world > 1 else 'single'}), KL 1 GPU"},
+        "roofline": roof,
         "cpu_baseline": cpu,
-        "result": {"lambda1": lam, "lanczos_matvecs": st["matvecs"], "lanczos_restarts": st["restarts"],
-                   "lanczos_ms": round(st["total_ms"], 3), "residual": st["residual"],
-                   "kl_iterations": kres["iterations"], "kl_loop_ms": round(kres["loop_ms"], 3),
-                   "initial_cut": kres["initial_cut"], "best_cut": kres["best_cut"],
-                   "net_cut_best": kres["net_cut_best"], "best_iter": kres["best_iter"]},
-        "e2e_file_wall_s": round(e2e, 4) if isinstance(e2e, float) else e2e,
-        "setup_s": round(setup_s, 3),
+        "result": {"lambda1": last["lambda"], "lanczos_matvecs": last["lanczos"]["matvecs"],
+                   "lanczos_restarts": last["lanczos"]["restarts"], "residual": last["lanczos"]["residual"],
+                   "kl_iterations": last["kl"]["iterations"], "kl_loop_ms": round(last["kl"]["loop_ms"], 3),
+                   "initial_cut": last["kl"]["initial_cut"], "best_cut": last["kl"]["best_cut"],
+                   "net_cut_best": last["kl"]["net_cut_best"], "net_cut_final": last["kl"]["net_cut_final"],
+                   "best_iter": last["kl"]["best_iter"], "phases_median_s": phases,
+                   "comm_ms_per_step": round(comm_ms, 3), "spmv_us_max_rank": round(spmv_us_max, 3),
+                   "resident_solve": resident},
+        "e2e_fresh_process_s": fresh,
+        "configs": subs,
+        "syn10_sharded_lanczos": syn10,
     }
     print(json.dumps(out), flush=True)
+    ctx.close()
+    shutil.rmtree(work, ignore_errors=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -57,6 +57,26 @@ class KLResult(ctypes.Structure):
                 ("total_ms", ctypes.c_double)]
 
 
+class SolveOpts(ctypes.Structure):
+    _fields_ = [("eig", _I32), ("seed", ctypes.c_uint32), ("write_results", _I32), ("limit", _I32),
+                ("out_dir", ctypes.c_char_p), ("sign_ref", ctypes.c_char_p), ("lanczos", LanczosOpts)]
+
+
+_SOLVE_TIMES = ("t_read", "t_laplacian", "t_lanczos", "t_split", "t_kl_graph_wait", "t_kl_setup", "t_kl",
+                "t_write", "t_total")
+
+
+class SolveResult(ctypes.Structure):
+    _fields_ = ([("nets", _I64), ("nodes", _I64), ("pins", _I64), ("lambda_", ctypes.c_double),
+                 ("median", ctypes.c_double), ("lanczos", LanczosStats), ("kl", KLResult)]
+                + [(k, ctypes.c_double) for k in _SOLVE_TIMES])
+
+
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), _I64,
+                                ctypes.POINTER(ctypes.c_double))
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), _I64)
+
+
 def _sig(name, res, *args):
     fn = getattr(_lib, name)
     fn.restype = res
@@ -75,6 +95,8 @@ _sig("ek_hgr_copy_pins", ctypes.c_int, _P, _P, _P)
 _sig("ek_hgr_free", None, _P)
 _sig("ek_laplacian_build", ctypes.c_int, _P, ctypes.POINTER(_P))
 _sig("ek_kl_graph_build", ctypes.c_int, _P, ctypes.POINTER(_P))
+_sig("ek_laplacian_build_rows", ctypes.c_int, _P, _I64, _I64, ctypes.POINTER(_P))
+_sig("ek_synchronize", ctypes.c_int, _P)
 _sig("ek_csr_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I32))
 _sig("ek_csr_copy", ctypes.c_int, _P, _P, _P, _P, _P)
 _sig("ek_csr_free", None, _P)
@@ -86,6 +108,12 @@ _sig("ek_destroy", None, _P)
 _sig("ek_get_stream", ctypes.c_int, _P, ctypes.POINTER(_P))
 _sig("ek_comm_unique_id", ctypes.c_int, _P)
 _sig("ek_comm_init", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P)
+_sig("ek_comm_init_host", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ALLGATHER_FN, ALLREDUCE_FN, _P)
+_sig("ek_hgr_largest_component", ctypes.c_int, _P, ctypes.POINTER(_P), _P)
+_sig("ek_random_split", ctypes.c_int, _I64, ctypes.c_uint32, _P, _P)
+_sig("ek_solve_default_opts", None, ctypes.POINTER(SolveOpts))
+_sig("ek_solve_file", ctypes.c_int, _P, ctypes.c_char_p, ctypes.POINTER(SolveOpts), _P, _I64,
+     ctypes.POINTER(SolveResult))
 _sig("ek_spmv_setup", ctypes.c_int, _P, _I64, _I64, _I64, _P, _P, _P)
 _sig("ek_spmv", ctypes.c_int, _P, _P, _P, _P)
 _sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
@@ -213,10 +241,23 @@ class Hypergraph:
     def write(self, path):
         _chk(_lib.ek_hgr_write(self._h, os.fsencode(path)), f"write {path}")
 
+    def largest_component(self):
+        """(Hypergraph of the largest connected component, node map old -> new or -1)."""
+        c = _P()
+        m = np.empty(self.nodes, np.int32)
+        _chk(_lib.ek_hgr_largest_component(self._h, ctypes.byref(c), _p(m)), "largest_component")
+        return Hypergraph(c), m
+
     def laplacian(self):
         """fp64 clique Laplacian (cEIG.cpp:86-133)."""
         c = _P()
         _chk(_lib.ek_laplacian_build(self._h, ctypes.byref(c)), "laplacian")
+        return _take_csr(c)
+
+    def laplacian_rows(self, row0, row1):
+        """Rows [row0, row1) of the Laplacian (global columns, rowptr from 0): one rank's shard."""
+        c = _P()
+        _chk(_lib.ek_laplacian_build_rows(self._h, int(row0), int(row1 - row0), ctypes.byref(c)), "laplacian_rows")
         return _take_csr(c)
 
     def kl_graph(self):
@@ -261,6 +302,14 @@ def eig_read(path, n):
     return lam.value, med.value, bits, v, o0[: n0.value].copy(), o1[: n1.value].copy()
 
 
+def random_split(n, seed):
+    """cKL.cpp:176-192 with std::mt19937(seed): (remain[0], remain[1])."""
+    o0 = np.empty(n // 2, np.int32)
+    o1 = np.empty(n - n // 2, np.int32)
+    _chk(_lib.ek_random_split(int(n), int(seed) & 0xFFFFFFFF, _p(o0), _p(o1)), "random_split")
+    return o0, o1
+
+
 def device_count():
     c = ctypes.c_int()
     _lib.ek_device_count(ctypes.byref(c))
@@ -292,6 +341,9 @@ class Context:
     def __del__(self):
         self.close()
 
+    def synchronize(self):
+        _chk(_lib.ek_synchronize(self._c), "synchronize")
+
     @property
     def stream(self):
         s = _P()
@@ -299,8 +351,36 @@ class Context:
         return s.value
 
     def comm_init(self, nranks, rank, uid):
+        """RCCL over xGMI (one process per GPU)."""
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         _chk(_lib.ek_comm_init(self._c, int(nranks), int(rank), buf), "comm_init")
+
+    def comm_init_host(self, nranks, rank, allgather, allreduce):
+        """Host-staged exchange (ek_comm_init_host): allgather(send: ndarray) -> ndarray of nranks*len(send),
+        allreduce(buf: ndarray) -> None (in-place sum), e.g. over torch.distributed gloo."""
+        def ag(_user, send, count, recv):
+            try:
+                src = np.ctypeslib.as_array(send, shape=(count,))
+                dst = np.ctypeslib.as_array(recv, shape=(count * nranks,))
+                dst[:] = allgather(src.copy())
+                return 0
+            except Exception:  # a failed collective must not unwind through C
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def ar(_user, buf, count):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(count,)))
+                return 0
+            except Exception:
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._comm_cbs = (ALLGATHER_FN(ag), ALLREDUCE_FN(ar))  # kept alive with the context
+        _chk(_lib.ek_comm_init_host(self._c, int(nranks), int(rank), self._comm_cbs[0], self._comm_cbs[1], None),
+             "comm_init_host")
 
     # SpMV seam (SparseSymMatProd::perform_op, cEIG.cpp:194)
     def spmv_setup(self, n, row0, rowptr, col, val):
@@ -378,6 +458,26 @@ class Context:
         _chk(_lib.ek_kl_run(self._c, int(limit), _p(log), cap, ctypes.byref(r)), "kl_run")
         res = {k: getattr(r, k) for k, _ in KLResult._fields_}
         return log[: min(r.iterations, cap)], res
+
+    def solve_file(self, path, eig=1, seed=0, write_results=True, out_dir=None, limit=-1, sign_ref=None, ncv=0,
+                   tol=1e-10, deflate=True, time_spmv=False, log_cap=0):
+        """The whole path, .hgr -> results/ (ek_solve_file).  eig: 1 GPU Fiedler split (gKL2 -EIG), 2 the
+        pre_saved_EIG file (cKL -EIG), 0 random split with std::mt19937(seed).  Returns (result dict, swap log)."""
+        o = SolveOpts()
+        _lib.ek_solve_default_opts(ctypes.byref(o))
+        o.eig, o.seed, o.write_results, o.limit = int(eig), int(seed) & 0xFFFFFFFF, 1 if write_results else 0, int(limit)
+        o.out_dir = os.fsencode(out_dir) if out_dir else None
+        o.sign_ref = os.fsencode(sign_ref) if sign_ref else None
+        o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, 1)
+        log = np.zeros(max(int(log_cap), 1), SWAP_DTYPE)
+        r = SolveResult()
+        _chk(_lib.ek_solve_file(self._c, os.fsencode(path), ctypes.byref(o), _p(log), int(log_cap), ctypes.byref(r)),
+             f"solve_file {path}")
+        out = {k: getattr(r, k) for k in ("nets", "nodes", "pins", "median") + _SOLVE_TIMES}
+        out["lambda"] = r.lambda_
+        out["lanczos"] = {k: getattr(r.lanczos, k) for k, _ in LanczosStats._fields_}
+        out["kl"] = {k: getattr(r.kl, k) for k, _ in KLResult._fields_}
+        return out, log[: min(int(log_cap), r.kl.iterations)]
 
     def kl_sides(self, which):
         out = np.empty(self.kl_n, np.uint8)

@@ -65,9 +65,15 @@ inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::d
 struct ek_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // RCCL
+    // RCCL, or the host-staged exchange of ek_comm_init_host
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    ek_allgather_fn host_ag = nullptr;
+    ek_allreduce_fn host_ar = nullptr;
+    void* host_user = nullptr;
+    double* stage = nullptr;  // pinned staging of the host-staged exchange
+    size_t stage_doubles = 0;
+    double comm_ms = 0.0;     // host-observed time inside collectives (current solve)
     // Laplacian rows owned by this context
     int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
     int block_nnz = 1024, nrb_spmv = 0;
@@ -117,9 +123,76 @@ ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
     return m;
 }
 
-// In-place sum all-reduce of `count` doubles on the context stream.
+double* stage_for(ek_ctx* c, size_t doubles) {
+    if (c->stage_doubles < doubles) {
+        if (c->stage) HIPCHK(hipHostFree(c->stage));
+        c->stage = nullptr;
+        c->stage_doubles = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->stage), doubles * 8, hipHostMallocDefault));
+        c->stage_doubles = doubles;
+    }
+    return c->stage;
+}
+
+struct CommTimer {  // host-observed time of one collective
+    ek_ctx* c;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~CommTimer() { c->comm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
+}  // namespace
+
+void ek::ctx_ranks(ek_ctx* c, int* rank, int* nranks) {
+    if (!c) fail(EK_EINVAL, "null ek_ctx");
+    if (rank) *rank = c->rank;
+    if (nranks) *nranks = c->nranks;
+}
+
+namespace {
+
+// In-place sum all-reduce of `count` device doubles, ordered on the context
+// stream.  RCCL: enqueued on the stream.  Host-staged: stream drained, the
+// operand staged through pinned memory around the caller's collective.
 void allreduce(ek_ctx* c, double* p, size_t count) {
-    if (c->nranks > 1 && count) NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, c->comm, c->stream));
+    if (c->nranks <= 1 || !count) return;
+    if (c->comm) {
+        NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, c->comm, c->stream));
+        return;
+    }
+    CommTimer t{c};
+    double* h = stage_for(c, count);
+    HIPCHK(hipMemcpyAsync(h, p, count * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->host_ar(c->host_user, h, int64_t(count)) != 0) ek::fail(EK_ECOMM, "host all-reduce callback failed");
+    HIPCHK(hipMemcpyAsync(p, h, count * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer is reused by the next collective
+}
+
+// recv[r*count .. (r+1)*count) = rank r's send block (rank-major), on the stream.
+void allgather(ek_ctx* c, const double* send, size_t count, double* recv) {
+    if (c->comm) {
+        NCCLCHK(ncclAllGather(send, recv, count, ncclDouble, c->comm, c->stream));
+        return;
+    }
+    CommTimer t{c};
+    const size_t tot = count * size_t(c->nranks);
+    double* h = stage_for(c, count + tot);
+    HIPCHK(hipMemcpyAsync(h, send, count * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->host_ag(c->host_user, h, int64_t(count), h + count) != 0)
+        ek::fail(EK_ECOMM, "host all-gather callback failed");
+    HIPCHK(hipMemcpyAsync(recv, h + count, tot * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+void comm_reset(ek_ctx* c) {
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    c->host_ag = nullptr;
+    c->host_ar = nullptr;
+    c->host_user = nullptr;
+    c->nranks = 1;
+    c->rank = 0;
 }
 
 }  // namespace
@@ -162,6 +235,7 @@ void ek_destroy(ek_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
     if (c->pin) (void)hipHostFree(c->pin);
+    if (c->stage) (void)hipHostFree(c->stage);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -170,6 +244,14 @@ int ek_get_stream(ek_ctx* c, void** s) {
     EK_TRY
     check_ctx(c);
     if (s) *s = c->stream;
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_synchronize(ek_ctx* c) {
+    EK_TRY
+    check_ctx(c);
+    HIPCHK(hipStreamSynchronize(c->stream));
     return EK_OK;
     EK_CATCH
 }
@@ -188,17 +270,31 @@ int ek_comm_init(ek_ctx* c, int nranks, int rank, const void* id128) {
     EK_TRY
     check_ctx(c);
     if (nranks < 1 || rank < 0 || rank >= nranks || !id128) ek::fail(EK_EINVAL, "ek_comm_init: bad argument");
-    if (c->comm) {
-        ncclCommDestroy(c->comm);
-        c->comm = nullptr;
-    }
-    c->nranks = nranks;
-    c->rank = rank;
+    comm_reset(c);
     if (nranks > 1) {
         ncclUniqueId id;
         std::memcpy(&id, id128, sizeof id);
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
     }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->n = 0;  // the shard map changed: ek_spmv_setup again
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_comm_init_host(ek_ctx* c, int nranks, int rank, ek_allgather_fn ag, ek_allreduce_fn ar, void* user) {
+    EK_TRY
+    check_ctx(c);
+    if (nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && (!ag || !ar)))
+        ek::fail(EK_EINVAL, "ek_comm_init_host: bad argument");
+    comm_reset(c);
+    c->nranks = nranks;
+    c->rank = rank;
+    c->host_ag = ag;
+    c->host_ar = ar;
+    c->host_user = user;
+    c->n = 0;
     return EK_OK;
     EK_CATCH
 }
@@ -398,7 +494,7 @@ struct Lanczos {
     // x for the matvec: the full vector (gathered when sharded)
     const double* gather_f() {
         if (c->nranks == 1) return c->f.as<double>();
-        NCCLCHK(ncclAllGather(c->f.as<double>(), c->xfull.as<double>(), size_t(c->nloc), ncclDouble, c->comm, s));
+        allgather(c, c->f.as<double>(), size_t(c->nloc), c->xfull.as<double>());
         return c->xfull.as<double>();
     }
 
@@ -570,6 +666,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     ek_lanczos_default_opts(&o);
     if (opts) o = *opts;
     const auto t0 = std::chrono::steady_clock::now();
+    c->comm_ms = 0.0;
     const int64_t n = c->n;
     const bool deflate = o.deflate != 0;
     const int nev = deflate ? 1 : 2;
@@ -644,14 +741,31 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
 
     std::vector<double> d(size_t(m), 0.0), e(size_t(m), 0.0), theta(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
     std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
-    int k = 0, restarts = 0, nconv = 0, breakdowns = 0;
+    int k = 0, restarts = 0, nconv = 0, injected = 0;
+    double fn2_k = 1.0;  // ||f_k||^2 entering a cycle (after an implicit restart: the restart's residual)
     bool converged = false;
     const double beta_eps = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     double host_restart_ms = 0.0, device_cycle_ms = 0.0, host_qr_ms = 0.0;  // EK_LANCZOS_TRACE diagnostics
+    auto anorm_of = [&] {
+        double a = 1.0;
+        for (int i = 0; i < m; ++i) a = std::max(a, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
+        return a;
+    };
     for (;;) {
         HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
         const auto tc = std::chrono::steady_clock::now();
-        for (int from = k;;) {
+        int cycle_breakdowns = 0;  // bounded per cycle: each one moves the factorisation forward
+        int from = k;
+        // After an implicit restart the residual f_k can collapse (the kept
+        // Ritz space is invariant, seen on the 2x synthetic): a zero column k
+        // would leave a spurious exact-zero Ritz pair whose vector is zero, so
+        // the cycle starts from a fresh vector at k instead of running on it.
+        if (k > 0 && !(std::sqrt(std::max(0.0, fn2_k)) > beta_eps * anorm_of())) {
+            if (trace) std::fprintf(stderr, "[lanczos] restart residual collapsed at %d (|f|^2=%.3e)\n", k, fn2_k);
+            ++cycle_breakdowns;
+            L.inject(k, ++injected);
+        }
+        for (;;) {
             L.factorize(from);
             L.collect_spmv_times(from);
             HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
@@ -662,13 +776,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                 d[size_t(i)] = alpha_h[size_t(i)];
                 if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
             }
-            double anorm = 1.0;
-            for (int i = 0; i < m; ++i)
-                anorm = std::max(anorm, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
-            // from `from` itself: after an implicit restart the residual f_k
-            // can collapse (the kept Ritz space is invariant, seen on the 2x
-            // synthetic), and a zero column k would leave a spurious exact-zero
-            // Ritz pair whose vector is zero
+            const double anorm = anorm_of();
             int j1 = -1;
             for (int i = std::max(from, 1); i < m; ++i)
                 if (!(std::sqrt(std::max(0.0, fn2_h[size_t(i)])) > beta_eps * anorm)) {
@@ -677,8 +785,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                 }
             if (j1 < 0) break;
             if (trace) std::fprintf(stderr, "[lanczos] breakdown at step %d (|f|^2=%.3e)\n", j1, fn2_h[size_t(j1)]);
-            if (++breakdowns > 4 * m) ek::fail(EK_ENOCONV, "Lanczos: repeated breakdown");
-            L.inject(j1, breakdowns);
+            if (++cycle_breakdowns > m) ek::fail(EK_ENOCONV, "Lanczos: repeated breakdown within one cycle");
+            L.inject(j1, ++injected);
             from = j1;
         }
         const auto th = std::chrono::steady_clock::now();
@@ -715,9 +823,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
                             c->npart.as<double>());
         L.reduce_scalar(c->fn2.as<double>() + knew);
+        HIPCHK(hipMemcpyAsync(&fn2_k, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
         std::swap(c->V.p, c->Vn.p);
         std::swap(c->V.bytes, c->Vn.bytes);
-        HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart
+        HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read
         for (int i = 0; i < knew; ++i) d[size_t(i)] = dd[size_t(i)];
         for (int i = 0; i + 1 < knew; ++i) e[size_t(i)] = ee[size_t(i)];
         k = knew;
@@ -751,7 +860,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     double* y = c->pin + n;
     double* xg = xloc;
     if (c->nranks > 1) {
-        NCCLCHK(ncclAllGather(xloc, c->xfull.as<double>(), size_t(c->nloc), ncclDouble, c->comm, s));
+        allgather(c, xloc, size_t(c->nloc), c->xfull.as<double>());
         xg = c->xfull.as<double>();
     }
     HIPCHK(hipMemcpyAsync(v, xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
@@ -791,7 +900,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         stats->spmv_ms = L.spmv_ms;
         stats->spmv_timed = L.spmv_timed;
-        stats->comm_ms = 0.0;
+        stats->comm_ms = c->comm_ms;
     }
     return EK_OK;
     EK_CATCH

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -24,6 +25,8 @@ int guard_exceptions();  // maps the in-flight exception to a status (call from 
 int host_threads();
 template <class F>
 void parallel_for(int64_t n, F&& fn);  // fn(begin, end)
+template <class F>
+void run_threads(int T, F&& fn);  // fn(t) for t < T, t = 0 on the calling thread
 }  // namespace ek
 
 #define EK_TRY try {
@@ -50,6 +53,7 @@ struct ek_csr {
 namespace ek {
 // graph_build.cpp
 void build_laplacian(const ek_hgr& h, ek_csr& out);
+void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& out);  // rows [r0, r1), global cols
 void build_kl_graph(const ek_hgr& h, ek_csr& out);
 // libstdc++ unordered_map<uint32_t,...> iteration order for keys inserted
 // (first insertion) in the given order; writes the iteration order to out.
@@ -64,6 +68,19 @@ bool tridiag_eig(int m, const double* d, const double* e, double* evals, double*
 // band >= 0: Q's lower bandwidth before this step (0 for the identity, +1 per
 // step), so rows below it are skipped; -1: full columns.
 void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int band = -1);
+}  // namespace ek
+
+// ---------------------------------------------------------------------------
+// the in-process pipeline (solve.cpp) and the context's rank (ctx.cpp)
+namespace ek {
+void ctx_ranks(ek_ctx* ctx, int* rank, int* nranks);
+// get_ctx is called when the GPU is first needed (the CLI initialises it on
+// a helper thread meanwhile); rank / nranks are the context's.
+void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const ek_hgr& h, const std::string& base,
+           const ek_solve_opts& o, ek_swap* log_out, int64_t cap, ek_solve_result& r);
+void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek_solve_opts& o, double& lambda,
+                    std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
+                    const std::function<void()>& after_laplacian = {});
 }  // namespace ek
 
 // ---------------------------------------------------------------------------
@@ -276,5 +293,14 @@ void ek::parallel_for(int64_t n, F&& fn) {
         const int64_t b = n * t / T, e = n * (t + 1) / T;
         th.emplace_back([&fn, b, e] { fn(b, e); });
     }
+    for (auto& x : th) x.join();
+}
+
+template <class F>
+void ek::run_threads(int T, F&& fn) {
+    std::vector<std::thread> th;
+    th.reserve(size_t(std::max(T - 1, 0)));
+    for (int t = 1; t < T; ++t) th.emplace_back([&fn, t] { fn(t); });
+    if (T >= 1) fn(0);
     for (auto& x : th) x.join();
 }

@@ -120,85 +120,125 @@ void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vect
 // (b,a); duplicates are summed (in net order here; setFromTriplets' order is
 // thread-dependent in the reference); then diag = -(sum of row i in ascending
 // column order, including any (i,i) triplets from repeated pins).
-void build_laplacian(const ek_hgr& h, ek_csr& L) {
-    const int64_t n = h.nodes;
-    std::vector<int64_t> cnt(size_t(n) + 1, 0);
+//
+// Row-major form: every row is assembled from its own pin incidences (nets in
+// ascending order, so each (row, col) sum runs in net order; contributions of
+// one net are equal, so their order inside the net cannot change a bit),
+// sorted by column, merged, and given its diagonal.  Threads own contiguous
+// row ranges and write their rows to private buffers that are then copied into
+// place, so there is no per-row allocation.  Rows [r0, r1) only: the shard of
+// one rank of the sharded Lanczos (col keeps global ids).
+void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& L) {
+    const int64_t n = h.nodes, nr = r1 - r0;
+    if (r0 < 0 || r1 > n || nr < 0) fail(EK_EINVAL, "Laplacian rows [%lld, %lld) outside [0, %lld)", (long long)r0,
+                                         (long long)r1, (long long)n);
+    // incidences (net, pin position) of the owned rows, nets ascending
+    std::vector<int64_t> ip(size_t(nr) + 1, 0);
     for (int64_t e = 0; e < h.nets; ++e) {
-        const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
-        if (k < 2) continue;
-        for (int64_t j = 0; j < k; ++j) cnt[size_t(h.pins[size_t(p0 + j)]) + 1] += k - 1;
-    }
-    for (int64_t i = 0; i < n; ++i) cnt[size_t(i) + 1] += cnt[size_t(i)];
-    std::vector<int32_t> tc(size_t(cnt[size_t(n)]));
-    std::vector<double> tv(size_t(cnt[size_t(n)]));
-    {
-        std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
-        for (int64_t e = 0; e < h.nets; ++e) {
-            const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
-            if (k < 2) continue;
-            const double wgt = 2.0 / double(k);
-            for (int64_t j = 0; j + 1 < k; ++j)
-                for (int64_t q = j + 1; q < k; ++q) {
-                    const int32_t a = h.pins[size_t(p0 + j)], b = h.pins[size_t(p0 + q)];
-                    tc[size_t(cur[size_t(a)])] = b;
-                    tv[size_t(cur[size_t(a)]++)] = -wgt;
-                    tc[size_t(cur[size_t(b)])] = a;
-                    tv[size_t(cur[size_t(b)]++)] = -wgt;
-                }
+        const int64_t p0 = h.net_ptr[size_t(e)], p1 = h.net_ptr[size_t(e) + 1];
+        if (p1 - p0 < 2) continue;
+        for (int64_t p = p0; p < p1; ++p) {
+            const int64_t v = h.pins[size_t(p)];
+            if (v >= r0 && v < r1) ++ip[size_t(v - r0) + 1];
         }
     }
-    // per row: stable sort by column, sum duplicates in net order, diagonal
-    std::vector<int32_t> rlen(size_t(n), 0);
-    std::vector<std::vector<std::pair<int32_t, double>>> rows(static_cast<size_t>(n));
-    parallel_for(n, [&](int64_t lo, int64_t hi) {
-        std::vector<int64_t> idx;
-        for (int64_t r = lo; r < hi; ++r) {
-            const int64_t b = cnt[size_t(r)], e = cnt[size_t(r) + 1];
-            idx.resize(size_t(e - b));
-            std::iota(idx.begin(), idx.end(), b);
-            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return tc[size_t(x)] < tc[size_t(y)]; });
-            auto& row = rows[size_t(r)];
-            row.clear();
-            for (int64_t t : idx) {
-                if (!row.empty() && row.back().first == tc[size_t(t)]) row.back().second += tv[size_t(t)];
-                else row.push_back({tc[size_t(t)], tv[size_t(t)]});
+    for (int64_t i = 0; i < nr; ++i) ip[size_t(i) + 1] += ip[size_t(i)];
+    std::vector<int64_t> inc(size_t(ip[size_t(nr)]));  // pin position p; its net from net_of
+    std::vector<int32_t> inc_net(inc.size());
+    {
+        std::vector<int64_t> cur(ip.begin(), ip.end() - 1);
+        for (int64_t e = 0; e < h.nets; ++e) {
+            const int64_t p0 = h.net_ptr[size_t(e)], p1 = h.net_ptr[size_t(e) + 1];
+            if (p1 - p0 < 2) continue;
+            for (int64_t p = p0; p < p1; ++p) {
+                const int64_t v = h.pins[size_t(p)];
+                if (v >= r0 && v < r1) {
+                    const int64_t q = cur[size_t(v - r0)]++;
+                    inc[size_t(q)] = p;
+                    inc_net[size_t(q)] = int32_t(e);
+                }
             }
+        }
+    }
+    const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, nr / 4096)));
+    std::vector<std::vector<int32_t>> tcol{size_t(T)};
+    std::vector<std::vector<double>> tval{size_t(T)};
+    std::vector<int32_t> rlen(size_t(nr), 0);
+    auto work = [&](int t) {
+        const int64_t lo = nr * t / T, hi = nr * (t + 1) / T;
+        auto& oc = tcol[size_t(t)];
+        auto& ov = tval[size_t(t)];
+        oc.reserve(size_t(ip[size_t(hi)] - ip[size_t(lo)]) * 4 + 16);
+        ov.reserve(oc.capacity());
+        std::vector<std::pair<int32_t, double>> row;
+        for (int64_t i = lo; i < hi; ++i) {
+            const int32_t r = int32_t(r0 + i);
+            row.clear();
+            for (int64_t q = ip[size_t(i)]; q < ip[size_t(i) + 1]; ++q) {
+                const int64_t e = inc_net[size_t(q)], p0 = h.net_ptr[size_t(e)], p1 = h.net_ptr[size_t(e) + 1];
+                const double w = -(2.0 / double(p1 - p0));
+                for (int64_t p = p0; p < p1; ++p)
+                    if (p != inc[size_t(q)]) row.push_back({h.pins[size_t(p)], w});
+            }
+            // stable by column: insertion sort (rows average ~6 entries)
+            if (row.size() <= 48) {
+                for (size_t a = 1; a < row.size(); ++a) {
+                    const auto x = row[a];
+                    size_t b = a;
+                    for (; b > 0 && row[b - 1].first > x.first; --b) row[b] = row[b - 1];
+                    row[b] = x;
+                }
+            } else {
+                std::stable_sort(row.begin(), row.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+            }
+            size_t m = 0;  // merge duplicates in order
+            for (size_t a = 0; a < row.size(); ++a) {
+                if (m > 0 && row[m - 1].first == row[a].first) row[m - 1].second += row[a].second;
+                else row[m++] = row[a];
+            }
+            row.resize(m);
             double s = 0.0;
             bool has_diag = false;
             for (auto& [c, v] : row) {
                 s += v;
                 has_diag |= (c == r);
             }
-            if (has_diag) {
-                for (auto& [c, v] : row)
-                    if (c == r) v = -s;
-            } else {
-                auto it = std::lower_bound(row.begin(), row.end(), std::make_pair(int32_t(r), -1e300));
-                row.insert(it, {int32_t(r), -s});
+            const size_t base = oc.size();
+            bool placed = has_diag;
+            for (auto& [c, v] : row) {
+                if (!placed && c > r) {
+                    oc.push_back(r);
+                    ov.push_back(-s);
+                    placed = true;
+                }
+                oc.push_back(c);
+                ov.push_back(c == r ? -s : v);
             }
-            rlen[size_t(r)] = int32_t(row.size());
+            if (!placed) {
+                oc.push_back(r);
+                ov.push_back(-s);
+            }
+            rlen[size_t(i)] = int32_t(oc.size() - base);
         }
-    });
-    L.nrows = n;
+    };
+    run_threads(T, work);
+    L.nrows = nr;
     L.value_bytes = 8;
-    L.rowptr.assign(size_t(n) + 1, 0);
-    for (int64_t r = 0; r < n; ++r) {
-        if (int64_t(L.rowptr[size_t(r)]) + rlen[size_t(r)] > INT32_MAX) fail(EK_EINVAL, "Laplacian nnz exceeds int32");
-        L.rowptr[size_t(r) + 1] = L.rowptr[size_t(r)] + rlen[size_t(r)];
+    L.rowptr.assign(size_t(nr) + 1, 0);
+    for (int64_t i = 0; i < nr; ++i) {
+        if (int64_t(L.rowptr[size_t(i)]) + rlen[size_t(i)] > INT32_MAX) fail(EK_EINVAL, "Laplacian nnz exceeds int32");
+        L.rowptr[size_t(i) + 1] = L.rowptr[size_t(i)] + rlen[size_t(i)];
     }
-    L.col.resize(size_t(L.rowptr[size_t(n)]));
-    L.val64.resize(size_t(L.rowptr[size_t(n)]));
-    parallel_for(n, [&](int64_t lo, int64_t hi) {
-        for (int64_t r = lo; r < hi; ++r) {
-            int64_t p = L.rowptr[size_t(r)];
-            for (auto& [c, v] : rows[size_t(r)]) {
-                L.col[size_t(p)] = c;
-                L.val64[size_t(p++)] = v;
-            }
-            std::vector<std::pair<int32_t, double>>().swap(rows[size_t(r)]);
-        }
+    L.col.resize(size_t(L.rowptr[size_t(nr)]));
+    L.val64.resize(L.col.size());
+    run_threads(T, [&](int t) {
+        const int64_t at = L.rowptr[size_t(nr * t / T)];
+        std::copy(tcol[size_t(t)].begin(), tcol[size_t(t)].end(), L.col.begin() + at);
+        std::copy(tval[size_t(t)].begin(), tval[size_t(t)].end(), L.val64.begin() + at);
     });
 }
+
+void build_laplacian(const ek_hgr& h, ek_csr& L) { build_laplacian_rows(h, 0, h.nodes, L); }
 
 // ---------------------------------------------------------------------------
 // cKL.cpp:107-131 + connections() order (cKL.cpp:229-248).
@@ -327,6 +367,16 @@ int ek_laplacian_build(const ek_hgr* h, ek_csr** out) {
     if (!h || !out) ek::fail(EK_EINVAL, "ek_laplacian_build: null argument");
     auto c = std::make_unique<ek_csr>();
     ek::build_laplacian(*h, *c);
+    *out = c.release();
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_laplacian_build_rows(const ek_hgr* h, int64_t row0, int64_t nrows, ek_csr** out) {
+    EK_TRY
+    if (!h || !out || row0 < 0 || nrows < 0) ek::fail(EK_EINVAL, "ek_laplacian_build_rows: bad argument");
+    auto c = std::make_unique<ek_csr>();
+    ek::build_laplacian_rows(*h, row0, row0 + nrows, *c);
     *out = c.release();
     return EK_OK;
     EK_CATCH

@@ -227,6 +227,60 @@ int ek_hgr_generate(double multiplier, uint64_t seed, ek_hgr** out) {
     EK_CATCH
 }
 
+// Largest connected component (union-find over each net's pins), nets kept in
+// file order with their pins renumbered by ascending original id.
+int ek_hgr_largest_component(const ek_hgr* h, ek_hgr** out, int32_t* node_map) {
+    EK_TRY
+    if (!h || !out) ek::fail(EK_EINVAL, "ek_hgr_largest_component: null argument");
+    const int64_t n = h->nodes;
+    std::vector<int32_t> parent(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) parent[size_t(i)] = int32_t(i);
+    auto find = [&](int32_t x) {
+        while (parent[size_t(x)] != x) {
+            parent[size_t(x)] = parent[size_t(parent[size_t(x)])];
+            x = parent[size_t(x)];
+        }
+        return x;
+    };
+    for (int64_t e = 0; e < h->nets; ++e) {
+        const int64_t p0 = h->net_ptr[size_t(e)], p1 = h->net_ptr[size_t(e) + 1];
+        if (p1 - p0 < 2) continue;
+        int32_t a = find(h->pins[size_t(p0)]);
+        for (int64_t p = p0 + 1; p < p1; ++p) {
+            const int32_t b = find(h->pins[size_t(p)]);
+            if (a == b) continue;
+            if (a < b) parent[size_t(b)] = a;  // the root is the component's smallest id
+            else {
+                parent[size_t(a)] = b;
+                a = b;
+            }
+        }
+    }
+    std::vector<int64_t> size(static_cast<size_t>(n), 0);
+    int32_t best = -1;
+    for (int64_t i = 0; i < n; ++i) ++size[size_t(find(int32_t(i)))];
+    for (int64_t i = 0; i < n; ++i)  // ties: the root (= smallest id) that comes first
+        if (parent[size_t(i)] == i && (best < 0 || size[size_t(i)] > size[size_t(best)])) best = int32_t(i);
+    std::vector<int32_t> nid(static_cast<size_t>(n), -1);
+    int32_t m = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (best >= 0 && find(int32_t(i)) == best) nid[size_t(i)] = m++;
+    auto c = std::make_unique<ek_hgr>();
+    c->nodes = m;
+    c->net_ptr.push_back(0);
+    for (int64_t e = 0; e < h->nets; ++e) {
+        const int64_t p0 = h->net_ptr[size_t(e)], p1 = h->net_ptr[size_t(e) + 1];
+        if (p1 == p0 || nid[size_t(h->pins[size_t(p0)])] < 0) continue;  // every pin of a kept net is kept
+        for (int64_t p = p0; p < p1; ++p) c->pins.push_back(nid[size_t(h->pins[size_t(p)])]);
+        c->net_ptr.push_back(int64_t(c->pins.size()));
+    }
+    c->nets = int64_t(c->net_ptr.size()) - 1;
+    if (node_map) std::copy(nid.begin(), nid.end(), node_map);
+    *out = c.release();
+    return EK_OK;
+    EK_CATCH
+}
+
 int ek_hgr_write(const ek_hgr* h, const char* path) {
     EK_TRY
     if (!h || !path) ek::fail(EK_EINVAL, "ek_hgr_write: null argument");

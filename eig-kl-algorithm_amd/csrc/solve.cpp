@@ -1,0 +1,228 @@
+// The whole hot path in-process, .hgr in -> results/ out (ek_solve_file):
+// the body the reference splits over two processes and a text file,
+//   cEIG <in>    : read, clique Laplacian, Spectra Lanczos, median split
+//                  (cEIG.cpp:138-237)
+//   cKL <in> -EIG: read, KL adjacency, split from the EIG file, KL loop,
+//                  results file (cKL.cpp:288-468)
+// with the Fiedler split handed over in memory (gKL2 <in> -EIG, gKL2.cu:989-1033,
+// whose "EIG" is replaced by the real Lanczos).  Host phases overlap the GPU:
+// the KL adjacency (hash-order emulation) is built on a host thread while the
+// GPU runs the Lanczos solve.  Multi-rank contexts shard the Lanczos rows
+// (each rank builds and uploads only its rows); the KL loop is rank 0's.
+#include <sys/stat.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <filesystem>
+#include <future>
+#include <random>
+#include <string>
+
+#include "ek_internal.hpp"
+
+namespace ek {
+
+namespace {
+using clk = std::chrono::steady_clock;
+double since(clk::time_point t) { return std::chrono::duration<double>(clk::now() - t).count(); }
+
+struct KLHost {
+    std::vector<int32_t> rowptr, col;
+    std::vector<float> w;
+};
+
+KLHost kl_graph_host(const ek_hgr* h) {
+    ek_csr G;
+    build_kl_graph(*h, G);
+    KLHost g;
+    g.rowptr.swap(G.rowptr);
+    g.col.swap(G.col);
+    g.w.swap(G.val32);
+    return g;
+}
+
+void chk(int rc) {
+    if (rc != EK_OK) throw Error{rc};  // ek_last_error() already holds the message
+}
+
+std::string join(const char* dir, const std::string& rel) {
+    if (!dir || !dir[0]) return rel;
+    return (std::filesystem::path(dir) / rel).string();
+}
+
+}  // namespace
+
+// Fiedler vector of this rank's Laplacian rows (cEIG.cpp:86-209): rows built
+// on the host, uploaded, Lanczos on the GPU; the full vector on every rank.
+void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek_solve_opts& o, double& lambda,
+                    std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
+                    const std::function<void()>& after_laplacian) {
+    const int64_t n = h.nodes;
+    int64_t row0 = 0, nrows = n, nloc = n;
+    chk(ek_shard_rows(n, nranks, rank, &row0, &nrows, &nloc));
+    auto t = clk::now();
+    {
+        ek_csr L;
+        build_laplacian_rows(h, row0, row0 + nrows, L);  // this rank's rows only
+        if (t_laplacian) *t_laplacian = since(t);
+        if (after_laplacian) after_laplacian();
+        t = clk::now();
+        chk(ek_spmv_setup(ctx, n, row0, nrows, L.rowptr.data(), L.col.data(), L.val64.data()));
+    }
+    v.assign(size_t(n), 0.0);
+    chk(ek_lanczos_fiedler(ctx, &o.lanczos, &lambda, v.data(), &st));
+    if (o.sign_ref && o.sign_ref[0]) {
+        std::vector<double> ref(static_cast<size_t>(n));
+        chk(ek_eig_read(o.sign_ref, n, nullptr, nullptr, nullptr, ref.data(), nullptr, nullptr, nullptr, nullptr));
+        chk(ek_align_sign(n, v.data(), ref.data()));
+    }
+    if (t_lanczos) *t_lanczos = since(t);
+}
+
+void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const ek_hgr& h, const std::string& base,
+           const ek_solve_opts& o, ek_swap* log_out, int64_t cap, ek_solve_result& r) {
+    const auto t0 = clk::now();
+    const int64_t n = h.nodes;
+    r.nets = h.nets;
+    r.nodes = n;
+    r.pins = int64_t(h.pins.size());
+    if (n < 2) fail(EK_EINVAL, "%s: %lld nodes, nothing to partition", base.c_str(), (long long)n);
+    // initial partition (shuffleSparceMatrix, cKL.cpp:151-197)
+    std::vector<int32_t> order0, order1;
+    std::future<KLHost> kg;
+    auto start_kl_graph = [&] {
+        if (rank == 0) kg = std::async(std::launch::async, kl_graph_host, &h);
+    };
+    if (o.eig == 1) {
+        std::vector<double> v;
+        // the KL adjacency starts once the Laplacian rows are built (both use
+        // every host thread), and runs while the GPU solves
+        fiedler_vector(get_ctx(), rank, nranks, h, o, r.lambda, v, r.lanczos, &r.t_laplacian, &r.t_lanczos,
+                       start_kl_graph);
+        if (rank != 0) {
+            r.t_total = since(t0);
+            return;
+        }
+        const auto t = clk::now();
+        std::vector<uint8_t> bits(static_cast<size_t>(n));
+        chk(ek_median_split(n, v.data(), &r.median, bits.data()));
+        order0.reserve(size_t(n) / 2 + 1);
+        order1.reserve(size_t(n) / 2 + 1);
+        for (int64_t i = 0; i < n; ++i) (bits[size_t(i)] ? order1 : order0).push_back(int32_t(i));  // cKL.cpp:155-174
+        r.t_split = since(t);
+    } else {
+        if (rank != 0) {  // the KL loop does not shard: other ranks have nothing to do
+            r.t_total = since(t0);
+            return;
+        }
+        start_kl_graph();
+        const auto t = clk::now();
+        if (o.eig == 2) {  // cKL -EIG: pre_saved_EIG/<base>_out.txt (cKL.cpp:442, 155-174)
+            const std::string eig_file = join(o.out_dir, "pre_saved_EIG/" + base + "_out.txt");
+            order0.resize(size_t(n));
+            order1.resize(size_t(n));
+            int64_t n0 = 0, n1 = 0;
+            if (ek_eig_read(eig_file.c_str(), n, &r.lambda, &r.median, nullptr, nullptr, order0.data(), &n0,
+                            order1.data(), &n1) != EK_OK)
+                fail(EK_EIO, "Error: EIG file not found (%s)", eig_file.c_str());
+            order0.resize(size_t(n0));
+            order1.resize(size_t(n1));
+        } else {
+            order0.resize(size_t(n / 2));
+            order1.resize(size_t(n - n / 2));
+            chk(ek_random_split(n, o.seed, order0.data(), order1.data()));
+        }
+        r.t_split = since(t);
+    }
+    ek_ctx* ctx = get_ctx();
+    auto t = clk::now();
+    const KLHost g = kg.get();
+    r.t_kl_graph_wait = since(t);
+    t = clk::now();
+    chk(ek_kl_graph_setup(ctx, n, g.rowptr.data(), g.col.data(), g.w.data()));
+    chk(ek_kl_nets_setup(ctx, h.nets, h.net_ptr.data(), h.pins.data()));
+    chk(ek_kl_set_partition(ctx, order0.data(), int64_t(order0.size()), order1.data(), int64_t(order1.size())));
+    r.t_kl_setup = since(t);
+    t = clk::now();
+    const int64_t lcap = int64_t(std::min(order0.size(), order1.size()));
+    std::vector<ek_swap> log(size_t(std::max<int64_t>(lcap, 1)));
+    chk(ek_kl_run(ctx, o.limit, log.data(), lcap, &r.kl));
+    r.t_kl = since(t);
+    const int64_t iters = std::min<int64_t>(r.kl.iterations, lcap);
+    if (log_out && cap > 0) std::copy(log.begin(), log.begin() + std::min(iters, cap), log_out);
+    t = clk::now();
+    if (o.write_results) {  // results/<base>_KL_CutSize[_EIG]_output.txt (cKL.cpp:438-444, 315, 380)
+        ::mkdir(join(o.out_dir, "results").c_str(), 0755);
+        const std::string path =
+            join(o.out_dir, "results/" + base + (o.eig ? "_KL_CutSize_EIG_output.txt" : "_KL_CutSize_output.txt"));
+        FILE* f = std::fopen(path.c_str(), "w");
+        if (!f) fail(EK_EIO, "Error: Cannot open output file %s (%s)", path.c_str(), std::strerror(errno));
+        std::vector<char> buf(size_t(1) << 20);
+        std::setvbuf(f, buf.data(), _IOFBF, buf.size());
+        std::fprintf(f, "0\t%g\t0\n", double(r.kl.initial_cut));  // ostream default format == %g
+        for (int64_t i = 0; i < iters; ++i)
+            std::fprintf(f, "%u\t%g\t%g\n", log[size_t(i)].iter, double(log[size_t(i)].cut), double(log[size_t(i)].gain));
+        const bool ok = std::fclose(f) == 0;
+        if (!ok) fail(EK_EIO, "short write to %s", path.c_str());
+    }
+    r.t_write = since(t);
+    r.t_total = since(t0);
+}
+
+}  // namespace ek
+
+extern "C" {
+
+void ek_solve_default_opts(ek_solve_opts* o) {
+    if (!o) return;
+    *o = ek_solve_opts{};
+    o->eig = 1;
+    o->seed = 0;
+    o->write_results = 1;
+    o->limit = -1;
+    o->out_dir = nullptr;
+    o->sign_ref = nullptr;
+    ek_lanczos_default_opts(&o->lanczos);
+}
+
+int ek_solve_file(ek_ctx* ctx, const char* path, const ek_solve_opts* opts, ek_swap* log_out, int64_t cap,
+                  ek_solve_result* res) {
+    EK_TRY
+    if (!ctx || !path) ek::fail(EK_EINVAL, "ek_solve_file: null argument");
+    ek_solve_opts o;
+    ek_solve_default_opts(&o);
+    if (opts) o = *opts;
+    if (o.eig < 0 || o.eig > 2) ek::fail(EK_EINVAL, "ek_solve_file: eig must be 0, 1 or 2");
+    int rank = 0, nranks = 1;
+    ek::ctx_ranks(ctx, &rank, &nranks);
+    ek_solve_result r{};
+    const auto t0 = std::chrono::steady_clock::now();
+    ek_hgr* h = nullptr;
+    if (const int rc = ek_hgr_read(path, &h); rc != EK_OK) throw ek::Error{rc};
+    std::unique_ptr<ek_hgr, void (*)(ek_hgr*)> hg(h, ek_hgr_free);
+    r.t_read = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    ek::solve([ctx] { return ctx; }, rank, nranks, *h, std::filesystem::path(path).filename().string(), o, log_out,
+              cap, r);
+    r.t_total += r.t_read;
+    if (res) *res = r;
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_random_split(int64_t n, uint32_t seed, int32_t* order0, int32_t* order1) {
+    EK_TRY
+    if (n < 0 || n > INT32_MAX || (n && (!order1 || (n >= 2 && !order0)))) ek::fail(EK_EINVAL, "ek_random_split: bad argument");
+    std::vector<uint32_t> nodes(static_cast<size_t>(n));  // cKL.cpp:176-181
+    for (int64_t i = 0; i < n; ++i) nodes[size_t(i)] = uint32_t(i);
+    std::mt19937 gen(seed);
+    std::shuffle(nodes.begin(), nodes.end(), gen);
+    const size_t mid = size_t(n / 2);  // cKL.cpp:183-191
+    for (size_t i = 0; i < mid; ++i) order0[i] = int32_t(nodes[i]);
+    for (size_t i = mid; i < size_t(n); ++i) order1[i - mid] = int32_t(nodes[i]);
+    return EK_OK;
+    EK_CATCH
+}
+
+}  // extern "C"

@@ -55,6 +55,13 @@ int ek_hgr_generate(double multiplier, uint64_t seed, ek_hgr** out);
 /* Build from 0-based pins: net e owns pins[net_ptr[e] .. net_ptr[e+1]). */
 int ek_hgr_from_pins(int64_t nets, int64_t nodes, const int64_t* net_ptr, const int32_t* pins,
                      ek_hgr** out);
+/* Largest connected component of the pin graph (nets with >= 2 pins join
+ * their pins; the largest component, ties to the one holding the smallest
+ * node id), as a new hypergraph: its nets in file order, nodes renumbered in
+ * ascending original id.  node_map (nodes of h, may be NULL) gets the new id
+ * or -1.  No reference counterpart: the connected ibm18-scale workload the
+ * disconnected synthetic lacks (SURVEY §0 finding 8). */
+int ek_hgr_largest_component(const ek_hgr* h, ek_hgr** out, int32_t* node_map);
 /* Write in the reference .hgr text format (circuit_generator.py:61-68). */
 int ek_hgr_write(const ek_hgr* h, const char* path);
 int ek_hgr_dims(const ek_hgr* h, int64_t* nets, int64_t* nodes, int64_t* pins);
@@ -70,6 +77,9 @@ typedef struct ek_csr ek_csr;
  * with ascending columns, diagonal included.  Replaces initializeMatrix,
  * cEIG.cpp:86-133. */
 int ek_laplacian_build(const ek_hgr* h, ek_csr** out);
+/* Rows [row0, row0+nrows) only (global column ids): one rank's shard of the
+ * sharded Lanczos, as ek_shard_rows assigns it. */
+int ek_laplacian_build_rows(const ek_hgr* h, int64_t row0, int64_t nrows, ek_csr** out);
 /* fp32 KL adjacency, w = 1/(|e|-1) accumulated in net order; each row holds
  * its forward (upper-triangle) entries in the iteration order of cKL's
  * std::unordered_map<uint32_t,float> (libstdc++ _Hashtable, emulated), then
@@ -97,12 +107,27 @@ int ek_init(int device, ek_ctx** out);
 void ek_destroy(ek_ctx* ctx);
 /* The context's hipStream_t (every kernel of this context runs on it). */
 int ek_get_stream(ek_ctx* ctx, void** stream_out);
+/* Wait for everything queued on the context's stream. */
+int ek_synchronize(ek_ctx* ctx);
 int ek_device_count(int* count);
 
 /* RCCL over xGMI: one process per GPU.  Rank 0 calls ek_comm_unique_id and
  * ships the 128 bytes to the other ranks (e.g. torch.distributed broadcast). */
 int ek_comm_unique_id(void* id128);
+/* Resets the context's row ownership: call ek_spmv_setup afterwards. */
 int ek_comm_init(ek_ctx* ctx, int nranks, int rank, const void* id128);
+/* Host-staged exchange instead of RCCL (no reference counterpart; the
+ * reference has no multi-GPU path).  Every collective of the sharded Lanczos
+ * drains the context stream, copies its operand to pinned host memory, calls
+ * the caller's collective and copies the result back.  Lets several ranks
+ * share one GPU (RCCL refuses that) and lets any host transport (e.g.
+ * torch.distributed gloo) drive the exchange: the multi-rank tests and
+ * debugging.  RCCL (ek_comm_init) is the production path.  Callbacks return
+ * 0 on success; recv holds nranks*count doubles, rank-major. */
+typedef int (*ek_allgather_fn)(void* user, const double* send, int64_t count, double* recv);
+typedef int (*ek_allreduce_fn)(void* user, double* buf, int64_t count); /* in-place sum */
+int ek_comm_init_host(ek_ctx* ctx, int nranks, int rank, ek_allgather_fn allgather, ek_allreduce_fn allreduce,
+                      void* user);
 
 /* ------------------------------------------------------------------ */
 /* SpMV seam: Spectra SparseSymMatProd<double>::perform_op, cEIG.cpp:194  */
@@ -215,6 +240,12 @@ int ek_kl_nets_setup(ek_ctx* ctx, int64_t nets, const int64_t* net_ptr, const in
 /* Initial remain[] lists (shuffleSparceMatrix, cKL.cpp:151-197): positions
  * are list order; the sides are split[0] = order0, split[1] = order1. */
 int ek_kl_set_partition(ek_ctx* ctx, const int32_t* order0, int64_t n0, const int32_t* order1, int64_t n1);
+/* The random branch of shuffleSparceMatrix (cKL.cpp:176-192), host only:
+ * nodes 0..n-1 shuffled by std::shuffle with std::mt19937(seed) (the
+ * reference seeds it from std::random_device; the seed makes it
+ * reproducible), the first n/2 to remain[0] (order0, n/2 entries), the rest
+ * to remain[1] (order1, n - n/2 entries). */
+int ek_random_split(int64_t n, uint32_t seed, int32_t* order0, int32_t* order1);
 /* The -EIG branch of shuffleSparceMatrix (cKL.cpp:155-174): node i goes to
  * split[bits[i]] in ascending node order (the EIG file's line order). */
 int ek_kl_set_partition_bits(ek_ctx* ctx, int64_t n, const uint8_t* bits);
@@ -224,6 +255,38 @@ int ek_kl_set_partition_bits(ek_ctx* ctx, int64_t n, const uint8_t* bits);
 int ek_kl_run(ek_ctx* ctx, int32_t limit, ek_swap* log_out, int64_t cap, ek_kl_result* res);
 /* Side of every node: which = 0 initial, 1 best prefix, 2 final. */
 int ek_kl_sides(ek_ctx* ctx, int32_t which, uint8_t* sides_out);
+
+/* ------------------------------------------------------------------ */
+/* Whole path, .hgr in -> results/ out, in-process: the body of          */
+/* gKL2 <in> -EIG (GPU Fiedler split) and cKL/gKL <in> (random split),   */
+/* main() + KL() of cKL.cpp:288-468 with cEIG.cpp:138-237 in front.      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int32_t eig;          /* 1: Fiedler split on the GPU (gKL2 -EIG); 0: random split (seed) */
+    uint32_t seed;        /* random split: std::mt19937 seed (ek_random_split) */
+    int32_t write_results;/* 1: results/<base>_KL_CutSize[_EIG]_output.txt under out_dir */
+    int32_t limit;        /* KL termination limit; < 0: floor(log2 n)+5 (cKL.cpp:303) */
+    const char* out_dir;  /* NULL: the CWD (the reference's convention) */
+    const char* sign_ref; /* optional pre_saved_EIG file whose sign the Fiedler vector takes */
+    ek_lanczos_opts lanczos;
+} ek_solve_opts;
+
+typedef struct {
+    int64_t nets, nodes, pins;
+    double lambda, median;
+    ek_lanczos_stats lanczos; /* eig = 1 */
+    ek_kl_result kl;          /* rank 0 only */
+    /* wall seconds of the phases on this rank (host clock) */
+    double t_read, t_laplacian, t_lanczos, t_split, t_kl_graph_wait, t_kl_setup, t_kl, t_write, t_total;
+} ek_solve_result;
+
+void ek_solve_default_opts(ek_solve_opts* o);
+/* Multi-rank contexts (ek_comm_init*): every rank calls it with the same
+ * file; the Lanczos rows are sharded (each rank builds and uploads its own
+ * rows), the KL loop and the results file are rank 0's.  log_out (may be
+ * NULL, cap entries) receives rank 0's swap log. */
+int ek_solve_file(ek_ctx* ctx, const char* path, const ek_solve_opts* o, ek_swap* log_out, int64_t cap,
+                  ek_solve_result* res);
 
 /* ------------------------------------------------------------------ */
 /* Drop-in CLIs: argv exactly as cEIG.cpp:138-237 / cKL.cpp:424-468 /    */

@@ -76,6 +76,13 @@ typedef struct {
 int eko_lanczos(const eko_graph* g, const eko_lanczos_opts* o, double* lambda, double* v,
                 eko_lanczos_stats* st);
 
+/* cKL.cpp:176-192 (random init) with std::mt19937(seed) instead of random_device. */
+int eko_random_split(int64_t n, uint32_t seed, int32_t* order0, int32_t* order1);
+/* OpenMP threads of the restatement (the KL gain sweep/update/selection and
+ * the Lanczos SpMV/projections run on them; results do not depend on it). */
+void eko_set_threads(int t);
+int eko_get_threads(void);
+
 /* libstdc++ bucket-count growth observed on THIS host's std::unordered_map:
  * fills out[i] = bucket_count() after inserting i+1 distinct keys. */
 int eko_bucket_growth(int64_t nkeys, int64_t* out);

@@ -67,7 +67,27 @@ Lap build_laplacian(const eko_graph& g) {
     return L;
 }
 
+// Sums over rows in fixed 4096-row blocks, the block partials added in block
+// order: the same bits for any thread count.
+constexpr int64_t SUM_BLK = 4096;
+template <class F>
+double block_sum(size_t n, F&& term) {
+    const int64_t nb = (int64_t(n) + SUM_BLK - 1) / SUM_BLK;
+    std::vector<double> part(size_t(std::max<int64_t>(nb, 1)), 0.0);
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nb; ++b) {
+        double s = 0.0;
+        const size_t r1 = std::min<size_t>(n, size_t(b + 1) * SUM_BLK);
+        for (size_t r = size_t(b) * SUM_BLK; r < r1; ++r) s += term(r);
+        part[size_t(b)] = s;
+    }
+    double s = 0.0;
+    for (double p : part) s += p;
+    return s;
+}
+
 void spmv(const Lap& L, const double* x, double* y, size_t n) {
+#pragma omp parallel for schedule(static)
     for (size_t r = 0; r < n; ++r) {
         double s = 0.0;
         for (int32_t p = L.rowptr[r]; p < L.rowptr[r + 1]; ++p) s += L.val[p] * x[L.col[p]];
@@ -185,25 +205,22 @@ int eko_lanczos(const eko_graph* g, const eko_lanczos_opts* o, double* lambda, d
         for (double& x : f) x -= s / double(n);
     }
     auto norm = [&](const std::vector<double>& x) {
-        double s = 0.0;
-        for (double t : x) s += t * t;
-        return std::sqrt(s);
+        return std::sqrt(block_sum(n, [&](size_t r) { return x[r] * x[r]; }));
     };
     // one classical Gram-Schmidt pass of x against V[:, 0..c) (+ u0)
     auto cgs = [&](std::vector<double>& x, int c, std::vector<double>& coef) {
         for (int j = 0; j < c; ++j) {
-            double s = 0.0;
             const double* vj = &V[size_t(j) * n];
-            for (size_t r = 0; r < n; ++r) s += vj[r] * x[r];
-            coef[j] = s;
+            coef[j] = block_sum(n, [&](size_t r) { return vj[r] * x[r]; });
         }
-        double su = 0.0;
-        if (deflate) for (size_t r = 0; r < n; ++r) su += u0 * x[r];
-        for (int j = 0; j < c; ++j) {
-            const double* vj = &V[size_t(j) * n];
-            for (size_t r = 0; r < n; ++r) x[r] -= vj[r] * coef[j];
+        const double su = deflate ? block_sum(n, [&](size_t r) { return u0 * x[r]; }) : 0.0;
+#pragma omp parallel for schedule(static)
+        for (size_t r = 0; r < n; ++r) {
+            double t = x[r];
+            for (int j = 0; j < c; ++j) t -= V[size_t(j) * n + r] * coef[j];
+            if (deflate) t -= u0 * su;
+            x[r] = t;
         }
-        if (deflate) for (size_t r = 0; r < n; ++r) x[r] -= u0 * su;
     };
 
     double beta = norm(f);
@@ -213,6 +230,7 @@ int eko_lanczos(const eko_graph* g, const eko_lanczos_opts* o, double* lambda, d
     for (;; ++restarts) {
         for (int j = k; j < m; ++j) {
             double* vj = &V[size_t(j) * n];
+#pragma omp parallel for schedule(static)
             for (size_t r = 0; r < n; ++r) vj[r] = f[r] / beta;
             spmv(L, vj, w.data(), n);
             ++matvecs;
@@ -243,12 +261,12 @@ int eko_lanczos(const eko_graph* g, const eko_lanczos_opts* o, double* lambda, d
         const int knew = nev_adjusted(nev, m, nconv, est);
         // thick restart: V[:, :knew] <- V Y[:, :knew]; T <- diag(theta); f unchanged
         std::vector<double> Vn(n * size_t(knew), 0.0);
-        for (int c = 0; c < knew; ++c)
-            for (int i = 0; i < m; ++i) {
-                const double y = Z[size_t(i) * m + c];
-                const double* vi = &V[size_t(i) * n];
-                double* out = &Vn[size_t(c) * n];
-                for (size_t r = 0; r < n; ++r) out[r] += vi[r] * y;
+#pragma omp parallel for schedule(static)
+        for (size_t r = 0; r < n; ++r)
+            for (int c = 0; c < knew; ++c) {
+                double t = 0.0;
+                for (int i = 0; i < m; ++i) t += V[size_t(i) * n + r] * Z[size_t(i) * m + c];
+                Vn[size_t(c) * n + r] = t;
             }
         std::copy(Vn.begin(), Vn.end(), V.begin());
         std::fill(T.begin(), T.end(), 0.0);

@@ -32,6 +32,9 @@
 #include <cstring>
 #include <fstream>
 #include <limits>
+#include <random>
+
+#include <omp.h>
 #include <sstream>
 #include <string>
 
@@ -187,13 +190,12 @@ int eko_kl(const eko_graph* cg, const int32_t* order0, int64_t n0, const int32_t
     // left endpoint.  The reference's OpenMP fp32 reduction has no fixed order;
     // here: fp32 per-node external sums (row order), added in fp64 by ascending
     // node id, rounded once to fp32 (DESIGN.md "initial cut").
-    std::vector<float> gains(n, 0.0f);
+    std::vector<float> gains(n, 0.0f), ext(n, 0.0f);
+#pragma omp parallel for schedule(static)  // initial gains (cKL.cpp:317-321, omp parallel for there too)
+    for (int64_t u = 0; u < int64_t(n); ++u) gains[u] = connections(*g, side, uint32_t(u), &ext[u]);
     double cut64 = 0.0;
-    for (uint32_t u = 0; u < n; ++u) {
-        float ext = 0.0f;
-        gains[u] = connections(*g, side, u, &ext);  // initial gains (cKL.cpp:318-321)
-        if (side[u] == 0) cut64 += double(ext);
-    }
+    for (uint32_t u = 0; u < n; ++u)
+        if (side[u] == 0) cut64 += double(ext[u]);
     float cutSize = float(cut64);
     const float initialCutSize = cutSize;
     float minCutSize = cutSize;
@@ -203,16 +205,44 @@ int eko_kl(const eko_graph* cg, const int32_t* order0, int64_t n0, const int32_t
     int64_t alive0 = n0, alive1 = n1;
     std::vector<uint32_t> affected;
     while (alive0 > 0 && alive1 > 0) {  // cKL.cpp:334
+        // cKL.cpp:341-355 (locked == erased): first position with the max
+        // (strict >) gain over remain[0], the min (strict <) over remain[1].
+        // Sequential in the reference; split over threads here, each keeping
+        // its first best, merged by (gain, then lower position): the same pick.
         float maxGain = -std::numeric_limits<float>::max();
         float minGain = std::numeric_limits<float>::max();
         int64_t maxIdx = -1, minIdx = -1;
-        for (int64_t i = 0; i < n0; ++i) {  // cKL.cpp:341-347 (locked == erased)
-            const uint32_t u = uint32_t(order0[i]);
-            if (!locked[u] && gains[u] > maxGain) { maxGain = gains[u]; maxIdx = i; }
-        }
-        for (int64_t i = 0; i < n1; ++i) {  // cKL.cpp:349-355
-            const uint32_t u = uint32_t(order1[i]);
-            if (!locked[u] && gains[u] < minGain) { minGain = gains[u]; minIdx = i; }
+        const int nth = omp_get_max_threads();
+        if (nth <= 1 || n0 + n1 < 8192) {
+            for (int64_t i = 0; i < n0; ++i) {
+                const uint32_t u = uint32_t(order0[i]);
+                if (!locked[u] && gains[u] > maxGain) { maxGain = gains[u]; maxIdx = i; }
+            }
+            for (int64_t i = 0; i < n1; ++i) {
+                const uint32_t u = uint32_t(order1[i]);
+                if (!locked[u] && gains[u] < minGain) { minGain = gains[u]; minIdx = i; }
+            }
+        } else {
+#pragma omp parallel
+            {
+                float mx = -std::numeric_limits<float>::max(), mn = std::numeric_limits<float>::max();
+                int64_t ix = -1, in = -1;
+#pragma omp for schedule(static) nowait
+                for (int64_t i = 0; i < n0; ++i) {
+                    const uint32_t u = uint32_t(order0[i]);
+                    if (!locked[u] && gains[u] > mx) { mx = gains[u]; ix = i; }
+                }
+#pragma omp for schedule(static) nowait
+                for (int64_t i = 0; i < n1; ++i) {
+                    const uint32_t u = uint32_t(order1[i]);
+                    if (!locked[u] && gains[u] < mn) { mn = gains[u]; in = i; }
+                }
+#pragma omp critical
+                {
+                    if (ix >= 0 && (maxIdx < 0 || mx > maxGain || (mx == maxGain && ix < maxIdx))) { maxGain = mx; maxIdx = ix; }
+                    if (in >= 0 && (minIdx < 0 || mn < minGain || (mn == minGain && in < minIdx))) { minGain = mn; minIdx = in; }
+                }
+            }
         }
         if (maxIdx < 0 || minIdx < 0) break;  // cKL.cpp:387-388
         const uint32_t node1 = uint32_t(order0[maxIdx]), node2 = uint32_t(order1[minIdx]);
@@ -230,7 +260,8 @@ int eko_kl(const eko_graph* cg, const int32_t* order0, int64_t n0, const int32_t
         for (int32_t p = g->rowptr[node2]; p < g->rowptr[node2 + 1]; ++p) affected.push_back(uint32_t(g->col[p]));
         std::sort(affected.begin(), affected.end());
         affected.erase(std::unique(affected.begin(), affected.end()), affected.end());
-        for (uint32_t u : affected) gains[u] = connections(*g, side, u);
+#pragma omp parallel for schedule(dynamic, 8) if (affected.size() > 64)  // cKL.cpp:267
+        for (size_t a = 0; a < affected.size(); ++a) gains[affected[a]] = connections(*g, side, affected[a]);
         iteration++;
         if (log && int64_t(iteration) <= cap)
             log[iteration - 1] = eko_swap{iteration, node1, node2, maxGain, minGain, gain, cutSize, 0};
@@ -256,6 +287,23 @@ int eko_kl(const eko_graph* cg, const int32_t* order0, int64_t n0, const int32_t
     }
     return 0;
 }
+
+// shuffleSparceMatrix's random branch (cKL.cpp:176-192) with the
+// std::random_device seed replaced by `seed`.
+int eko_random_split(int64_t n, uint32_t seed, int32_t* order0, int32_t* order1) {
+    std::vector<uint32_t> nodes(n);
+    for (int64_t i = 0; i < n; ++i) nodes[i] = uint32_t(i);
+    std::mt19937 gen(seed);
+    std::shuffle(nodes.begin(), nodes.end(), gen);
+    const int64_t mid = n / 2;
+    for (int64_t i = 0; i < mid; ++i) order0[i] = int32_t(nodes[i]);
+    for (int64_t i = mid; i < n; ++i) order1[i - mid] = int32_t(nodes[i]);
+    return 0;
+}
+
+// Thread count of the oracle's OpenMP regions (the CPU baseline's core count).
+void eko_set_threads(int t) { omp_set_num_threads(t > 0 ? t : 1); }
+int eko_get_threads(void) { return omp_get_max_threads(); }
 
 int eko_bucket_growth(int64_t nkeys, int64_t* out) {
     std::unordered_map<uint32_t, float> m;

@@ -14,8 +14,21 @@ Runs in THIS container (the only place /root/reference exists):
    to ``tests/golden/ref_results/``.  These rows (iteration, fp32 cut, fp32
    gain at 6 significant digits) pin the oracle restatement and the HIP path.
 3. Records wall time / thread count per run in ``tests/golden/ref_runs.json``.
+4. ``--seeded``: runs ``oracle/_ref/cKL_seeded`` (the same reference source,
+   its std::random_device seed taken from $EK_REF_SEED: oracle/ref_seed.h) as
+   ``cKL <c>.hgr`` (random init, cKL.cpp:176-192) for the (circuit, seed)
+   pairs in SEEDED and keeps ``results/<c>.hgr_KL_CutSize_output.txt`` as
+   ``tests/golden/ref_results_seed/<c>.seed<S>.txt``.
+5. ``--lcc``: the largest connected component of the product generator's 1.0x
+   seed-1 synthetic (ek_hgr_largest_component; 184,306 nodes), its Fiedler
+   split from the oracle Lanczos (median split, sign: largest |v| positive),
+   and the REAL reference cKL run on it (``cKL syn1_lcc.hgr -EIG``, ~25 min on
+   4 cores): ``tests/golden/syn1_lcc/`` keeps the packed split bits, lambda /
+   median / the near-median nodes, and the gzipped reference results file.
 
 Usage: python oracle/gen_golden.py [circuit ...]   (default: all four)
+       python oracle/gen_golden.py --seeded
+       python oracle/gen_golden.py --lcc [EIG_FILE REF_RESULTS_FILE]
 """
 import json
 import os
@@ -33,7 +46,87 @@ CKL = os.path.join(HERE, "_ref", "cKL")
 CIRCUITS = ["fract", "ibm01", "industry2", "ibm10"]
 
 
+SEEDED = [("fract", 1), ("fract", 7), ("fract", 12345), ("ibm01", 1)]
+
+
+def seeded():
+    exe = os.path.join(HERE, "_ref", "cKL_seeded")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-f", os.path.join(HERE, "ref.mk")])
+    dst = os.path.join(GOLD, "ref_results_seed")
+    os.makedirs(dst, exist_ok=True)
+    runs_path = os.path.join(GOLD, "ref_runs.json")
+    runs = json.load(open(runs_path)) if os.path.exists(runs_path) else {}
+    for c, seed in SEEDED:
+        hgr = f"{c}.hgr"
+        with tempfile.TemporaryDirectory() as tmp:
+            shutil.copy(os.path.join(REF, "circuit", hgr), os.path.join(tmp, hgr))
+            t0 = time.time()
+            subprocess.run([exe, hgr], cwd=tmp, capture_output=True, text=True, check=True,
+                           env=dict(os.environ, EK_REF_SEED=str(seed)))
+            runs[f"{c}.seed{seed}"] = {"wall_s": round(time.time() - t0, 3), "threads": os.cpu_count(),
+                                       "binary": "oracle/_ref/cKL_seeded"}
+            shutil.copy(os.path.join(tmp, "results", f"{hgr}_KL_CutSize_output.txt"),
+                        os.path.join(dst, f"{c}.seed{seed}.txt"))
+        print(c, seed, runs[f"{c}.seed{seed}"], flush=True)
+    json.dump(runs, open(runs_path, "w"), indent=1, sort_keys=True)
+
+
+def lcc(eig_file=None, ref_results=None):
+    """syn1_lcc fixture.  eig_file / ref_results: an EIG file written for the
+    component and the reference results of a cKL run on it (the run takes
+    ~25 min on 4 cores), else both are made here (oracle Lanczos on all host
+    cores, then the reference)."""
+    import gzip
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    sys.path.insert(0, HERE)
+    from conftest import load_package
+    import oracle
+    ek = load_package()
+    dst = os.path.join(GOLD, "syn1_lcc")
+    os.makedirs(dst, exist_ok=True)
+    h, _ = ek.Hypergraph.generate(1.0, 1).largest_component()
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "syn1_lcc.hgr")
+        h.write(path)
+        meta = {"nodes": h.nodes, "nets": h.nets,
+                "made_by": "oracle/gen_golden.py --lcc: oracle Lanczos (sign: largest |v| positive), median split, "
+                           "real reference cKL syn1_lcc.hgr -EIG"}
+        if eig_file is None:
+            g = oracle.Graph.read(path)
+            oracle.set_threads(os.cpu_count())
+            lam, v, st = g.lanczos(deflate=True)
+            v = v * np.sign(v[np.argmax(np.abs(v))])
+            med, bits = ek.median_split(v)
+            meta.update(oracle_matvecs=st["matvecs"], oracle_residual=st["residual"])
+            os.makedirs(os.path.join(tmp, "pre_saved_EIG"))
+            eig_file = os.path.join(tmp, "pre_saved_EIG", "syn1_lcc.hgr_out.txt")
+            ek.eig_write(eig_file, lam, med, bits, v)
+        lam, med, bits, v, _, _ = ek.eig_read(eig_file, h.nodes)
+        near = np.flatnonzero(np.abs(v - med) <= 1e-8)
+        meta.update(lambda1=lam, median=med, near_median_nodes=near.tolist())
+        np.save(os.path.join(dst, "split_bits.npy"), np.packbits(bits))
+        if ref_results is None:
+            os.makedirs(os.path.join(tmp, "pre_saved_EIG"), exist_ok=True)
+            if os.path.abspath(eig_file) != os.path.join(tmp, "pre_saved_EIG", "syn1_lcc.hgr_out.txt"):
+                shutil.copy(eig_file, os.path.join(tmp, "pre_saved_EIG", "syn1_lcc.hgr_out.txt"))
+            t0 = time.time()
+            subprocess.run([CKL, "syn1_lcc.hgr", "-EIG"], cwd=tmp, capture_output=True, text=True, check=True)
+            meta["reference_wall_s"] = round(time.time() - t0, 1)
+            ref_results = os.path.join(tmp, "results", "syn1_lcc.hgr_KL_CutSize_EIG_output.txt")
+        if os.path.exists(ref_results):
+            with open(ref_results, "rb") as f, gzip.open(os.path.join(dst, "ref_results.txt.gz"), "wb", 9) as z:
+                z.write(f.read())
+        json.dump(meta, open(os.path.join(dst, "meta.json"), "w"), indent=1)
+        print("lcc", {k: meta[k] for k in ("nodes", "lambda1", "median")}, len(near), "near-median")
+
+
 def main(argv):
+    if len(argv) > 1 and argv[1] == "--seeded":
+        return seeded()
+    if len(argv) > 1 and argv[1] == "--lcc":
+        return lcc(*argv[2:4])
     names = argv[1:] or CIRCUITS
     if not os.path.exists(CKL):
         subprocess.check_call(["make", "-f", os.path.join(HERE, "ref.mk")])

@@ -64,6 +64,12 @@ def lib():
         L.eko_spmv.argtypes = [P, P, P]
         L.eko_lanczos.argtypes = [P, ctypes.POINTER(_LzOpts), P, P, ctypes.POINTER(_LzStats)]
         L.eko_bucket_growth.argtypes = [ctypes.c_int64, P]
+        L.eko_random_split.argtypes = [ctypes.c_int64, ctypes.c_uint32, P, P]
+        L.eko_set_threads.argtypes = [ctypes.c_int]
+        L.eko_get_threads.restype = ctypes.c_int
+        # one thread unless asked: the checker's results do not depend on it,
+        # and an oversubscribed host makes OpenMP barriers crawl
+        L.eko_set_threads(int(os.environ.get("EKO_THREADS", "1")))
         _lib = L
     return _lib
 
@@ -156,6 +162,19 @@ class Graph:
         rc = lib().eko_lanczos(self._h, ctypes.byref(o), ctypes.byref(lam), _p(v), ctypes.byref(st))
         return lam.value, v, {"restarts": st.restarts, "matvecs": st.matvecs,
                               "converged": bool(st.converged), "residual": st.residual, "rc": rc}
+
+
+def set_threads(t):
+    """OpenMP threads of the restatement (CPU baseline); results do not depend on it."""
+    lib().eko_set_threads(int(t))
+
+
+def random_split(n, seed):
+    """cKL.cpp:176-192 with std::mt19937(seed) in place of random_device: (remain[0], remain[1])."""
+    o0 = np.empty(n // 2, np.int32)
+    o1 = np.empty(n - n // 2, np.int32)
+    lib().eko_random_split(int(n), int(seed) & 0xFFFFFFFF, _p(o0), _p(o1))
+    return o0, o1
 
 
 def bucket_growth(nkeys):

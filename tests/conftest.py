@@ -2,6 +2,7 @@ import importlib.util
 import os
 import sys
 
+import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -68,11 +69,24 @@ def ref_results_path(name):
 def compare_results_text(mine, ref, cut_tol=0.05):
     """results/ rows 'iter\\tcut\\tgain' (cKL.cpp:315,380): iteration and gain
     columns must match as printed (%g of bit-identical fp32); the cut column
-    within cut_tol (the reference's initial cut is a nondeterministic OpenMP
-    fp32 reduction, cKL.cpp:203)."""
+    within max(cut_tol, 3e-5 |cut0|): the reference's initial cut is a
+    nondeterministic OpenMP fp32 reduction (cKL.cpp:203), whose error grows with
+    the cut (0.3 on ibm01's random-init cut of 12,658)."""
     a = [ln.split("\t") for ln in mine.strip().splitlines()]
     b = [ln.split("\t") for ln in ref.strip().splitlines()]
     assert len(a) == len(b), (len(a), len(b))
+    tol = max(cut_tol, 3e-5 * abs(float(b[0][1])))
     for x, y in zip(a, b):
         assert x[0] == y[0] and x[2] == y[2], (x, y)
-        assert abs(float(x[1]) - float(y[1])) <= cut_tol, (x, y)
+        assert abs(float(x[1]) - float(y[1])) <= tol, (x, y)
+
+
+def swap_fields_equal(a, b):
+    """Two swap logs (ek_swap / eko_swap rows) field by field, fp32 fields by bits."""
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("iter", "node_left", "node_right"):
+        bad = np.flatnonzero(a[f] != b[f])
+        assert bad.size == 0, (f, int(bad[0]) if bad.size else None)
+    for f in ("max_gain", "min_gain", "gain", "cut"):  # bit-exact fp32
+        bad = np.flatnonzero(a[f].view(np.uint32) != b[f].view(np.uint32))
+        assert bad.size == 0, (f, int(bad[0]) if bad.size else None)

@@ -222,3 +222,57 @@ def test_shard_rows_tile_the_matrix(ek, n, ranks):
         assert row0 == covered
         covered += nrows
     assert covered == n
+
+
+# ------------------------------------------- random split (cKL.cpp:176-192)
+@pytest.mark.parametrize("n,seed", [(149, 1), (149, 7), (12752, 1), (12637, 99), (2, 0), (3, 5)])
+def test_random_split_is_the_reference_shuffle(ek, oracle, n, seed):
+    """The product's split (ek_random_split) and the oracle's are both
+    std::mt19937(seed) + std::shuffle over iota, first n/2 left; the oracle's is
+    pinned to the seeded reference cKL (test_oracle_golden)."""
+    a0, a1 = ek.random_split(n, seed)
+    b0, b1 = oracle.random_split(n, seed)
+    assert np.array_equal(a0, b0) and np.array_equal(a1, b1)
+    assert len(a0) == n // 2 and sorted(np.concatenate([a0, a1]).tolist()) == list(range(n))
+
+
+# ------------------------------------------------ largest component
+def test_largest_component_matches_scipy(ek):
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    h = ek.Hypergraph.generate(0.1, 4)
+    net_ptr, pins = h.pins()
+    k = np.diff(net_ptr)
+    first = np.repeat(pins[net_ptr[:-1]], k)
+    ncomp, lab = connected_components(coo_matrix((np.ones(len(pins)), (first, pins)), shape=(h.nodes,) * 2),
+                                      directed=False)
+    assert ncomp > 1  # the synthetic is disconnected (SURVEY §0 finding 8)
+    big = np.argmax(np.bincount(lab))
+    keep = lab == big
+    c, m = h.largest_component()
+    assert c.nodes == keep.sum() and np.array_equal(m >= 0, keep)
+    assert np.array_equal(m[keep], np.arange(c.nodes))  # ascending original ids
+    cp, cpins = c.pins()
+    kept_nets = np.flatnonzero(keep[pins[net_ptr[:-1]]])
+    assert c.nets == len(kept_nets)
+    assert np.array_equal(cpins, m[np.concatenate([pins[net_ptr[e]: net_ptr[e + 1]] for e in kept_nets])])
+    # connected: one component
+    k2 = np.diff(cp)
+    f2 = np.repeat(cpins[cp[:-1]], k2)
+    assert connected_components(coo_matrix((np.ones(len(cpins)), (f2, cpins)), shape=(c.nodes,) * 2),
+                                directed=False)[0] == 1
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 8])
+def test_laplacian_rows_are_the_full_rows(ek, ranks):
+    """Each rank builds only its rows (ek_laplacian_build_rows): the same
+    entries and values, bit for bit, as the full Laplacian's slice."""
+    h = ek.Hypergraph.read(circuit_path("ibm01"))
+    L = h.laplacian()
+    for r in range(ranks):
+        row0, nrows, _ = ek.shard_rows(h.nodes, ranks, r)
+        S = h.laplacian_rows(row0, row0 + nrows)
+        p0, p1 = L.rowptr[row0], L.rowptr[row0 + nrows]
+        assert np.array_equal(S.rowptr, L.rowptr[row0: row0 + nrows + 1] - p0)
+        assert np.array_equal(S.col, L.col[p0:p1])
+        assert np.array_equal(S.val.view(np.uint64), L.val[p0:p1].view(np.uint64))

@@ -5,11 +5,13 @@ reference), the SURVEY §8c swap-log md5s and known-answer swaps, the derived
 integer net cuts, and the reference's shipped cEIG Fiedler files
 (tests/golden/pre_saved_EIG)."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
 
-from conftest import CIRCUITS, NET_CUTS, SWAP_MD5, circuit_path, compare_results_text, eig_path, ref_results_path
+from conftest import (CIRCUITS, GOLD, NET_CUTS, SWAP_MD5, circuit_path, compare_results_text, eig_path,
+                      ref_results_path)
 
 # SURVEY §8c known answers: (swap index, node1, node2, hex gain)
 KAT = {"ibm01": (0, 10028, 11654, "0x1.59999cp+3"), "industry2": (0, 5263, 6568, "0x1.d1451ap+2"),
@@ -73,3 +75,21 @@ def test_oracle_spmv_is_the_laplacian(oracle):
     ref = np.add.reduceat(val * x[col], rp[:-1])
     assert np.allclose(y, ref, rtol=1e-13, atol=1e-13)
     assert np.abs(g.spmv(np.ones(g.nodes))).max() < 1e-12
+
+
+# ------------------------------------------------ random init (cKL.cpp:176-192)
+SEEDED = [("fract", 1), ("fract", 7), ("fract", 12345), ("ibm01", 1)]
+
+
+@pytest.mark.parametrize("name,seed", SEEDED)
+def test_oracle_random_init_matches_seeded_reference(oracle, name, seed):
+    """The random branch of shuffleSparceMatrix replayed: the real reference cKL
+    built with its random_device seed fixed (oracle/ref_seed.h) vs the oracle
+    on oracle.random_split (std::mt19937 + std::shuffle): every row of the
+    results file (tests/golden/ref_results_seed, oracle/gen_golden.py --seeded)."""
+    g = oracle.Graph.read(circuit_path(name))
+    o0, o1 = oracle.random_split(g.nodes, seed)
+    assert len(o0) == g.nodes // 2 and sorted(np.concatenate([o0, o1]).tolist()) == list(range(g.nodes))
+    log, res = g.kl(o0, o1)
+    ref = open(os.path.join(GOLD, "ref_results_seed", f"{name}.seed{seed}.txt")).read()
+    compare_results_text(oracle.format_results(log, res["initial_cut"]), ref)
