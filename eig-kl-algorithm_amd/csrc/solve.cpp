@@ -9,8 +9,6 @@
 // the KL adjacency (hash-order emulation) is built on a host thread while the
 // GPU runs the Lanczos solve.  Multi-rank contexts shard the Lanczos rows
 // (each rank builds and uploads only its rows); the KL loop is rank 0's.
-#include <sys/stat.h>
-
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -154,7 +152,8 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     if (log_out && cap > 0) std::copy(log.begin(), log.begin() + std::min(iters, cap), log_out);
     t = clk::now();
     if (o.write_results) {  // results/<base>_KL_CutSize[_EIG]_output.txt (cKL.cpp:438-444, 315, 380)
-        ::mkdir(join(o.out_dir, "results").c_str(), 0755);
+        std::error_code ec;  // results/ (and out_dir) created as needed, like the reference's createDir
+        std::filesystem::create_directories(join(o.out_dir, "results"), ec);
         const std::string path =
             join(o.out_dir, "results/" + base + (o.eig ? "_KL_CutSize_EIG_output.txt" : "_KL_CutSize_output.txt"));
         FILE* f = std::fopen(path.c_str(), "w");

@@ -15,7 +15,13 @@ GPU; prints one JSON line.
              -EIG branch cKL.cpp:155-174), compared swap by swap with the GPU
              swap log and net cuts bench.py saved
 
-usage: cpu_baseline.py HGR SPLIT_NPZ THREADS
+The Lanczos runs to convergence, capped at MAX_MATVEC matvecs (bench.py
+passes 3x the GPU solve's count: on the disconnected synthetic the null space
+is huge and the thick-restart restatement can take far longer than the GPU's
+implicit-restart solve to settle on one null vector; a capped run is reported
+as such, never extrapolated).
+
+usage: cpu_baseline.py HGR SPLIT_NPZ THREADS [MAX_MATVEC]
 """
 import json
 import os
@@ -27,6 +33,11 @@ import numpy as np
 
 def main():
     hgr, split_npz, threads = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    max_matvec = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+
+    def note(msg):
+        print(f"[cpu_baseline {threads}t] {msg}", file=sys.stderr, flush=True)
+
     cpus = sorted(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(cpus)))
     os.sched_setaffinity(0, cpus[:threads])  # before libgomp starts its pool
@@ -38,15 +49,18 @@ def main():
     t0 = time.time()
     g = oracle.Graph.read(hgr)
     t_parse = time.time() - t0
+    note(f"parsed in {t_parse:.2f} s; Lanczos (cap {max_matvec or 'none'} matvecs)")
     t1 = time.time()
-    lam, _, st = g.lanczos(deflate=True)
+    lam, _, st = g.lanczos(deflate=True, max_matvec=max_matvec)
     t_lanczos = time.time() - t1
+    note(f"Lanczos {t_lanczos:.2f} s, {st['matvecs']} matvecs, converged {st['converged']}; KL")
     z = np.load(split_npz)
     bits, glog = z["bits"], z["log"]
     idx = np.arange(len(bits), dtype=np.int32)
     t2 = time.time()
     olog, ores = g.kl(idx[bits == 0], idx[bits == 1], cap=None)
     t_kl = time.time() - t2
+    note(f"KL {t_kl:.2f} s, {ores['iterations']} swaps")
     n = min(len(olog), len(glog))
     fields_equal = len(olog) == len(glog) and all(
         np.array_equal(olog[f], glog[f]) for f in ("iter", "node_left", "node_right")) and all(

@@ -114,10 +114,9 @@ def test_lcc_fiedler_and_kl_vs_reference(ek, oracle, ctx):
     assert np.array_equal(bits[far], bits_ref[far])
     # KL from the reference run's split: the real cKL results file, and the oracle swap by swap
     log, res = _kl_vs_oracle(ek, oracle, ctx, h, bits_ref)
-    gz = os.path.join(d, "ref_results.txt.gz")
-    if not os.path.exists(gz):
-        pytest.skip("reference cKL run on the component not committed yet (oracle/gen_golden.py --lcc)")
-    compare_results_text(oracle.format_results(log, res["initial_cut"]), gzip.open(gz, "rt").read())
+    ref = gzip.open(os.path.join(d, "ref_results.txt.gz"), "rt").read()
+    compare_results_text(oracle.format_results(log, res["initial_cut"]), ref)
+    assert res["iterations"] == meta["reference_run"]["iterations"]
 
 
 @pytest.mark.parametrize("name,seed", [("fract", 1), ("fract", 7), ("fract", 12345), ("ibm01", 1)])

@@ -93,3 +93,23 @@ def test_oracle_random_init_matches_seeded_reference(oracle, name, seed):
     log, res = g.kl(o0, o1)
     ref = open(os.path.join(GOLD, "ref_results_seed", f"{name}.seed{seed}.txt")).read()
     compare_results_text(oracle.format_results(log, res["initial_cut"]), ref)
+
+
+def test_oracle_kl_matches_reference_on_lcc_1x(oracle, ek):
+    """The oracle at ibm18 scale against the REAL reference: the 1.0x
+    synthetic's largest connected component (184,306 nodes), KL from the split
+    the reference run used (tests/golden/syn1_lcc: 22,872 swaps, 41 min of
+    reference cKL on 4 cores), every row of its results file."""
+    import gzip
+    import json
+    d = os.path.join(GOLD, "syn1_lcc")
+    meta = json.load(open(os.path.join(d, "meta.json")))
+    h, _ = ek.Hypergraph.generate(1.0, 1).largest_component()
+    assert (h.nodes, h.nets) == (meta["nodes"], meta["nets"])
+    bits = np.unpackbits(np.load(os.path.join(d, "split_bits.npy")))[: h.nodes]
+    g = oracle.Graph.from_pins(h.nodes, *h.pins())
+    idx = np.arange(h.nodes, dtype=np.int32)
+    log, res = g.kl(idx[bits == 0], idx[bits == 1])
+    assert res["iterations"] == meta["reference_run"]["iterations"]
+    compare_results_text(oracle.format_results(log, res["initial_cut"]),
+                         gzip.open(os.path.join(d, "ref_results.txt.gz"), "rt").read())
