@@ -63,7 +63,7 @@ class SolveOpts(ctypes.Structure):
 
 
 _SOLVE_TIMES = ("t_read", "t_laplacian", "t_lanczos", "t_split", "t_kl_graph_wait", "t_kl_setup", "t_kl",
-                "t_write", "t_total")
+                "t_write", "t_total", "t_spmv_setup")
 
 
 class SolveResult(ctypes.Structure):
@@ -118,6 +118,7 @@ _sig("ek_spmv_setup", ctypes.c_int, _P, _I64, _I64, _I64, _P, _P, _P)
 _sig("ek_spmv", ctypes.c_int, _P, _P, _P, _P)
 _sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
 _sig("ek_spmv_bytes", _I64, _P)
+_sig("ek_spmv_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("ek_spmv_format", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64))
 _sig("ek_spmv_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
@@ -400,15 +401,21 @@ class Context:
     def spmv_device(self, x_ptr, y_ptr, stream=None):
         _chk(_lib.ek_spmv(self._c, x_ptr, y_ptr, stream), "spmv")
 
+    def spmv_dims(self):
+        """(n, row0, nrows) of the rows the context owns (ek_spmv_dims)."""
+        n, r0, nr = _I64(), _I64(), _I64()
+        _chk(_lib.ek_spmv_dims(self._c, ctypes.byref(n), ctypes.byref(r0), ctypes.byref(nr)), "spmv_dims")
+        return n.value, r0.value, nr.value
+
     def spmv_bytes(self, fused=False):
         """Algorithmic bytes of one SpMV; fused: the Lanczos form (+ f read, basis column write)."""
-        return _lib.ek_spmv_bytes(self._c) + (16 * self.nrows if fused else 0)
+        return _lib.ek_spmv_bytes(self._c) + (16 * self.spmv_dims()[2] if fused else 0)
 
     def spmv_format(self, fused=False):
         """(packed, stored bytes per launch): the storage the SpMV reads (ek_spmv_format)."""
         pk, b = ctypes.c_int32(0), _I64(0)
         _chk(_lib.ek_spmv_format(self._c, ctypes.byref(pk), ctypes.byref(b)), "ek_spmv_format")
-        return bool(pk.value), int(b.value) + (16 * self.nrows if fused else 0)
+        return bool(pk.value), int(b.value) + (16 * self.spmv_dims()[2] if fused else 0)
 
     def spmv_bench(self, iters=200, fused=True):
         """Average microseconds per back-to-back SpMV launch on resident buffers."""

@@ -47,8 +47,13 @@ int guard_exceptions() {
     }
 }
 
+static thread_local int g_thread_cap = 0;
+
+ThreadCap::ThreadCap(int cap) : prev(g_thread_cap) { g_thread_cap = cap; }
+ThreadCap::~ThreadCap() { g_thread_cap = prev; }
+
 int host_threads() {
-    static int cached = [] {
+    static const int cached = [] {
         for (const char* var : {"EK_THREADS", "OMP_NUM_THREADS"}) {
             if (const char* s = std::getenv(var)) {
                 const int v = std::atoi(s);
@@ -58,7 +63,7 @@ int host_threads() {
         const unsigned hw = std::thread::hardware_concurrency();
         return int(std::min(16u, std::max(1u, hw)));
     }();
-    return cached;
+    return g_thread_cap > 0 ? std::max(1, std::min(cached, g_thread_cap)) : cached;
 }
 
 }  // namespace ek

@@ -361,6 +361,16 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     EK_CATCH
 }
 
+int ek_spmv_dims(ek_ctx* c, int64_t* n, int64_t* row0, int64_t* nrows) {
+    EK_TRY
+    check_ctx(c);
+    if (n) *n = c->n;
+    if (row0) *row0 = c->row0;
+    if (nrows) *nrows = c->nrows;
+    return EK_OK;
+    EK_CATCH
+}
+
 int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
     EK_TRY
     check_ctx(c);

@@ -21,8 +21,14 @@ struct Error {
 [[noreturn]] void fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int guard_exceptions();  // maps the in-flight exception to a status (call from catch(...))
 
-// bounded host parallelism (std::thread); EK_THREADS or OMP_NUM_THREADS caps it
+// bounded host parallelism (std::thread); EK_THREADS or OMP_NUM_THREADS caps it,
+// and a ThreadCap on the calling thread lowers it for the work that thread starts
 int host_threads();
+struct ThreadCap {
+    explicit ThreadCap(int cap);
+    ~ThreadCap();
+    int prev;
+};
 template <class F>
 void parallel_for(int64_t n, F&& fn);  // fn(begin, end)
 template <class F>
@@ -80,7 +86,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
            const ek_solve_opts& o, ek_swap* log_out, int64_t cap, ek_solve_result& r);
 void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek_solve_opts& o, double& lambda,
                     std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
-                    const std::function<void()>& after_laplacian = {});
+                    const std::function<void()>& after_laplacian = {}, double* t_spmv_setup = nullptr);
 }  // namespace ek
 
 // ---------------------------------------------------------------------------

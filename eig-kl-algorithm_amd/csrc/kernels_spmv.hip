@@ -32,123 +32,7 @@
 namespace ek {
 namespace dev {
 
-std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int block_nnz) {
-    std::vector<int32_t> starts{0};
-    int64_t rows_in = 0, nnz_in = 0;
-    for (int64_t r = 0; r < nrows; ++r) {
-        const int64_t len = rowptr[r + 1] - rowptr[r];
-        if (rows_in > 0 && (nnz_in + len > block_nnz || rows_in == SPMV_THREADS)) {
-            starts.push_back(int32_t(r));
-            rows_in = nnz_in = 0;
-        }
-        ++rows_in;
-        nnz_in += len;
-        if (len > block_nnz) {  // long row: a workgroup of its own (vector mode)
-            starts.push_back(int32_t(r + 1));
-            rows_in = nnz_in = 0;
-        }
-    }
-    if (starts.back() != int32_t(nrows)) starts.push_back(int32_t(nrows));
-    // one {row0, nrows, nnz0, cnt} record per block
-    std::vector<int32_t> desc;
-    desc.reserve((starts.size() - 1) * 4);
-    for (size_t b = 0; b + 1 < starts.size(); ++b) {
-        const int32_t r0 = starts[b], r1 = starts[b + 1];
-        desc.push_back(r0);
-        desc.push_back(r1 - r0);
-        desc.push_back(rowptr[r0]);
-        desc.push_back(rowptr[r1] - rowptr[r0]);
-    }
-    return desc;
-}
-
-// Dictionary coding of the Laplacian values (see SpmvMat in ek_internal.hpp).
-// One open-addressing pass assigns first-seen codes and counts them; the codes
-// are then renumbered by descending frequency (ties: first seen) so the hot
-// off-diagonal values (-2/|e| for the few net sizes) share one cache line.
-bool spmv_pack(int64_t n, int64_t nnz, const int32_t* col, const double* val, std::vector<uint32_t>& pk,
-               std::vector<double>& dict, int& colbits) {
-    colbits = 1;
-    while (colbits < 31 && (int64_t(1) << colbits) < n) ++colbits;
-    if (colbits > 28) return false;
-    const uint32_t max_codes = 1u << (32 - colbits);
-    size_t cap = 1024;
-    std::vector<uint64_t> keys(cap);
-    std::vector<int32_t> slot(cap, -1);  // code in the slot, -1 = empty
-    std::vector<uint64_t> first;         // bit pattern of code c
-    std::vector<int64_t> cnt;
-    std::vector<uint32_t> code(size_t(std::max<int64_t>(nnz, 0)));
-    auto hash = [](uint64_t k) { return (k ^ (k >> 29)) * 0x9E3779B97F4A7C15ull; };
-    for (int64_t p = 0; p < nnz; ++p) {
-        uint64_t k;
-        std::memcpy(&k, &val[p], 8);
-        size_t h = size_t(hash(k) >> 20) & (cap - 1);
-        while (slot[h] >= 0 && keys[h] != k) h = (h + 1) & (cap - 1);
-        if (slot[h] < 0) {
-            if (first.size() >= max_codes) return false;
-            slot[h] = int32_t(first.size());
-            keys[h] = k;
-            first.push_back(k);
-            cnt.push_back(0);
-            if (first.size() * 2 > cap) {  // grow: rehash the codes seen so far
-                cap *= 2;
-                keys.assign(cap, 0);
-                slot.assign(cap, -1);
-                for (size_t c = 0; c < first.size(); ++c) {
-                    size_t g = size_t(hash(first[c]) >> 20) & (cap - 1);
-                    while (slot[g] >= 0) g = (g + 1) & (cap - 1);
-                    slot[g] = int32_t(c);
-                    keys[g] = first[c];
-                }
-                h = 0;
-                while (!(slot[h] >= 0 && keys[h] == k)) h = (h + 1) & (cap - 1);
-            }
-        }
-        ++cnt[size_t(slot[h])];
-        code[size_t(p)] = uint32_t(slot[h]);
-    }
-    std::vector<uint32_t> order(first.size());
-    for (size_t c = 0; c < order.size(); ++c) order[c] = uint32_t(c);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cnt[a] > cnt[b]; });
-    std::vector<uint32_t> rank(order.size());
-    dict.resize(order.size());
-    for (size_t r = 0; r < order.size(); ++r) {
-        rank[order[r]] = uint32_t(r);
-        std::memcpy(&dict[r], &first[order[r]], 8);
-    }
-    pk.resize(size_t(std::max<int64_t>(nnz, 0)));
-    for (int64_t p = 0; p < nnz; ++p) pk[size_t(p)] = (rank[code[size_t(p)]] << colbits) | uint32_t(col[p]);
-    return true;
-}
-
-// Per-block segments of the coded entries: block b's entries at
-// [b*seg_nnz, +cnt), padded with word 0; a long row (vector mode) goes
-// to an overflow area after the segments and its descriptor's nnz0 points
-// there.  rel[b*SPMV_REL_STRIDE + t] = start of the block's row t inside the
-// segment for t <= nrows, cnt beyond.
-void spmv_segment(std::vector<int32_t>& desc, const int32_t* rowptr, const std::vector<uint32_t>& pk, int seg_nnz,
-                  std::vector<uint32_t>& seg, std::vector<uint16_t>& rel) {
-    const size_t SEG = size_t(seg_nnz);
-    const size_t nb = desc.size() / 4;
-    size_t over = 0;
-    for (size_t b = 0; b < nb; ++b)
-        if (size_t(desc[4 * b + 3]) > SEG) over += size_t(desc[4 * b + 3]);
-    seg.assign(nb * SEG + over, 0u);
-    rel.assign(nb * SPMV_REL_STRIDE, 0);
-    size_t off = nb * SEG;
-    for (size_t b = 0; b < nb; ++b) {
-        const int32_t r0 = desc[4 * b], nr = desc[4 * b + 1], p0 = desc[4 * b + 2], cnt = desc[4 * b + 3];
-        if (size_t(cnt) > SEG) {
-            std::copy(pk.begin() + p0, pk.begin() + p0 + cnt, seg.begin() + off);
-            desc[4 * b + 2] = int32_t(off);
-            off += size_t(cnt);
-            continue;
-        }
-        std::copy(pk.begin() + p0, pk.begin() + p0 + cnt, seg.begin() + b * SEG);
-        for (int t = 0; t < SPMV_REL_STRIDE; ++t)
-            rel[b * SPMV_REL_STRIDE + t] = uint16_t(t <= nr ? rowptr[r0 + t] - p0 : cnt);
-    }
-}
+// Host preparation of the row blocks and the coded segments: spmv_host.cpp.
 
 __device__ __forceinline__ void finalize_publish(const StepFin& f, double n2) {
     f.fn2_out[0] = n2;

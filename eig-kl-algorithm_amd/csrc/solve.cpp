@@ -31,7 +31,8 @@ struct KLHost {
     std::vector<float> w;
 };
 
-KLHost kl_graph_host(const ek_hgr* h) {
+KLHost kl_graph_host(const ek_hgr* h, int threads) {
+    ThreadCap cap(threads);
     ek_csr G;
     build_kl_graph(*h, G);
     KLHost g;
@@ -56,7 +57,7 @@ std::string join(const char* dir, const std::string& rel) {
 // on the host, uploaded, Lanczos on the GPU; the full vector on every rank.
 void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek_solve_opts& o, double& lambda,
                     std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
-                    const std::function<void()>& after_laplacian) {
+                    const std::function<void()>& after_laplacian, double* t_spmv_setup) {
     const int64_t n = h.nodes;
     int64_t row0 = 0, nrows = n, nloc = n;
     chk(ek_shard_rows(n, nranks, rank, &row0, &nrows, &nloc));
@@ -68,6 +69,7 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
         if (after_laplacian) after_laplacian();
         t = clk::now();
         chk(ek_spmv_setup(ctx, n, row0, nrows, L.rowptr.data(), L.col.data(), L.val64.data()));
+        if (t_spmv_setup) *t_spmv_setup = since(t);
     }
     v.assign(size_t(n), 0.0);
     chk(ek_lanczos_fiedler(ctx, &o.lanczos, &lambda, v.data(), &st));
@@ -90,15 +92,18 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     // initial partition (shuffleSparceMatrix, cKL.cpp:151-197)
     std::vector<int32_t> order0, order1;
     std::future<KLHost> kg;
+    // while the GPU solves, the KL adjacency leaves the solve's host thread
+    // (and the HIP runtime's) a few cores
     auto start_kl_graph = [&] {
-        if (rank == 0) kg = std::async(std::launch::async, kl_graph_host, &h);
+        if (rank == 0)
+            kg = std::async(std::launch::async, kl_graph_host, &h, o.eig == 1 ? std::max(1, host_threads() - 4) : 0);
     };
     if (o.eig == 1) {
         std::vector<double> v;
         // the KL adjacency starts once the Laplacian rows are built (both use
         // every host thread), and runs while the GPU solves
         fiedler_vector(get_ctx(), rank, nranks, h, o, r.lambda, v, r.lanczos, &r.t_laplacian, &r.t_lanczos,
-                       start_kl_graph);
+                       start_kl_graph, &r.t_spmv_setup);
         if (rank != 0) {
             r.t_total = since(t0);
             return;

@@ -137,6 +137,9 @@ int ek_comm_init_host(ek_ctx* ctx, int nranks, int rank, ek_allgather_fn allgath
  * are copied; the caller keeps ownership. */
 int ek_spmv_setup(ek_ctx* ctx, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr,
                   const int32_t* col, const double* val);
+/* The rows the context owns after the last ek_spmv_setup (any of the
+ * pointers may be NULL). */
+int ek_spmv_dims(ek_ctx* ctx, int64_t* n, int64_t* row0, int64_t* nrows);
 /* y[0:nrows] = L[row0:row0+nrows, :] x.  x_dev: n doubles, y_dev: nrows
  * doubles, device pointers borrowed.  stream = hipStream_t or NULL (ctx
  * stream).  Asynchronous. */
@@ -276,8 +279,10 @@ typedef struct {
     double lambda, median;
     ek_lanczos_stats lanczos; /* eig = 1 */
     ek_kl_result kl;          /* rank 0 only */
-    /* wall seconds of the phases on this rank (host clock) */
+    /* wall seconds of the phases on this rank (host clock); t_lanczos
+     * includes t_spmv_setup (the rows' coding and upload) */
     double t_read, t_laplacian, t_lanczos, t_split, t_kl_graph_wait, t_kl_setup, t_kl, t_write, t_total;
+    double t_spmv_setup;
 } ek_solve_result;
 
 void ek_solve_default_opts(ek_solve_opts* o);
