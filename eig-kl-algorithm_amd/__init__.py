@@ -54,7 +54,7 @@ class KLResult(ctypes.Structure):
     _fields_ = [("iterations", _I64), ("initial_cut", ctypes.c_float), ("best_cut", ctypes.c_float),
                 ("final_cut", ctypes.c_float), ("best_iter", _I64), ("net_cut_initial", _I64),
                 ("net_cut_best", _I64), ("net_cut_final", _I64), ("loop_ms", ctypes.c_double),
-                ("total_ms", ctypes.c_double)]
+                ("total_ms", ctypes.c_double), ("prefetch_hits", _I64)]
 
 
 class SolveOpts(ctypes.Structure):

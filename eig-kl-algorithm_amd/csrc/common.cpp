@@ -1,4 +1,5 @@
 // Error plumbing and host-thread sizing for libeigkl_hip.so.
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <exception>
@@ -51,6 +52,21 @@ static thread_local int g_thread_cap = 0;
 
 ThreadCap::ThreadCap(int cap) : prev(g_thread_cap) { g_thread_cap = cap; }
 ThreadCap::~ThreadCap() { g_thread_cap = prev; }
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+PhaseTimer::PhaseTimer(const char* t) : tag(t), t0(0.0), on(std::getenv("EK_TRACE") != nullptr) {
+    if (on) t0 = now_ms();
+}
+
+void PhaseTimer::mark(const char* what) {
+    if (!on) return;
+    const double t = now_ms();
+    std::fprintf(stderr, "[%s] %s %.3f ms\n", tag, what, t - t0);
+    t0 = t;
+}
 
 int host_threads() {
     static const int cached = [] {

@@ -308,6 +308,7 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     if (n <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > n || !rowptr || (nrows && (!col || !val)))
         ek::fail(EK_EINVAL, "ek_spmv_setup: bad argument");
     if (rowptr[0] != 0) ek::fail(EK_EINVAL, "ek_spmv_setup: rowptr[0] must be 0 (local rows)");
+    ek::PhaseTimer pt("spmv_setup");
     const int64_t nnz = rowptr[nrows];
     for (int64_t r = 0; r < nrows; ++r)
         if (rowptr[r + 1] < rowptr[r]) ek::fail(EK_EINVAL, "ek_spmv_setup: rowptr not monotone");
@@ -328,7 +329,9 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     std::vector<double> dictv;
     int colbits = 0;
     const char* plain = std::getenv("EK_SPMV_PLAIN");
+    pt.mark("validate");
     const bool packed = !(plain && plain[0] && plain[0] != '0') && ek::dev::spmv_pack(n, nnz, col, val, pkv, dictv, colbits);
+    pt.mark("pack");
     // 512-nnz blocks (tools/spmv_lab.hip for plain CSR; for the coded form,
     // 1024-nnz segments measured 14.3 against 12.7 us inside the solve)
     c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
@@ -338,7 +341,9 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     if (packed) {
         std::vector<uint32_t> segv;
         std::vector<uint16_t> relv;
+        pt.mark("row blocks");
         ek::dev::spmv_segment(rbv, rowptr, pkv, c->block_nnz, segv, relv);  // long rows: desc nnz0 -> overflow area
+        pt.mark("segments");
         upload(c->pk, segv.data(), segv.size(), c->stream);
         upload(c->rel, relv.data(), relv.size(), c->stream);
         upload(c->dict, dictv.data(), dictv.size(), c->stream);
@@ -357,6 +362,7 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     }
     upload(c->rb, rbv.data(), rbv.size(), c->stream);
     HIPCHK(hipStreamSynchronize(c->stream));
+    pt.mark("upload");
     return EK_OK;
     EK_CATCH
 }
@@ -1189,6 +1195,7 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_best = nets ? int64_t(hc[1]) : -1;
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
+        res->prefetch_hits = (long long)ho.prof[12];
         if (std::getenv("EK_KL_PROF")) {
             static const char* names[12] = {"select", "G1-key", "bar1", "G2a", "G2bc", "bar2", "G1-aux", "G1-sum",
                                             "n_stale", "n_late+tail", "G1-load", "G1-look"};

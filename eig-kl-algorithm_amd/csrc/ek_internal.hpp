@@ -5,6 +5,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <functional>
+#include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -29,6 +31,14 @@ struct ThreadCap {
     ~ThreadCap();
     int prev;
 };
+// EK_TRACE=1: host phase timings on stderr ("[tag] what ms")
+struct PhaseTimer {
+    explicit PhaseTimer(const char* tag);
+    void mark(const char* what);
+    const char* tag;
+    double t0;
+    bool on;
+};
 template <class F>
 void parallel_for(int64_t n, F&& fn);  // fn(begin, end)
 template <class F>
@@ -41,19 +51,44 @@ void run_threads(int T, F&& fn);  // fn(t) for t < T, t = 0 on the calling threa
     catch (...) { return ek::guard_exceptions(); }
 
 // ---------------------------------------------------------------------------
-// host objects
+// host objects.  Large arrays use dvec: std::vector whose resize leaves new
+// elements default-initialised (not zeroed), so the threads that fill them
+// also first-touch their pages instead of one thread zeroing them first.
+namespace ek {
+template <class T>
+struct default_init_allocator : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = default_init_allocator<U>;
+    };
+    default_init_allocator() = default;
+    template <class U>
+    default_init_allocator(const default_init_allocator<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using dvec = std::vector<T, default_init_allocator<T>>;
+}  // namespace ek
+
 struct ek_hgr {
     int64_t nets = 0, nodes = 0;
-    std::vector<int64_t> net_ptr;  // nets + 1
-    std::vector<int32_t> pins;     // 0-based
+    ek::dvec<int64_t> net_ptr;  // nets + 1
+    ek::dvec<int32_t> pins;     // 0-based
 };
 
 struct ek_csr {
     int64_t nrows = 0;
     int32_t value_bytes = 8;
-    std::vector<int32_t> rowptr, col, nfwd;
-    std::vector<double> val64;
-    std::vector<float> val32;
+    ek::dvec<int32_t> rowptr, col, nfwd;
+    ek::dvec<double> val64;
+    ek::dvec<float> val32;
 };
 
 namespace ek {

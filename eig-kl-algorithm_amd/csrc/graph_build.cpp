@@ -132,34 +132,70 @@ void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& L) {
     const int64_t n = h.nodes, nr = r1 - r0;
     if (r0 < 0 || r1 > n || nr < 0) fail(EK_EINVAL, "Laplacian rows [%lld, %lld) outside [0, %lld)", (long long)r0,
                                          (long long)r1, (long long)n);
-    // incidences (net, pin position) of the owned rows, nets ascending
-    std::vector<int64_t> ip(size_t(nr) + 1, 0);
-    for (int64_t e = 0; e < h.nets; ++e) {
-        const int64_t p0 = h.net_ptr[size_t(e)], p1 = h.net_ptr[size_t(e) + 1];
-        if (p1 - p0 < 2) continue;
-        for (int64_t p = p0; p < p1; ++p) {
-            const int64_t v = h.pins[size_t(p)];
-            if (v >= r0 && v < r1) ++ip[size_t(v - r0) + 1];
-        }
-    }
-    for (int64_t i = 0; i < nr; ++i) ip[size_t(i) + 1] += ip[size_t(i)];
-    std::vector<int64_t> inc(size_t(ip[size_t(nr)]));  // pin position p; its net from net_of
-    std::vector<int32_t> inc_net(inc.size());
+    PhaseTimer pt("laplacian");
+    // incidences (pin position, net) of the owned rows, nets ascending: each
+    // thread counts its own range of nets, and the per-thread counts give
+    // every (thread, row) its slot range, so the parallel fill keeps net order
+    const int TI = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, int64_t(h.pins.size()) / 65536)));
+    std::vector<int64_t> ebeg(size_t(TI) + 1, 0);  // net ranges with balanced pin counts
     {
-        std::vector<int64_t> cur(ip.begin(), ip.end() - 1);
-        for (int64_t e = 0; e < h.nets; ++e) {
+        const int64_t np = int64_t(h.pins.size());
+        int64_t e = 0;
+        for (int t = 1; t < TI; ++t) {
+            const int64_t want = np * t / TI;
+            while (e < h.nets && h.net_ptr[size_t(e)] < want) ++e;
+            ebeg[size_t(t)] = e;
+        }
+        ebeg[size_t(TI)] = h.nets;
+    }
+    dvec<int32_t> tcnt(size_t(TI) * size_t(nr));
+    run_threads(TI, [&](int t) {
+        int32_t* c = tcnt.data() + size_t(t) * size_t(nr);
+        std::fill(c, c + nr, 0);
+        for (int64_t e = ebeg[size_t(t)]; e < ebeg[size_t(t) + 1]; ++e) {
+            const int64_t p0 = h.net_ptr[size_t(e)], p1 = h.net_ptr[size_t(e) + 1];
+            if (p1 - p0 < 2) continue;
+            for (int64_t p = p0; p < p1; ++p) {
+                const int64_t v = h.pins[size_t(p)];
+                if (v >= r0 && v < r1) ++c[v - r0];
+            }
+        }
+    });
+    std::vector<int64_t> ip(size_t(nr) + 1, 0);
+    for (int64_t i = 0; i < nr; ++i) {
+        int64_t tot = 0;
+        for (int t = 0; t < TI; ++t) tot += tcnt[size_t(t) * size_t(nr) + size_t(i)];
+        ip[size_t(i) + 1] = ip[size_t(i)] + tot;
+    }
+    parallel_for(nr, [&](int64_t lo, int64_t hi) {  // counts -> each thread's first slot per row
+        for (int64_t i = lo; i < hi; ++i) {
+            int64_t at = ip[size_t(i)];
+            for (int t = 0; t < TI; ++t) {
+                int32_t& c = tcnt[size_t(t) * size_t(nr) + size_t(i)];
+                const int32_t k = c;
+                c = int32_t(at - ip[size_t(i)]);
+                at += k;
+            }
+        }
+    });
+    dvec<int64_t> inc(size_t(ip[size_t(nr)]));  // pin position p
+    dvec<int32_t> inc_net(inc.size());
+    run_threads(TI, [&](int t) {
+        int32_t* c = tcnt.data() + size_t(t) * size_t(nr);
+        for (int64_t e = ebeg[size_t(t)]; e < ebeg[size_t(t) + 1]; ++e) {
             const int64_t p0 = h.net_ptr[size_t(e)], p1 = h.net_ptr[size_t(e) + 1];
             if (p1 - p0 < 2) continue;
             for (int64_t p = p0; p < p1; ++p) {
                 const int64_t v = h.pins[size_t(p)];
                 if (v >= r0 && v < r1) {
-                    const int64_t q = cur[size_t(v - r0)]++;
+                    const int64_t q = ip[size_t(v - r0)] + c[v - r0]++;
                     inc[size_t(q)] = p;
                     inc_net[size_t(q)] = int32_t(e);
                 }
             }
         }
-    }
+    });
+    pt.mark("incidences");
     const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, nr / 4096)));
     std::vector<std::vector<int32_t>> tcol{size_t(T)};
     std::vector<std::vector<double>> tval{size_t(T)};
@@ -222,6 +258,7 @@ void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& L) {
         }
     };
     run_threads(T, work);
+    pt.mark("rows");
     L.nrows = nr;
     L.value_bytes = 8;
     L.rowptr.assign(size_t(nr) + 1, 0);
@@ -236,6 +273,7 @@ void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& L) {
         std::copy(tcol[size_t(t)].begin(), tcol[size_t(t)].end(), L.col.begin() + at);
         std::copy(tval[size_t(t)].begin(), tval[size_t(t)].end(), L.val64.begin() + at);
     });
+    pt.mark("assemble");
 }
 
 void build_laplacian(const ek_hgr& h, ek_csr& L) { build_laplacian_rows(h, 0, h.nodes, L); }
@@ -243,6 +281,7 @@ void build_laplacian(const ek_hgr& h, ek_csr& L) { build_laplacian_rows(h, 0, h.
 // ---------------------------------------------------------------------------
 // cKL.cpp:107-131 + connections() order (cKL.cpp:229-248).
 void build_kl_graph(const ek_hgr& h, ek_csr& G) {
+    PhaseTimer pt("kl_graph");
     const int64_t n = h.nodes;
     // 1. upper-triangle pairs per row (min endpoint), in net order
     std::vector<int64_t> cnt(size_t(n) + 1, 0);
@@ -320,6 +359,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
         }
     });
     if (too_big) fail(EK_EINVAL, "hash-order emulation: a row exceeds the bucket table");
+    pt.mark("pairs + map order");
     std::vector<float>().swap(pw);
     std::vector<uint32_t>().swap(pk);
     // 3. backward lists: for rows i ascending, (i, w) appended to key k's list
@@ -356,6 +396,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
                 G.col[size_t(bcur[k])] = int32_t(i);
                 G.val32[size_t(bcur[k]++)] = w;
             }
+    pt.mark("backward + assemble");
 }
 
 }  // namespace ek
@@ -435,3 +476,4 @@ int ek_shard_rows(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows
 }
 
 }  // extern "C"
+

@@ -57,14 +57,22 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 }
 
 // partial dot products of w with GT_COLS basis columns over GT_ROWS rows.
-// grid = (nrb, ceil((ncols + has_u0) / GT_COLS)); 256 threads, each
-// GT_ROWS/512 double2 rows; column ncols is the deflation vector u0.
+// 1-D grid of nrb * ncg blocks (ncg = ceil((ncols + has_u0) / GT_COLS));
+// 256 threads, each GT_ROWS/512 double2 rows; column ncols is the deflation
+// vector u0.  The blocks are dealt round-robin over the 8 XCDs; the
+// (row block, column group) map gives each XCD a contiguous run of row
+// blocks with all their column groups (the guide's bijective XCD remap), so
+// a row block's slice of w is fetched into one XCD's L2 and re-read from
+// there by its other column groups.  Same partials, same bits.
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part) {
     __shared__ double red[4][GT_COLS];
     const int t = threadIdx.x;
-    const int rbk = blockIdx.x, j0 = blockIdx.y * GT_COLS;
+    const int ncg = (ncols + has_u0 + GT_COLS - 1) / GT_COLS;
+    const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+    const int v = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+    const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
     double acc[GT_COLS];
 #pragma unroll
     for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
@@ -347,8 +355,8 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
            const double* w, double* part) {
     const int cols = ncols + has_u0;
     if (cols <= 0) return;
-    hipLaunchKernelGGL(k_gemvt, dim3(nrb, (cols + GT_COLS - 1) / GT_COLS), dim3(256), 0, s, ldv, nrb, V, ncols, has_u0,
-                       u0val, nreal, w, part);
+    hipLaunchKernelGGL(k_gemvt, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V, ncols,
+                       has_u0, u0val, nreal, w, part);
 }
 
 

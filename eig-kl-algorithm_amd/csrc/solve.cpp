@@ -27,8 +27,8 @@ using clk = std::chrono::steady_clock;
 double since(clk::time_point t) { return std::chrono::duration<double>(clk::now() - t).count(); }
 
 struct KLHost {
-    std::vector<int32_t> rowptr, col;
-    std::vector<float> w;
+    dvec<int32_t> rowptr, col;
+    dvec<float> w;
 };
 
 KLHost kl_graph_host(const ek_hgr* h, int threads) {
@@ -163,12 +163,22 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
             join(o.out_dir, "results/" + base + (o.eig ? "_KL_CutSize_EIG_output.txt" : "_KL_CutSize_output.txt"));
         FILE* f = std::fopen(path.c_str(), "w");
         if (!f) fail(EK_EIO, "Error: Cannot open output file %s (%s)", path.c_str(), std::strerror(errno));
-        std::vector<char> buf(size_t(1) << 20);
-        std::setvbuf(f, buf.data(), _IOFBF, buf.size());
-        std::fprintf(f, "0\t%g\t0\n", double(r.kl.initial_cut));  // ostream default format == %g
-        for (int64_t i = 0; i < iters; ++i)
-            std::fprintf(f, "%u\t%g\t%g\n", log[size_t(i)].iter, double(log[size_t(i)].cut), double(log[size_t(i)].gain));
-        const bool ok = std::fclose(f) == 0;
+        // rows formatted on the host threads (ostream default format == %g), written in order
+        const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, iters / 2048)));
+        std::vector<std::string> part(static_cast<size_t>(T));
+        run_threads(T, [&](int t) {
+            const int64_t lo = iters * t / T, hi = iters * (t + 1) / T;
+            std::string& out = part[size_t(t)];
+            out.reserve(size_t(hi - lo) * 28 + 32);
+            char line[96];
+            if (t == 0) out.append(line, size_t(std::snprintf(line, sizeof line, "0\t%g\t0\n", double(r.kl.initial_cut))));
+            for (int64_t i = lo; i < hi; ++i)
+                out.append(line, size_t(std::snprintf(line, sizeof line, "%u\t%g\t%g\n", log[size_t(i)].iter,
+                                                      double(log[size_t(i)].cut), double(log[size_t(i)].gain))));
+        });
+        bool ok = true;
+        for (const std::string& p : part) ok &= std::fwrite(p.data(), 1, p.size(), f) == p.size();
+        ok &= std::fclose(f) == 0;
         if (!ok) fail(EK_EIO, "short write to %s", path.c_str());
     }
     r.t_write = since(t);

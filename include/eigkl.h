@@ -234,6 +234,7 @@ typedef struct {
     int64_t net_cut_initial, net_cut_best, net_cut_final; /* integer hyperedge cuts */
     double loop_ms;      /* device time of the swap loop */
     double total_ms;     /* device time of gain scan + loop + cuts */
+    int64_t prefetch_hits; /* swaps whose neighbour rows were loaded during the previous swap (speculation right) */
 } ek_kl_result;
 
 /* Upload the KL graph (from ek_kl_graph_build, or any rows in cKL order). */
