@@ -54,7 +54,7 @@ class KLResult(ctypes.Structure):
     _fields_ = [("iterations", _I64), ("initial_cut", ctypes.c_float), ("best_cut", ctypes.c_float),
                 ("final_cut", ctypes.c_float), ("best_iter", _I64), ("net_cut_initial", _I64),
                 ("net_cut_best", _I64), ("net_cut_final", _I64), ("loop_ms", ctypes.c_double),
-                ("total_ms", ctypes.c_double), ("prefetch_hits", _I64)]
+                ("total_ms", ctypes.c_double)]
 
 
 class SolveOpts(ctypes.Structure):
@@ -116,6 +116,7 @@ _sig("ek_solve_file", ctypes.c_int, _P, ctypes.c_char_p, ctypes.POINTER(SolveOpt
      ctypes.POINTER(SolveResult))
 _sig("ek_spmv_setup", ctypes.c_int, _P, _I64, _I64, _I64, _P, _P, _P)
 _sig("ek_spmv", ctypes.c_int, _P, _P, _P, _P)
+_sig("ek_spmv_setup_pins", ctypes.c_int, _P, _I64, _I64, _P, _P, ctypes.POINTER(ctypes.c_int32))
 _sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
 _sig("ek_spmv_bytes", _I64, _P)
 _sig("ek_spmv_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
@@ -391,6 +392,16 @@ class Context:
         nrows = len(rowptr) - 1
         _chk(_lib.ek_spmv_setup(self._c, int(n), int(row0), nrows, _p(rowptr), _p(col), _p(val)), "spmv_setup")
         self.n, self.nrows = int(n), nrows
+
+    def spmv_setup_pins(self, hgr):
+        """This context's Laplacian rows assembled on the GPU from the pins (ek_spmv_setup_pins);
+        returns True when the device build ran (False: the host fallback)."""
+        net_ptr, pins = hgr.pins()
+        dev = ctypes.c_int32(0)
+        _chk(_lib.ek_spmv_setup_pins(self._c, hgr.nodes, len(net_ptr) - 1, _p(net_ptr), _p(pins), ctypes.byref(dev)),
+             "spmv_setup_pins")
+        self.n, _, self.nrows = self.spmv_dims()
+        return bool(dev.value)
 
     def spmv_host(self, x):
         x = np.ascontiguousarray(x, np.float64)

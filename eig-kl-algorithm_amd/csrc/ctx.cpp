@@ -58,6 +58,24 @@ void upload(DBuf& d, const T* h, size_t n, hipStream_t s) {
 }
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+// Setup uploads through the context's pinned staging: a copy from pageable
+// memory makes the runtime pin (or bounce) the user pages on every call,
+// which on freshly parsed arrays costs milliseconds; a memcpy into pinned
+// memory and an async DMA do not.  The caller sizes the arena for all the
+// uploads of one setup call and drains the stream before the next call.
+struct Uploader {
+    ek_ctx* c;
+    hipStream_t s;
+    size_t off = 0;
+    Uploader(ek_ctx* ctx, hipStream_t st, size_t total);
+    template <class T>
+    void put(DBuf& d, const T* h, size_t n);
+};
+
+namespace {
 inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::dev::KL_CHUNK), ek::dev::KL_CHUNK); }
 
 }  // namespace
@@ -73,6 +91,8 @@ struct ek_ctx {
     void* host_user = nullptr;
     double* stage = nullptr;  // pinned staging of the host-staged exchange
     size_t stage_doubles = 0;
+    unsigned char* up = nullptr;  // pinned staging of the setup uploads (see Uploader)
+    size_t up_bytes = 0;
     double comm_ms = 0.0;     // host-observed time inside collectives (current solve)
     // Laplacian rows owned by this context
     int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
@@ -88,12 +108,37 @@ struct ek_ctx {
         kl_ckey0, kl_ckey1, kl_aux, kl_seg, kl_cutpart, kl_cut0, kl_log, kl_out, kl_sides_tmp, kl_count, kl_netptr, kl_pins;
     bool kl_graph_ready = false, kl_part_ready = false, kl_seg_ok = false, kl_segc_ok = false;
     DBuf kl_segc, kl_wdict;
+    // device build of the Laplacian rows (ek_spmv_setup_pins)
+    DBuf lb_netptr, lb_pins, lb_icnt, lb_rcnt, lb_cur, lb_ip, lb_rp, lb_tiles, lb_inc, lb_scol, lb_sval, lb_tval,
+        lb_ulen, lb_len, lb_diag, lb_long, lb_cnt, lb_off, lb_table, lb_flags, lb_codes;
     int kl_nwd = 0, kl_wcolbits = 0;
     std::vector<int32_t> kl_rowptr_h;  // host copy (row descriptors)
     std::vector<hipEvent_t> spmv_ev;   // SpMV timing events, created once per context
     double* pin = nullptr;             // pinned host staging (Ritz vector + residual rows)
     size_t pin_doubles = 0;
 };
+
+Uploader::Uploader(ek_ctx* ctx, hipStream_t st, size_t total) : c(ctx), s(st) {
+    total = (total + 64) * 2;  // alignment slack
+    if (c->up_bytes < total) {
+        if (c->up) HIPCHK(hipHostFree(c->up));
+        c->up = nullptr;
+        c->up_bytes = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->up), total, hipHostMallocDefault));
+        c->up_bytes = total;
+    }
+}
+
+template <class T>
+void Uploader::put(DBuf& d, const T* h, size_t n) {
+    d.ensure(n * sizeof(T));
+    if (!n) return;
+    off = (off + 63) / 64 * 64;
+    if (off + n * sizeof(T) > c->up_bytes) ek::fail(EK_EINVAL, "upload staging overflow");
+    std::memcpy(c->up + off, h, n * sizeof(T));
+    HIPCHK(hipMemcpyAsync(d.p, c->up + off, n * sizeof(T), hipMemcpyHostToDevice, s));
+    off += n * sizeof(T);
+}
 
 namespace {
 
@@ -236,6 +281,7 @@ void ek_destroy(ek_ctx* c) {
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
+    if (c->up) (void)hipHostFree(c->up);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -373,6 +419,177 @@ int ek_spmv_dims(ek_ctx* c, int64_t* n, int64_t* row0, int64_t* nrows) {
     if (n) *n = c->n;
     if (row0) *row0 = c->row0;
     if (nrows) *nrows = c->nrows;
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_ptr, const int32_t* pins,
+                       int32_t* on_device) {
+    EK_TRY
+    check_ctx(c);
+    if (n <= 0 || n > INT32_MAX || nets < 0 || !net_ptr || (net_ptr[nets] > 0 && !pins) || net_ptr[0] != 0)
+        ek::fail(EK_EINVAL, "ek_spmv_setup_pins: bad argument");
+    const int64_t npins = net_ptr[nets];
+    if (npins > INT32_MAX) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: too many pins");
+    int64_t raw_bound = 0;  // raw entries: every pin of a net of k >= 2 pins sees k - 1 others
+    for (int64_t e = 0; e < nets; ++e) {
+        const int64_t k = net_ptr[e + 1] - net_ptr[e];
+        if (k < 0) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: net_ptr not monotone");
+        if (k >= 2) raw_bound += k * (k - 1);
+    }
+    int64_t row0 = 0, nrows = n, nloc = n;
+    ek_shard_rows(n, c->nranks, c->rank, &row0, &nrows, &nloc);
+    ek::PhaseTimer pt("spmv_setup_pins");
+    hipStream_t s = c->stream;
+    auto host_fallback = [&](const char* why) {
+        if (std::getenv("EK_TRACE")) std::fprintf(stderr, "[spmv_setup_pins] host build: %s\n", why);
+        ek_hgr h;
+        h.nets = nets;
+        h.nodes = n;
+        h.net_ptr.assign(net_ptr, net_ptr + nets + 1);
+        h.pins.assign(pins, pins + npins);
+        ek_csr L;
+        ek::build_laplacian_rows(h, row0, row0 + nrows, L);
+        const int rc = ek_spmv_setup(c, n, row0, nrows, L.rowptr.data(), L.col.data(), L.val64.data());
+        if (rc != EK_OK) throw ek::Error{rc};
+        if (on_device) *on_device = 0;
+    };
+    if (std::getenv("EK_HOST_LAPLACIAN")) {
+        host_fallback("EK_HOST_LAPLACIAN");
+        return EK_OK;
+    }
+    for (int64_t p = 0; p < npins; ++p)
+        if (pins[p] < 0 || pins[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: pin %d out of range", pins[p]);
+    {
+        Uploader up(c, s, (size_t(nets) + 1) * 8 + size_t(std::max<int64_t>(npins, 1)) * 4);
+        up.put(c->lb_netptr, net_ptr, size_t(nets) + 1);
+        up.put(c->lb_pins, pins, size_t(std::max<int64_t>(npins, 1)));
+    }
+    const size_t nr = size_t(nrows);
+    ek::dev::LapBuild b;
+    b.nets = nets;
+    b.r0 = row0;
+    b.r1 = row0 + nrows;
+    b.net_ptr = c->lb_netptr.as<int64_t>();
+    b.pins = c->lb_pins.as<int32_t>();
+    c->lb_icnt.ensure((nr + 1) * 4);
+    c->lb_rcnt.ensure((nr + 1) * 4);
+    c->lb_cur.ensure((nr + 1) * 4);
+    c->lb_cnt.ensure(16);
+    HIPCHK(hipMemsetAsync(c->lb_icnt.p, 0, (nr + 1) * 4, s));
+    HIPCHK(hipMemsetAsync(c->lb_rcnt.p, 0, (nr + 1) * 4, s));
+    HIPCHK(hipMemsetAsync(c->lb_cur.p, 0, (nr + 1) * 4, s));
+    HIPCHK(hipMemsetAsync(c->lb_cnt.p, 0, 16, s));
+    c->lb_ip.ensure((nr + 1) * 8);
+    c->lb_rp.ensure((nr + 1) * 8);
+    c->lb_off.ensure((nr + 1) * 8);
+    constexpr int TSIZE = 1 << 16;  // dictionary table slots (power of two)
+    c->lb_tiles.ensure((std::max<size_t>(nr, TSIZE) / 1024 + 2) * 8);
+    c->lb_inc.ensure(size_t(std::max<int64_t>(npins, 1)) * 8);
+    const size_t raw = size_t(std::max<int64_t>(raw_bound, 1));
+    c->lb_scol.ensure(raw * 4);
+    c->lb_sval.ensure(raw * 8);
+    c->lb_tval.ensure(raw * 8);
+    c->lb_ulen.ensure((nr + 1) * 4);
+    c->lb_len.ensure((nr + 1) * 4);
+    c->lb_diag.ensure((nr + 1) * 8);
+    c->lb_long.ensure((nr + 1) * 4);
+    b.icnt = c->lb_icnt.as<int>();
+    b.rcnt = c->lb_rcnt.as<int>();
+    b.cur = c->lb_cur.as<int>();
+    b.ip = c->lb_ip.as<long long>();
+    b.rp = c->lb_rp.as<long long>();
+    b.inc = c->lb_inc.as<int32_t>();
+    b.scol = c->lb_scol.as<int>();
+    b.sval = c->lb_sval.as<double>();
+    b.tval = c->lb_tval.as<double>();
+    b.ulen = c->lb_ulen.as<int>();
+    b.len = c->lb_len.as<int>();
+    b.diag = c->lb_diag.as<double>();
+    b.long_rows = c->lb_long.as<int>();
+    b.counters = c->lb_cnt.as<int>();
+    long long* tiles = c->lb_tiles.as<long long>();
+    ek::dev::lap_count(s, b);
+    ek::dev::exclusive_scan(s, b.icnt, int64_t(nr), b.ip, tiles);
+    ek::dev::exclusive_scan(s, b.rcnt, int64_t(nr), b.rp, tiles);
+    ek::dev::lap_fill_rows(s, b);
+    int cnt_h[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(cnt_h, b.counters, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ek::dev::lap_long_rows(s, b, cnt_h[0]);
+    ek::dev::exclusive_scan(s, b.len, int64_t(nr), c->lb_off.as<long long>(), tiles);
+    // CSR on the device: rowptr (local), col, val; at most raw + nrows entries
+    c->rowptr.ensure((nr + 1) * 4);
+    c->col.ensure((raw + nr) * 4);
+    c->val.ensure((raw + nr) * 8);
+    ek::dev::lap_write(s, b, c->lb_off.as<long long>(), c->rowptr.as<int>(), c->col.as<int>(), c->val.as<double>());
+    std::vector<int32_t> rowptr(nr + 1);
+    HIPCHK(hipMemcpyAsync(rowptr.data(), c->rowptr.p, (nr + 1) * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cnt_h, b.counters, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    pt.mark("rows on device");
+    if (cnt_h[1] > 0) {
+        host_fallback("a row longer than the LDS sort");
+        return EK_OK;
+    }
+    const int64_t nnz = rowptr[nr];
+    c->n = n;
+    c->row0 = row0;
+    c->nrows = nrows;
+    c->nloc = c->nranks > 1 ? nloc : n;
+    c->nnz = nnz;
+    // the same greedy row blocks as the host path (ek_spmv_setup)
+    int colbits = 1;
+    while (colbits < 31 && (int64_t(1) << colbits) < n) ++colbits;
+    const char* plain_env = std::getenv("EK_SPMV_PLAIN");
+    bool packed = !(plain_env && plain_env[0] && plain_env[0] != '0') && colbits <= 28;
+    int64_t ncodes = 0;
+    if (packed) {
+        c->lb_table.ensure(size_t(TSIZE) * 8);
+        c->lb_flags.ensure(size_t(TSIZE) * 4);
+        c->lb_codes.ensure((size_t(TSIZE) + 1) * 8);
+        ek::dev::dict_build(s, nnz, c->val.as<double>(), c->lb_table.as<unsigned long long>(), TSIZE,
+                            b.counters + 1, c->lb_flags.as<int>(), c->lb_codes.as<long long>(), tiles);
+        long long nd = 0;
+        HIPCHK(hipMemcpyAsync(&nd, c->lb_codes.as<long long>() + TSIZE, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(cnt_h, b.counters, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        ncodes = nd;
+        packed = cnt_h[1] == 0 && nd <= TSIZE / 2 && nd <= (int64_t(1) << (32 - colbits));
+    }
+    c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
+    auto rbv = ek::dev::spmv_row_blocks(rowptr.data(), nrows, c->block_nnz);
+    c->nrb_spmv = int(rbv.size() / 4);
+    if (packed) {
+        const size_t nb = size_t(c->nrb_spmv), SEG = size_t(ek::dev::SPMV_SEG_NNZ);
+        size_t over = 0;  // long rows: overflow area after the segments (spmv_segment's layout)
+        for (size_t bk = 0; bk < nb; ++bk)
+            if (size_t(rbv[4 * bk + 3]) > SEG) {
+                rbv[4 * bk + 2] = int32_t(nb * SEG + over);
+                over += size_t(rbv[4 * bk + 3]);
+            }
+        c->pk.ensure((nb * SEG + over) * 4);
+        c->rel.ensure(nb * ek::dev::SPMV_REL_STRIDE * 2);
+        c->dict.ensure(size_t(std::max<int64_t>(ncodes, 1)) * 8);
+        upload(c->rb, rbv.data(), rbv.size(), s);
+        ek::dev::dict_values(s, c->lb_table.as<unsigned long long>(), TSIZE, c->lb_codes.as<long long>(),
+                             c->dict.as<double>());
+        ek::dev::encode_segments(s, int(nb), c->rb.as<int32_t>(), c->rowptr.as<int>(), c->col.as<int>(),
+                                 c->val.as<double>(), c->lb_table.as<unsigned long long>(), TSIZE,
+                                 c->lb_codes.as<long long>(), colbits, c->pk.as<uint32_t>(), c->rel.as<uint16_t>());
+        c->colbits = colbits;
+        c->mat_bytes = int64_t((nb * SEG + over) * 4 + nb * ek::dev::SPMV_REL_STRIDE * 2 + size_t(ncodes) * 8 +
+                               rbv.size() * 4);
+    } else {
+        upload(c->rb, rbv.data(), rbv.size(), s);
+        c->colbits = 0;
+        c->mat_bytes = 12 * nnz + 4 * (nrows + 1);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    pt.mark("blocks + coding");
+    if (on_device) *on_device = 1;
     return EK_OK;
     EK_CATCH
 }
@@ -938,14 +1155,21 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     hipStream_t s = c->stream;
     c->kl_n = n;
     c->kl_rowptr_h.assign(rowptr, rowptr + n + 1);
-    upload(c->kl_rowptr, rowptr, size_t(n) + 1, s);
+    Uploader up(c, s, (size_t(n) + 1) * 4 + size_t(nnz) * 8 + size_t(nnz) * 4);
+    up.put(c->kl_rowptr, rowptr, size_t(n) + 1);
     // 16 zero entries of tail padding: the swap loop reads rows 16 at a time unconditionally
     c->kl_col.ensure((size_t(nnz) + 16) * 4);
     c->kl_w.ensure((size_t(nnz) + 16) * 4);
     HIPCHK(hipMemsetAsync(c->kl_col.as<int32_t>() + nnz, 0, 16 * 4, s));
     HIPCHK(hipMemsetAsync(c->kl_w.as<float>() + nnz, 0, 16 * 4, s));
-    if (nnz) HIPCHK(hipMemcpyAsync(c->kl_col.p, col, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
-    if (nnz) HIPCHK(hipMemcpyAsync(c->kl_w.p, w, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
+    if (nnz) {
+        std::memcpy(c->up + up.off, col, size_t(nnz) * 4);
+        HIPCHK(hipMemcpyAsync(c->kl_col.p, c->up + up.off, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
+        up.off += size_t(nnz) * 4;
+        std::memcpy(c->up + up.off, w, size_t(nnz) * 4);
+        HIPCHK(hipMemcpyAsync(c->kl_w.p, c->up + up.off, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
+        up.off += size_t(nnz) * 4;
+    }
     // inline neighbour-row segments for the swap loop: weight-coded (128 B per
     // entry) when the distinct weights fit the code bits and the LDS table,
     // else plain (256 B per entry); skipped past 32 GB.  EK_KL_NOSEGC=1 at
@@ -959,7 +1183,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     c->kl_seg_ok = !c->kl_segc_ok && size_t(nnz) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30);
     if (c->kl_segc_ok) {
         DBuf dkw;
-        upload(dkw, kw.data(), kw.size(), s);
+        up.put(dkw, kw.data(), kw.size());
         upload(c->kl_wdict, wdict.data(), wdict.size(), s);
         c->kl_nwd = int(wdict.size());
         c->kl_wcolbits = wcolbits;
@@ -998,8 +1222,9 @@ int ek_kl_nets_setup(ek_ctx* c, int64_t nets, const int64_t* net_ptr, const int3
     check_ctx(c);
     if (nets < 0 || !net_ptr || (net_ptr[nets] > 0 && !pins)) ek::fail(EK_EINVAL, "ek_kl_nets_setup: bad argument");
     c->kl_nets = nets;
-    upload(c->kl_netptr, net_ptr, size_t(nets) + 1, c->stream);
-    upload(c->kl_pins, pins, size_t(net_ptr[nets]), c->stream);
+    Uploader up(c, c->stream, (size_t(nets) + 1) * 8 + size_t(net_ptr[nets]) * 4);
+    up.put(c->kl_netptr, net_ptr, size_t(nets) + 1);
+    up.put(c->kl_pins, pins, size_t(net_ptr[nets]));
     HIPCHK(hipStreamSynchronize(c->stream));
     return EK_OK;
     EK_CATCH
@@ -1029,10 +1254,11 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
     hipStream_t s = c->stream;
     c->kl_n0 = n0;
     c->kl_n1 = n1;
-    upload(c->kl_order0, order0, size_t(n0), s);
-    upload(c->kl_order1, order1, size_t(n1), s);
-    upload(c->kl_side_init, side.data(), size_t(n), s);
-    upload(c->kl_plist, plist.data(), size_t(n), s);
+    Uploader up(c, s, size_t(n0) * 4 + size_t(n1) * 4 + size_t(n) + size_t(n) * 4);
+    up.put(c->kl_order0, order0, size_t(n0));
+    up.put(c->kl_order1, order1, size_t(n1));
+    up.put(c->kl_side_init, side.data(), size_t(n));
+    up.put(c->kl_plist, plist.data(), size_t(n));
     // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr,
     // rowlen, plist}, built on the device from the lists just uploaded (the
     // by-position arrays are padded to whole chunks with zero descriptors, and
@@ -1195,7 +1421,6 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_best = nets ? int64_t(hc[1]) : -1;
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
-        res->prefetch_hits = (long long)ho.prof[12];
         if (std::getenv("EK_KL_PROF")) {
             static const char* names[12] = {"select", "G1-key", "bar1", "G2a", "G2bc", "bar2", "G1-aux", "G1-sum",
                                             "n_stale", "n_late+tail", "G1-load", "G1-look"};

@@ -191,6 +191,37 @@ void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const dou
           double* vcol, double* apart, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
           hipEvent_t ev_stop = nullptr);
 
+// kernels_build.hip — the Laplacian rows built on the device from the pins
+struct LapBuild {
+    long long nets = 0, r0 = 0, r1 = 0;  // rows [r0, r1) of the global matrix
+    const int64_t* net_ptr = nullptr;
+    const int32_t* pins = nullptr;
+    int *icnt = nullptr, *rcnt = nullptr, *cur = nullptr;  // per row: incidences, raw entries, fill cursor
+    long long *ip = nullptr, *rp = nullptr;                // their exclusive scans (nr + 1)
+    int32_t* inc = nullptr;                                // (net, position in net) pairs, by row
+    int* scol = nullptr;                                   // raw entries of each row at rp[i]
+    double *sval = nullptr, *tval = nullptr;
+    int *ulen = nullptr, *len = nullptr;  // merged entries; final row length (+ the diagonal if absent)
+    double* diag = nullptr;
+    int* long_rows = nullptr;  // rows past the per-thread sort
+    int* counters = nullptr;   // [0] long rows, [1] rows too long for the LDS sort
+};
+// out[0..n] = exclusive scan of in[0..n) (out[n] = total); tiles: ceil(n/1024) scratch
+void exclusive_scan(hipStream_t s, const int* in, long long n, long long* out, long long* tiles);
+void lap_count(hipStream_t s, const LapBuild& b);
+void lap_fill_rows(hipStream_t s, const LapBuild& b);
+void lap_long_rows(hipStream_t s, const LapBuild& b, int n_long);
+void lap_write(hipStream_t s, const LapBuild& b, const long long* off, int* rowptr, int* col, double* val);
+// value dictionary: table[tsize] (power of two) of the distinct fp64 bit
+// patterns; code_of_slot[tsize] = the number of distinct values
+void dict_build(hipStream_t s, long long nnz, const double* val, unsigned long long* table, int tsize, int* overflow,
+                int* flags, long long* code_of_slot, long long* tiles);
+void dict_values(hipStream_t s, const unsigned long long* table, int tsize, const long long* code_of_slot,
+                 double* dict);
+void encode_segments(hipStream_t s, int nblocks, const int32_t* desc, const int* rowptr, const int* col,
+                     const double* val, const unsigned long long* table, int tsize, const long long* code_of_slot,
+                     int colbits, uint32_t* seg, uint16_t* rel);
+
 // kernels_lanczos.hip
 constexpr int GT_ROWS = 1024;  // rows per gemv-T block; ldv is a multiple of this
 constexpr int GT_COLS = 8;     // basis columns per gemv-T block (16: 18.9 vs 16.6 us, 204 VGPRs)

@@ -439,15 +439,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     float cut = *d.cut0, best = cut;  // loop-carried scalars: the W wave's lane 0 only
     long long best_it = 0, it = 0;
     unsigned term = 0;
-    // G1 waves: the rows of the speculated next pair (P), loaded during G2 /
-    // barrier (2) / selection; used when the selection confirms the pair
-    constexpr int LPR = SEGC ? 4 : 8, RPW = 64 / LPR;
-    constexpr int PPL = (SEGC ? KL_SEGC_PIECES : KL_SEG_LANES) / LPR;  // 16-B pieces per lane
-    int preA = -1, preB = -1;  // wave-uniform; -1: nothing prefetched
-    int4 pre_piece[PPL], pre_a = make_int4(0, 0, 0, 0);
-#pragma unroll
-    for (int r = 0; r < PPL; ++r) pre_piece[r] = make_int4(0, 0, 0, 0);
-    unsigned long long n_hit = 0;
     unsigned long long tph[12] = {}, tstamp = 0;  // diagnostic build only (PROF)
     const unsigned long long c_start = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long r_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -558,35 +549,29 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // ones (2 pieces each): 16 rows per wave, 48 per pass over the
             // three gain waves, so 0.1 % of the swaps (tot > 48) need a second
             // pass instead of 11 % (tot > 24) at ibm18 shape
+            constexpr int LPR = SEGC ? 4 : 8, RPW = 64 / LPR;
             int4* stage = sg_stage + wv * KL_STAGE_ROWS * KL_STAGE_ROW;  // this wave's rows x KL_SEG_LANES pieces (+1 pad)
-            const bool hit = A == preA && B == preB;  // wave-uniform: the speculated pair was selected
-            n_hit += hit ? 1u : 0u;
             for (int i0 = wv * RPW; i0 < tot; i0 += NG * RPW) {
                 // LPR lanes per row, each loading 16-B pieces j8, j8 + LPR, ... of
                 // the row's inline segment: each instruction touches each 128-B
                 // line once.  (One lane loading all pieces of a line issues them
                 // as separate instructions on the same line, and each waits for
                 // the previous one's miss: serial L2 trips.)
+                constexpr int PPL = (SEGC ? KL_SEGC_PIECES : KL_SEG_LANES) / LPR;  // pieces per lane
                 const int gi = i0 + lane / LPR, j8 = lane % LPR, srow = lane / LPR;
                 const int pg = gi < tot ? (gi < la ? pa + gi : pb + gi - la) : pa;
-                int4 piece[PPL], a;
-                if (hit && i0 == wv * RPW) {  // loaded during the previous swap's G2 (same rows: static data)
+                int4 piece[PPL];
+                if constexpr (SEGC) {  // pieces of 4 coded entries
 #pragma unroll
-                    for (int r = 0; r < PPL; ++r) piece[r] = pre_piece[r];
-                    a = pre_a;
+                    for (int r = 0; r < PPL; ++r)
+                        piece[r] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8 + LPR * r);
                 } else {
-                    if constexpr (SEGC) {  // pieces of 4 coded entries
 #pragma unroll
-                        for (int r = 0; r < PPL; ++r)
-                            piece[r] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8 + LPR * r);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < PPL; ++r)
-                            piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + LPR * r)
-                                             : make_int4(0, 0, 0, 0);
-                    }
-                    a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
+                    for (int r = 0; r < PPL; ++r)
+                        piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + LPR * r)
+                                         : make_int4(0, 0, 0, 0);
                 }
+                const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
                 if constexpr (PROF) {
                     if (tid == 0 && (piece[0].x == -12345 || a.x == -12345)) s_stop[2] = 0;  // waits for the loads
                 }
@@ -726,86 +711,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         stamp(1);
         __syncthreads();  // (1) gains, early rescans, merged keys and tags visible
         stamp(2);
-        // P. the G1 waves speculate the next selection from what barrier (1)
-        // published — every chunk's merged key (minus node1's / node2's
-        // chunks, whose keys G2a is resolving from the early rescans and the
-        // updated rows, done the same way here) — and start loading its rows
-        // now, so they arrive during G2, barrier (2) and the selection.  A
-        // wrong guess (a tagged chunk's fallen winner, a stale early rescan)
-        // only costs the loads: the next G1 compares the selected pair.
-        if (wv < NG) {
-            const int s = half, cS = s ? cB : cA, nck = s ? d.nck1 : d.nck0;
-            const u64* ckn = s ? ckn1 : ckn0;
-            u64 k = 0ull;
-            for (int c0 = hl; c0 < nck; c0 += 8 * 32) {
-                u64 kv[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int c = min(c0 + 32 * u, nck - 1);
-                    kv[u] = c == cS ? 0ull : ckn[c];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) k = kv[u] > k ? kv[u] : k;
-            }
-            const int ni = tot < KL_ITEM_CAP ? tot : KL_ITEM_CAP;
-            const uint32_t csS = (uint32_t(s) << 31) | uint32_t(cS);
-            for (int i = hl; i < ni; i += 32)
-                if (uint32_t(it_cs[i]) == csS && it_key[i] > k) k = it_key[i];
-            if (hl < E_PARTS && er_key[s * E_PARTS + hl] > k) k = er_key[s * E_PARTS + hl];
-            const u64 kw = half_max_u64(k);
-            // its row descriptor: an updated row's, an early rescan's, or the chunk winner's
-            const int cw = int(~uint32_t(kw & 0xffffffffull)) / KL_CHUNK;
-            bool found = false;
-            KLInfo f{-1, 0, 0, 0};
-            for (int i = hl; i < ni; i += 32)
-                if (kw != 0ull && it_key[i] == kw && (uint32_t(it_cs[i]) >> 31) == uint32_t(s)) {
-                    found = true;
-                    f = it_info[i];
-                }
-            const u64 fb = __ballot(found);
-            const u64 fb0 = fb & 0x00000000ffffffffull, fb1 = fb & 0xffffffff00000000ull;
-            const int l0 = fb0 ? __ffsll((long long)fb0) - 1 : 0, l1 = fb1 ? __ffsll((long long)fb1) - 1 : 32;
-            const KLInfo g0{__builtin_amdgcn_readlane(f.a, l0), __builtin_amdgcn_readlane(f.b, l0),
-                            __builtin_amdgcn_readlane(f.c, l0), 0};
-            const KLInfo g1{__builtin_amdgcn_readlane(f.a, l1), __builtin_amdgcn_readlane(f.b, l1),
-                            __builtin_amdgcn_readlane(f.c, l1), 0};
-            KLInfo w = s ? g1 : g0;
-            if (!(s ? fb1 : fb0)) {
-                if (cw == cS) {
-                    w = KLInfo{-1, 0, 0, 0};
-#pragma unroll
-                    for (int q = 0; q < E_PARTS; ++q)
-                        if (er_key[s * E_PARTS + q] == kw) w = er_info[s * E_PARTS + q];
-                } else {
-                    w = (s ? ci1 : ci0)[cw];
-                }
-            }
-            if (kw == 0ull) w = KLInfo{-1, 0, 0, 0};
-            const int nA = __builtin_amdgcn_readlane(w.a, 0), qa = __builtin_amdgcn_readlane(w.b, 0),
-                      ma = __builtin_amdgcn_readlane(w.c, 0);
-            const int nB = __builtin_amdgcn_readlane(w.a, 32), qb = __builtin_amdgcn_readlane(w.b, 32),
-                      mb = __builtin_amdgcn_readlane(w.c, 32);
-            const bool ok = nA >= 0 && nB >= 0 && qa >= 0 && qb >= 0 && ma >= 0 && mb >= 0 &&
-                            (long long)qa + ma <= d.nnz && (long long)qb + mb <= d.nnz;
-            preA = ok ? nA : -1;
-            preB = ok ? nB : -1;
-            const int tot2 = ma + mb;
-            if (ok && wv * RPW < tot2) {
-                const int gi = wv * RPW + lane / LPR, j8 = lane % LPR;
-                const int pg = gi < tot2 ? (gi < ma ? qa + gi : qb + gi - ma) : qa;
-                if constexpr (SEGC) {
-#pragma unroll
-                    for (int r = 0; r < PPL; ++r)
-                        pre_piece[r] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8 + LPR * r);
-                } else {
-#pragma unroll
-                    for (int r = 0; r < PPL; ++r)
-                        pre_piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + LPR * r)
-                                             : make_int4(0, 0, 0, 0);
-                }
-                pre_a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
-            }
-        }
         // G2a. node1's and node2's chunks: one wave (lanes 0-31 list 0, 32-63
         // list 1), beside G2b/G2c in the others
         if (wv == W_EA) {
@@ -883,18 +788,16 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             s_lock[B >> 5] |= 1u << (B & 31);
         }
         // G2b. publish merged keys of the other untagged chunks (every item of
-        // a chunk writes the same value) and the descriptor of the item that
-        // won: the second early-rescan wave (idle now; the gain waves speculate)
-        if (wv == W_EB)
-            for (int i = lane; i < tot && i < KL_ITEM_CAP; i += 64) {
-                const int cs = it_cs[i];
-                if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
-                const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
-                if ((s ? c == cB : c == cA) || (s ? dtag1 : dtag0)[c] == tag) continue;
-                const u64 kmerged = (s ? ckn1 : ckn0)[c];
-                (s ? ck1 : ck0)[c] = kmerged;
-                if (kmerged == it_key[i]) (s ? ci1 : ci0)[c] = it_info[i];
-            }
+        // a chunk writes the same value) and the descriptor of the item that won
+        for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
+            const int cs = it_cs[i];
+            if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
+            const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
+            if ((s ? c == cB : c == cA) || (s ? dtag1 : dtag0)[c] == tag) continue;
+            const u64 kmerged = (s ? ckn1 : ckn0)[c];
+            (s ? ck1 : ck0)[c] = kmerged;
+            if (kmerged == it_key[i]) (s ? ci1 : ci0)[c] = it_info[i];
+        }
         // G2c. full rescans of the tagged chunks (one wave each, claimed once);
         // s_stop[3] holds the last iteration that tagged any
         for (int i = wv; i < tot && s_stop[3] == tag; i += NW) {
@@ -934,7 +837,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     }
     __syncthreads();
     for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
-    if (wv == 0 && lane == 0) out->prof[12] = n_hit;  // swaps whose rows the speculation had loaded
     if (wv == W_W && lane == 0) {
         out->iterations = it;
         out->best_iter = best_it;

@@ -59,18 +59,16 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
                     std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
                     const std::function<void()>& after_laplacian, double* t_spmv_setup) {
     const int64_t n = h.nodes;
-    int64_t row0 = 0, nrows = n, nloc = n;
-    chk(ek_shard_rows(n, nranks, rank, &row0, &nrows, &nloc));
+    (void)rank;
+    (void)nranks;
     auto t = clk::now();
-    {
-        ek_csr L;
-        build_laplacian_rows(h, row0, row0 + nrows, L);  // this rank's rows only
-        if (t_laplacian) *t_laplacian = since(t);
-        if (after_laplacian) after_laplacian();
-        t = clk::now();
-        chk(ek_spmv_setup(ctx, n, row0, nrows, L.rowptr.data(), L.col.data(), L.val64.data()));
-        if (t_spmv_setup) *t_spmv_setup = since(t);
-    }
+    // this rank's rows, assembled on the GPU from the pins into the SpMV's
+    // coded form (the host build only as ek_spmv_setup_pins' fallback)
+    chk(ek_spmv_setup_pins(ctx, n, h.nets, h.net_ptr.data(), h.pins.data(), nullptr));
+    if (t_laplacian) *t_laplacian = since(t);
+    if (t_spmv_setup) *t_spmv_setup = 0.0;
+    if (after_laplacian) after_laplacian();
+    t = clk::now();
     v.assign(size_t(n), 0.0);
     chk(ek_lanczos_fiedler(ctx, &o.lanczos, &lambda, v.data(), &st));
     if (o.sign_ref && o.sign_ref[0]) {

@@ -137,6 +137,17 @@ int ek_comm_init_host(ek_ctx* ctx, int nranks, int rank, ek_allgather_fn allgath
  * are copied; the caller keeps ownership. */
 int ek_spmv_setup(ek_ctx* ctx, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr,
                   const int32_t* col, const double* val);
+/* The same rows built on the GPU straight from the hypergraph's pins (net e
+ * owns pins[net_ptr[e] .. net_ptr[e+1]), 0-based): the clique Laplacian of
+ * initializeMatrix (cEIG.cpp:86-133) assembled by device kernels into the
+ * SpMV's coded form, the rows of this context's shard only (ek_shard_rows).
+ * The values and the row blocks are the host build's (ek_laplacian_build),
+ * so every SpMV and Lanczos result is bit-identical to ek_spmv_setup on
+ * those rows.  Falls back to the host build for a row too long for the
+ * device sort (or with EK_HOST_LAPLACIAN set); *on_device (may be NULL)
+ * tells which ran. */
+int ek_spmv_setup_pins(ek_ctx* ctx, int64_t n, int64_t nets, const int64_t* net_ptr, const int32_t* pins,
+                       int32_t* on_device);
 /* The rows the context owns after the last ek_spmv_setup (any of the
  * pointers may be NULL). */
 int ek_spmv_dims(ek_ctx* ctx, int64_t* n, int64_t* row0, int64_t* nrows);
@@ -234,7 +245,6 @@ typedef struct {
     int64_t net_cut_initial, net_cut_best, net_cut_final; /* integer hyperedge cuts */
     double loop_ms;      /* device time of the swap loop */
     double total_ms;     /* device time of gain scan + loop + cuts */
-    int64_t prefetch_hits; /* swaps whose neighbour rows were loaded during the previous swap (speculation right) */
 } ek_kl_result;
 
 /* Upload the KL graph (from ek_kl_graph_build, or any rows in cKL order). */

@@ -31,6 +31,9 @@ void ek_lanczos_default_opts(ek_lanczos_opts* o) {
 int ek_spmv_setup(ek_ctx*, int64_t, int64_t, int64_t, const int32_t*, const int32_t*, const double*) {
     return absent("ek_spmv_setup");
 }
+int ek_spmv_setup_pins(ek_ctx*, int64_t, int64_t, const int64_t*, const int32_t*, int32_t*) {
+    return absent("ek_spmv_setup_pins");
+}
 int ek_lanczos_fiedler(ek_ctx*, const ek_lanczos_opts*, double*, double*, ek_lanczos_stats*) {
     return absent("ek_lanczos_fiedler");
 }
