@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libeigkl_hip.so")
+# EK_LIB_PATH: a design lab's A/B build of the same library (tools/ab_lab.sh)
+LIB_PATH = os.environ.get("EK_LIB_PATH") or os.path.join(HERE, "build", "libeigkl_hip.so")
 BIN_DIR = os.path.join(HERE, "build", "bin")
 
 if not os.path.exists(LIB_PATH):

@@ -13,6 +13,10 @@
 
 #include "ek_internal.hpp"
 
+#ifndef EK_UPD_UB
+#define EK_UPD_UB 8  // basis columns per load batch of the update (two batches in flight)
+#endif
+
 namespace ek {
 namespace dev {
 
@@ -42,7 +46,10 @@ __device__ __forceinline__ double strided_sum256(const double* __restrict__ x, i
     return s;
 }
 
-constexpr int TT_ROWS = 1024;  // rows per three-term block (ldv is a multiple of GT_ROWS = 1024)
+#ifndef EK_TT_ROWS
+#define EK_TT_ROWS 1024
+#endif
+constexpr int TT_ROWS = EK_TT_ROWS;  // rows per three-term block (ldv is a multiple of GT_ROWS = 1024)
 static_assert(GT_ROWS % TT_ROWS == 0, "ldv must be a multiple of TT_ROWS");
 
 // block of 256: returns the block sum in thread 0
@@ -107,43 +114,88 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
             }
         }
     }
+    // wave reduction of the 8 column sums as a reduce-scatter: each xor step
+    // halves the values a lane carries (10 shuffles instead of 8 x 6); lane L
+    // ends with column 4*b5 + 2*b4 + b3 (bits of L) summed over the wave
+    static_assert(GT_COLS == 8, "the reduce-scatter is written for 8 columns");
+    const int lane = t & 63;
+    double a4[4], a2[2];
+    {
+        const bool hi = lane & 32;
 #pragma unroll
-    for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = wave_sum(acc[jj]);
-    if ((t & 63) == 0) {
-#pragma unroll
-        for (int jj = 0; jj < GT_COLS; ++jj) red[t >> 6][jj] = acc[jj];
+        for (int k = 0; k < 4; ++k) a4[k] = (hi ? acc[k + 4] : acc[k]) + __shfl_xor(hi ? acc[k] : acc[k + 4], 32, 64);
     }
+    {
+        const bool hi = lane & 16;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) a2[k] = (hi ? a4[k + 2] : a4[k]) + __shfl_xor(hi ? a4[k] : a4[k + 2], 16, 64);
+    }
+    double a1;
+    {
+        const bool hi = lane & 8;
+        a1 = (hi ? a2[1] : a2[0]) + __shfl_xor(hi ? a2[0] : a2[1], 8, 64);
+    }
+    a1 += __shfl_xor(a1, 4, 64);
+    a1 += __shfl_xor(a1, 2, 64);
+    a1 += __shfl_xor(a1, 1, 64);
+    if ((lane & 7) == 0) red[t >> 6][((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = a1;
     __syncthreads();
     if (t < GT_COLS && j0 + t < ncols + has_u0)
         part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
 }
 
-// The canonical order of a column sum over the projection partials: lane
-// pair (2j, 2j+1) sums the even / odd blocks in order, then one add.  Used by
+// The canonical order of a column sum over the projection partials: 8 lanes
+// per column, lane l summing blocks l, l+8, l+16, ... in order, then a fixed
+// xor tree over the 8 lanes (every lane of the group gets the sum).  Used by
 // k_reduce_cols and by the fused update alike, so both give the same bits.
-// 32 loads in flight, then the adds in order.  The loads are unconditional
-// (clamped index) and so are the adds (0.0 past the end): a load behind a
-// branch waits for the loads before it.  s + 0.0 == s here because s starts
-// at +0 and a sum of these partials never becomes -0.0.
-__device__ __forceinline__ double col_sum(const double* __restrict__ pj, int nrb, int half) {
+// The loads are unconditional (clamped index) and so are the adds (0.0 past
+// the end): a load behind a branch waits for the loads before it.  s + 0.0
+// == s here because s starts at +0 and a sum of these partials never becomes
+// -0.0.  Two columns at a time, all their loads in flight together: one
+// round trip for up to 8 * CB row blocks (ibm18 shape: 198).  (Two lanes per
+// column, as before, took four dependent round trips and every update
+// workgroup ~7.5 us of its 20.)
+constexpr int CS_LANES = 8;
+__device__ __forceinline__ void col_sum2(const double* __restrict__ pa, const double* __restrict__ pb, int nrb, int l,
+                                         double* sa, double* sb) {
     constexpr int CB = 32;
-    double s = 0.0;
-    for (int b0 = half; b0 < nrb; b0 += 2 * CB) {
-        double v[CB];
+    double a = 0.0, b = 0.0;
+    for (int b0 = l; b0 < nrb; b0 += CS_LANES * CB) {
+        double va[CB], vb[CB];
 #pragma unroll
-        for (int u = 0; u < CB; ++u) v[u] = pj[min(b0 + 2 * u, nrb - 1)];
+        for (int u = 0; u < CB; ++u) {
+            const int i = min(b0 + CS_LANES * u, nrb - 1);
+            va[u] = pa[i];
+            vb[u] = pb[i];
+        }
 #pragma unroll
-        for (int u = 0; u < CB; ++u) s += b0 + 2 * u < nrb ? v[u] : 0.0;
+        for (int u = 0; u < CB; ++u) {
+            const bool live = b0 + CS_LANES * u < nrb;
+            a += live ? va[u] : 0.0;
+            b += live ? vb[u] : 0.0;
+        }
     }
-    return s + __shfl_xor(s, 1, 64);
+#pragma unroll
+    for (int o = 1; o < CS_LANES; o <<= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    *sa = a;
+    *sb = b;
 }
 
-// h[j] = sum_b part[j*nrb + b]; 128 columns per workgroup.
+// h[j] = sum_b part[j*nrb + b] for j < ncols (col_sum2 order): 64 columns
+// per workgroup, 8 lanes each, two columns per lane group.
 __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ part, int nrb, int ncols,
                                                      double* __restrict__ h) {
-    const int j = blockIdx.x * 128 + (threadIdx.x >> 1);
-    const double s = col_sum(part + size_t(j < ncols ? j : 0) * nrb, nrb, threadIdx.x & 1);
-    if (j < ncols && (threadIdx.x & 1) == 0) h[j] = s;
+    const int g = int(threadIdx.x) / CS_LANES, l = int(threadIdx.x) % CS_LANES;
+    const int ja = blockIdx.x * 64 + g, jb = ja + 32;
+    double sa, sb;
+    col_sum2(part + size_t(min(ja, ncols - 1)) * nrb, part + size_t(min(jb, ncols - 1)) * nrb, nrb, l, &sa, &sb);
+    if (l == 0) {
+        if (ja < ncols) h[ja] = sa;
+        if (jb < ncols) h[jb] = sb;
+    }
 }
 
 // dst = src - V[:, :ncols] h - u0 h[ncols]; 256 threads x 2 rows (double2).
@@ -156,55 +208,87 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
                                                 const double* __restrict__ src, double* __restrict__ dst,
                                                 double* __restrict__ npart, const double* __restrict__ part, int nrb,
                                                 double* __restrict__ h_out) {
-    __shared__ double hs[MAX_NCV + 2];
+    constexpr int UB = EK_UPD_UB;
+    // hc: the basis coefficients, zero past ncols (whole batches read it
+    // unconditionally); hu0: the deflation vector's
+    __shared__ double hc[MAX_NCV + 2 * UB];
+    __shared__ double hu0;
     __shared__ double lds4[4];
     const int tot = ncols + has_u0;
-    // Basis columns in batches of UB, double-buffered: batch b+1's loads are
-    // issued before batch b is used, and batch 0's (with src) before h is
-    // reduced, so the projection reduce and every batch overlap a round trip.
-    // Clamped column index and unconditional subtractions (a column past
-    // ncols is subtracted with coefficient 0): a load or a use behind a branch
-    // makes the load wait for the ones before it.  The subtractions keep their
-    // sequential order; x - v*0 == x for every x but -0.0, which these sums do
-    // not produce (a difference of equal values rounds to +0).
+    // Basis columns in batches of UB, two batches in flight: batch b+1's
+    // loads are issued before batch b is used, and batch 0's (with src)
+    // before h is reduced, so the projection reduce and every batch overlap a
+    // round trip.  Clamped column index and unconditional subtractions (a
+    // column past ncols is subtracted with coefficient 0): a load or a use
+    // behind a branch makes the load wait for the ones before it, and a
+    // branch splits the loop into blocks the scheduler hoists the next
+    // batch's loads across.  The subtractions keep their sequential order;
+    // x - v*0 == x for every x but -0.0, which these sums do not produce (a
+    // difference of equal values rounds to +0).
+    // The two buffers swap roles in a loop unrolled by two: with a register
+    // copy `cur = nxt` (which needs nxt's data) the compiler waited for the
+    // next batch at every trip (vmcnt(0) at the back edge), so only one batch
+    // was ever in flight: 20.3 us per step at ibm18 shape.
     // (One row per thread with 8-B loads in 512-thread blocks, twice the
     // waves: 28 vs 20 us per step.)
-    constexpr int UB = 8;  // 16: 21.5 vs 20.3 us
     const int jmax = ncols > 0 ? ncols - 1 : 0;
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
     auto load_batch = [&](double2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB; ++u) vb[u] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + u, jmax)) * ldv + r);
     };
-    double2 cur[UB], nxt[UB];
+    double2 ba[UB], bb[UB];
     double2 x = *reinterpret_cast<const double2*>(src + r);
-    load_batch(cur, 0);
+    load_batch(ba, 0);
+    load_batch(bb, UB);
+    auto put = [&](int j, double v) {
+        if (j < ncols) hc[j] = v;
+        else hu0 = v;
+    };
     if constexpr (RED) {
-        for (int j0 = 0; j0 < tot; j0 += 128) {
-            const int j = j0 + (threadIdx.x >> 1);
-            const double s = col_sum(part + size_t(j < tot ? j : 0) * nrb, nrb, threadIdx.x & 1);
-            if (j < tot && (threadIdx.x & 1) == 0) {
-                hs[j] = s;
-                if (blockIdx.x == 0) h_out[j] = s;
+        const int g = int(threadIdx.x) / CS_LANES, l = int(threadIdx.x) % CS_LANES;
+        for (int ja = g; ja < tot; ja += 64) {  // lane groups: uniform trip counts
+            const int jb = ja + 32;
+            double sa, sb;
+            col_sum2(part + size_t(ja) * nrb, part + size_t(min(jb, tot - 1)) * nrb, nrb, l, &sa, &sb);
+            if (l == 0) {
+                put(ja, sa);
+                if (blockIdx.x == 0) h_out[ja] = sa;
+                if (jb < tot) {
+                    put(jb, sb);
+                    if (blockIdx.x == 0) h_out[jb] = sb;
+                }
             }
         }
     } else {
-        for (int j = threadIdx.x; j < tot; j += 256) hs[j] = h[j];
+        for (int j = threadIdx.x; j < tot; j += 256) put(j, h[j]);
     }
+    for (int j = ncols + int(threadIdx.x); j < ncols + 2 * UB; j += 256) hc[j] = 0.0;
     __syncthreads();
-    for (int j0 = 0; j0 < ncols; j0 += UB) {
-        load_batch(nxt, j0 + UB);  // past the end: clamped re-reads of column jmax (cache hits)
+    auto consume = [&](const double2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
-            const double hj = j0 + u < ncols ? hs[min(j0 + u, jmax)] : 0.0;
-            x.x -= cur[u].x * hj;
-            x.y -= cur[u].y * hj;
+            const double hj = hc[j0 + u];
+            x.x -= vb[u].x * hj;
+            x.y -= vb[u].y * hj;
         }
-#pragma unroll
-        for (int u = 0; u < UB; ++u) cur[u] = nxt[u];
+    };
+    // past the end: clamped re-reads of column jmax (cache hits), coefficient 0
+    // (scheduling barriers keep each batch's loads ahead of the other's use:
+    // left alone the scheduler sank them below it)
+    // (both first batches were issued before the coefficients were reduced)
+    for (int j0 = 0; j0 < ncols; j0 += 2 * UB) {
+        consume(ba, j0);
+        __builtin_amdgcn_sched_barrier(0);
+        load_batch(ba, j0 + 2 * UB);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(bb, j0 + UB);
+        __builtin_amdgcn_sched_barrier(0);
+        load_batch(bb, j0 + 3 * UB);
+        __builtin_amdgcn_sched_barrier(0);
     }
     if (has_u0) {
-        const double c = u0val * hs[ncols];
+        const double c = u0val * hu0;
         if (r < size_t(nreal)) x.x -= c;
         if (r + 1 < size_t(nreal)) x.y -= c;
     }
@@ -305,12 +389,23 @@ __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restri
     double2 acc[TJ];
 #pragma unroll
     for (int jj = 0; jj < TJ; ++jj) acc[jj] = make_double2(0.0, 0.0);
-    for (int i = 0; i < m; ++i) {
-        const double2 v = *reinterpret_cast<const double2*>(V + size_t(i) * ldv + r);
+    // 8 basis rows' loads in flight per trip (clamped index, coefficient 0
+    // past the end; the sums keep their order)
+    constexpr int IB = 8;
+    for (int i0 = 0; i0 < m; i0 += IB) {
+        double2 v[IB];
 #pragma unroll
-        for (int jj = 0; jj < TJ; ++jj) {
-            acc[jj].x += v.x * qs[i][jj];
-            acc[jj].y += v.y * qs[i][jj];
+        for (int u = 0; u < IB; ++u) v[u] = *reinterpret_cast<const double2*>(V + size_t(min(i0 + u, m - 1)) * ldv + r);
+#pragma unroll
+        for (int u = 0; u < IB; ++u) {
+            const int i = min(i0 + u, m - 1);
+            const bool live = i0 + u < m;
+#pragma unroll
+            for (int jj = 0; jj < TJ; ++jj) {
+                const double q = live ? qs[i][jj] : 0.0;
+                acc[jj].x += v[u].x * q;
+                acc[jj].y += v[u].y * q;
+            }
         }
     }
 #pragma unroll
@@ -362,7 +457,7 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
 
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h) {
     if (ncols_total <= 0) return;
-    hipLaunchKernelGGL(k_reduce_cols, dim3((ncols_total + 127) / 128), dim3(256), 0, s, part, nrb, ncols_total, h);
+    hipLaunchKernelGGL(k_reduce_cols, dim3((ncols_total + 63) / 64), dim3(256), 0, s, part, nrb, ncols_total, h);
 }
 
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
