@@ -42,7 +42,7 @@ SWAP_DTYPE = np.dtype([("iter", "<u4"), ("node_left", "<u4"), ("node_right", "<u
 
 class LanczosOpts(ctypes.Structure):
     _fields_ = [("ncv", _I32), ("maxit", _I32), ("tol", ctypes.c_double), ("deflate", _I32),
-                ("time_spmv", _I32), ("reorth", _I32)]
+                ("time_spmv", _I32), ("reorth", _I32), ("check_every", _I32)]
 
 
 class LanczosStats(ctypes.Structure):
@@ -435,9 +435,11 @@ class Context:
         _chk(_lib.ek_spmv_bench(self._c, int(iters), 1 if fused else 0, ctypes.byref(us)), "spmv_bench")
         return us.value
 
-    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=1):
-        """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207)."""
-        o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0, int(reorth))
+    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=1, check_every=8):
+        """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207).  check_every: steps
+        between mid-cycle convergence tests after the first cycle (0: at cycle ends only, Spectra's schedule)."""
+        o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0, int(reorth),
+                        int(check_every))
         st = LanczosStats()
         lam = ctypes.c_double()
         v = np.empty(self.n, np.float64)
@@ -479,7 +481,7 @@ class Context:
         return log[: min(r.iterations, cap)], res
 
     def solve_file(self, path, eig=1, seed=0, write_results=True, out_dir=None, limit=-1, sign_ref=None, ncv=0,
-                   tol=1e-10, deflate=True, time_spmv=False, log_cap=0):
+                   tol=1e-10, deflate=True, time_spmv=False, log_cap=0, check_every=8):
         """The whole path, .hgr -> results/ (ek_solve_file).  eig: 1 GPU Fiedler split (gKL2 -EIG), 2 the
         pre_saved_EIG file (cKL -EIG), 0 random split with std::mt19937(seed).  Returns (result dict, swap log)."""
         o = SolveOpts()
@@ -487,7 +489,8 @@ class Context:
         o.eig, o.seed, o.write_results, o.limit = int(eig), int(seed) & 0xFFFFFFFF, 1 if write_results else 0, int(limit)
         o.out_dir = os.fsencode(out_dir) if out_dir else None
         o.sign_ref = os.fsencode(sign_ref) if sign_ref else None
-        o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, 1)
+        o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, 1,
+                                int(check_every))
         log = np.zeros(max(int(log_cap), 1), SWAP_DTYPE)
         r = SolveResult()
         _chk(_lib.ek_solve_file(self._c, os.fsencode(path), ctypes.byref(o), _p(log), int(log_cap), ctypes.byref(r)),

@@ -116,6 +116,11 @@ struct ek_ctx {
     std::vector<hipEvent_t> spmv_ev;   // SpMV timing events, created once per context
     double* pin = nullptr;             // pinned host staging (Ritz vector + residual rows)
     size_t pin_doubles = 0;
+    // mid-cycle convergence checks of the Lanczos driver: a copy stream, two
+    // pinned slots of {alpha, offd, fn2} and their events (created on first use)
+    hipStream_t cstream = nullptr;
+    hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
+    double* chk_pin = nullptr;
 };
 
 Uploader::Uploader(ek_ctx* ctx, hipStream_t st, size_t total) : c(ctx), s(st) {
@@ -279,6 +284,12 @@ void ek_destroy(ek_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (c->chk_done[i]) (void)hipEventDestroy(c->chk_done[i]);
+        if (c->chk_copied[i]) (void)hipEventDestroy(c->chk_copied[i]);
+    }
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->chk_pin) (void)hipHostFree(c->chk_pin);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->up) (void)hipHostFree(c->up);
@@ -692,13 +703,18 @@ void ek_lanczos_default_opts(ek_lanczos_opts* o) {
     o->deflate = 1;
     o->time_spmv = 0;
     o->reorth = 1;
+    o->check_every = 8;
 }
 
 }  // extern "C"
 
 namespace {
 
-// Spectra SymEigsBase::nev_adjusted
+// Spectra SymEigsBase::nev_adjusted (ARPACK dsaup2's count of converged
+// unwanted values).  "Converged" = |last component| < machine epsilon: with
+// the 10 x DBL_MIN bound (an exact-zero test) the restarts kept 50 vectors
+// and ibm10 took 11,006 matvecs instead of 1,201, the 1x synthetic 2,683
+// instead of 507 (tools/lanczos_trace.py)
 int nev_adjusted(int nev, int ncv, int nconv, const std::vector<double>& est) {
     const double eps = std::numeric_limits<double>::epsilon();
     int nev_new = nev;
@@ -745,17 +761,20 @@ struct Lanczos {
     // H(i,i) / H(i-1,i) take the projections as corrections (Spectra's
     // H += V^T f after its re-orthogonalisation).
     int reorth = 1;
-    void factorize(int k) {
+    int seg0 = 0;  // first step of the current run of steps (cycle start or injected vector)
+    // steps [k, kend) of a run that started at seg0 (the driver enqueues a
+    // cycle in chunks to check convergence between them)
+    void factorize(int k, int kend) {
         // EK_LANCZOS_UNFUSED: run the multi-rank step sequence on one GPU (tests)
         static const bool unfused = std::getenv("EK_LANCZOS_UNFUSED") != nullptr;
-        if (c->nranks == 1 && reorth == 1 && !unfused) return factorize_fused(k);
+        if (c->nranks == 1 && reorth == 1 && !unfused) return factorize_fused(k, kend);
         double* fn2 = c->fn2.as<double>();
-        for (int i = k; i < m; ++i) {
+        for (int i = k; i < kend; ++i) {
             const double* x = gather_f();
-            const bool timed = spmv_timed_step(i, k);
+            const bool timed = spmv_timed_step(i);
             ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
                           reorth == 1 ? c->apart.as<double>() : nullptr, nullptr,
-                          timed ? ev[size_t(2 * (i - k))] : nullptr, timed ? ev[size_t(2 * (i - k) + 1)] : nullptr);
+                          timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
             ++matvecs;
             const int nc = i + 1, tot = nc + has_u0;
             if (reorth == 1) {
@@ -803,14 +822,16 @@ struct Lanczos {
     // the projection partials itself (same column-sum order as k_reduce_cols,
     // so the fused and unfused paths give identical bits).  Folding the
     // three-term recurrence into the projection was measured slower: every
-    // column tile re-reads w, v_i and v_{i-1}.
-    void factorize_fused(int k) {
+    // column tile re-reads w, v_i and v_{i-1}.  Step i > seg0 finalizes step
+    // i - 1 in its SpMV, also across chunks; the last step of the cycle is
+    // finalized by its own launch.
+    void factorize_fused(int k, int kend) {
         double* fn2 = c->fn2.as<double>();
         double* a3 = c->scal.as<double>() + 2;
         const double* bov = c->bov.as<double>();
-        for (int i = k; i < m; ++i) {
+        for (int i = k; i < kend; ++i) {
             ek::dev::StepFin fin;
-            if (i > k) {
+            if (i > seg0) {
                 fin.npart = c->npart.as<double>();
                 fin.nb = nub;
                 fin.fn2_out = fn2 + i;
@@ -822,10 +843,10 @@ struct Lanczos {
                 fin.fn2_i = fn2 + i - 1;
                 fin.bov_i = bov + i - 1;
             }
-            const bool timed = spmv_timed_step(i, k);
+            const bool timed = spmv_timed_step(i);
             ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
-                          c->apart.as<double>(), i > k ? &fin : nullptr,
-                          timed ? ev[size_t(2 * (i - k))] : nullptr, timed ? ev[size_t(2 * (i - k) + 1)] : nullptr);
+                          c->apart.as<double>(), i > seg0 ? &fin : nullptr,
+                          timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
             ++matvecs;
             const int nc = i + 1;
             ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
@@ -834,8 +855,9 @@ struct Lanczos {
             ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
                               c->f.as<double>(), c->f.as<double>(), c->npart.as<double>());
         }
-        ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + m, nullptr, c->h2.as<double>(), m - 1,
-                               c->alpha.as<double>(), c->offd.as<double>(), a3, fn2 + m - 1, bov + m - 1);
+        if (kend == m)
+            ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + m, nullptr, c->h2.as<double>(), m - 1,
+                                   c->alpha.as<double>(), c->offd.as<double>(), a3, fn2 + m - 1, bov + m - 1);
         HIPCHK(hipGetLastError());
     }
 
@@ -865,23 +887,27 @@ struct Lanczos {
         HIPCHK(hipStreamSynchronize(s));                             // h is a host temporary
     }
 
+    // pinned slot i of the mid-cycle checks: alpha[m], offd[m], fn2[m]
+    double* chk_slot(int i) { return c->chk_pin + size_t(i) * 3 * size_t(ek::dev::MAX_NCV + 2); }
+
     // The SpMV's kernel timestamps are taken on every 4th step of a cycle: a
     // launch with timing events costs the host ~7 us more, which the timed
     // solve would otherwise carry on every step.  The sample starts at the
     // cycle's second step: the first SpMV after a restart (1 in 100 of the
     // launches) follows the V <- VQ stream and would be 1 in 25 of the sample.
     static constexpr int SPMV_SAMPLE = 4;
-    bool spmv_timed_step(int i, int k) const {
-        return time_spmv && (i - k) % SPMV_SAMPLE == 1 && size_t(2 * (i - k) + 1) < ev.size();
+    bool spmv_timed_step(int i) const {
+        return time_spmv && (i - seg0) % SPMV_SAMPLE == 1 && size_t(2 * (i - seg0) + 1) < ev.size();
     }
 
-    void collect_spmv_times(int k) {
+    // the timed SpMVs of steps [seg0, kend) (the steps launched in this run)
+    void collect_spmv_times(int kend) {
         if (!time_spmv) return;
         HIPCHK(hipStreamSynchronize(s));
-        for (int i = k; i < m && size_t(2 * (i - k) + 1) < ev.size(); ++i) {
-            if (!spmv_timed_step(i, k)) continue;
+        for (int i = seg0; i < kend && size_t(2 * (i - seg0) + 1) < ev.size(); ++i) {
+            if (!spmv_timed_step(i)) continue;
             float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, ev[size_t(2 * (i - k))], ev[size_t(2 * (i - k) + 1)]));
+            HIPCHK(hipEventElapsedTime(&ms, ev[size_t(2 * (i - seg0))], ev[size_t(2 * (i - seg0) + 1)]));
             spmv_ms += ms;
             ++spmv_timed;
         }
@@ -947,6 +973,15 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     HIPCHK(hipMemsetAsync(c->Vn.p, 0, c->Vn.bytes, s));
     HIPCHK(hipMemsetAsync(c->w.p, 0, c->w.bytes, s));
     if (c->nranks > 1) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
+    if (!c->cstream) {  // mid-cycle check resources, created once per context
+        HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(hipEventCreateWithFlags(&c->chk_done[i], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&c->chk_copied[i], hipEventDisableTiming));
+        }
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 3 * size_t(ek::dev::MAX_NCV + 2) * 8,
+                             hipHostMallocDefault));
+    }
     if (L.time_spmv) {  // created once per context: ~200 creations per solve cost milliseconds
         while (c->spmv_ev.size() < size_t(2 * m)) {
             hipEvent_t e;
@@ -977,6 +1012,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     int k = 0, restarts = 0, nconv = 0, injected = 0;
     double fn2_k = 1.0;  // ||f_k||^2 entering a cycle (after an implicit restart: the restart's residual)
     bool converged = false;
+    int mf = m;  // steps the returned Ritz pair is taken from (< m: converged at a mid-cycle check)
     const double beta_eps = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     double host_restart_ms = 0.0, device_cycle_ms = 0.0, host_qr_ms = 0.0;  // EK_LANCZOS_TRACE diagnostics
     auto anorm_of = [&] {
@@ -998,29 +1034,104 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             ++cycle_breakdowns;
             L.inject(k, ++injected);
         }
+        int jconv = -1;  // > 0: converged on the projected matrix of the first jconv steps (mid-cycle check)
         for (;;) {
-            L.factorize(from);
-            L.collect_spmv_times(from);
-            HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(offd_h.data(), c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(fn2_h.data(), c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            for (int i = from; i < m; ++i) {
-                d[size_t(i)] = alpha_h[size_t(i)];
-                if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
-            }
-            const double anorm = anorm_of();
-            int j1 = -1;
-            for (int i = std::max(from, 1); i < m; ++i)
-                if (!(std::sqrt(std::max(0.0, fn2_h[size_t(i)])) > beta_eps * anorm)) {
-                    j1 = i;
-                    break;
+            L.seg0 = from;
+            // After the first cycle the cycle is enqueued in chunks; the host
+            // tests the projected matrix of each chunk (its {alpha, offd,
+            // fn2} copied on a second stream into a pinned slot) while the GPU
+            // runs the next one: a converged Ritz pair stops the cycle there,
+            // a collapsed residual is injected without running the rest of
+            // the cycle on a zero vector.
+            // (about 0.5 ms of GPU work per chunk: the host's check of one
+            // chunk and its launches of the next must fit in the chunk the GPU
+            // is running.  The step time is modelled from n, not measured, so
+            // the stopping step and the result bits do not depend on timing:
+            // ~12 us + 0.23 ns per row, 15 us at ibm01, 58 us at ibm18 shape.)
+            const int chunk = (restarts > 0 && o.check_every > 0)
+                                  ? std::max({2, int(o.check_every), int(std::ceil(500.0 / (12.0 + 2.3e-4 * double(n))))})
+                                  : m;
+            int a = from, launched = from, j1 = -1;
+            int pend = -1, pend_slot = 0, slot = 0;
+            while (a < m) {
+                const int b = std::min(m, a + chunk);
+                L.factorize(a, b);
+                launched = b;
+                int cur = -1;
+                if (b < m) {
+                    double* pinned = L.chk_slot(slot);
+                    HIPCHK(hipEventRecord(c->chk_done[slot], s));
+                    HIPCHK(hipStreamWaitEvent(c->cstream, c->chk_done[slot], 0));
+                    HIPCHK(hipMemcpyAsync(pinned, c->alpha.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                    HIPCHK(hipMemcpyAsync(pinned + m, c->offd.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                    HIPCHK(hipMemcpyAsync(pinned + 2 * m, c->fn2.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                    HIPCHK(hipEventRecord(c->chk_copied[slot], c->cstream));
+                    cur = b - 1;  // complete: alpha, offd of steps < b - 1 (the fused finalize lags one step), fn2 <= b - 1
                 }
-            if (j1 < 0) break;
-            if (trace) std::fprintf(stderr, "[lanczos] breakdown at step %d (|f|^2=%.3e)\n", j1, fn2_h[size_t(j1)]);
+                if (pend >= 0) {  // the previous chunk's check, while this chunk runs
+                    HIPCHK(hipEventSynchronize(c->chk_copied[pend_slot]));
+                    const double* pa = L.chk_slot(pend_slot);
+                    const int j = pend;
+                    for (int i = from; i < j; ++i) {
+                        d[size_t(i)] = pa[i];
+                        if (i > 0) e[size_t(i - 1)] = pa[m + i];
+                    }
+                    double an = 1.0;
+                    for (int i = 0; i < j; ++i) an = std::max(an, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
+                    for (int i = std::max(from, 1); i <= j && j1 < 0; ++i)
+                        if (!(std::sqrt(std::max(0.0, pa[2 * m + i])) > beta_eps * an)) j1 = i;
+                    if (j1 >= 0) break;
+                    if (!ek::tridiag_eig(j, d.data(), e.data(), theta.data(), zl.data(), nullptr))
+                        ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
+                    const double fj = std::sqrt(std::max(0.0, pa[2 * m + j]));
+                    int nc = 0;
+                    for (int i = 0; i < nev && i < j; ++i)
+                        if (std::fabs(zl[size_t(i)]) * fj < tol * std::max(eps23, std::fabs(theta[size_t(i)]))) ++nc;
+                    if (trace)
+                        std::fprintf(stderr, "[lanczos]   check j=%d theta0=%.15g est0=%.3e\n", j, theta[0],
+                                     std::fabs(zl[0]) * fj);
+                    if (nc >= nev) {
+                        jconv = j;
+                        break;
+                    }
+                }
+                pend = cur;
+                pend_slot = slot;
+                slot ^= 1;
+                a = b;
+            }
+            L.collect_spmv_times(launched);
+            if (jconv > 0) break;
+            if (j1 < 0) {  // the whole cycle ran: its projected matrix and residuals
+                HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(offd_h.data(), c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(fn2_h.data(), c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                for (int i = from; i < m; ++i) {
+                    d[size_t(i)] = alpha_h[size_t(i)];
+                    if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
+                }
+                const double anorm = anorm_of();
+                for (int i = std::max(from, 1); i < m; ++i)
+                    if (!(std::sqrt(std::max(0.0, fn2_h[size_t(i)])) > beta_eps * anorm)) {
+                        j1 = i;
+                        break;
+                    }
+                if (j1 < 0) break;
+            } else {
+                HIPCHK(hipStreamSynchronize(s));  // the chunk launched beyond the breakdown
+            }
+            if (trace) std::fprintf(stderr, "[lanczos] breakdown at step %d\n", j1);
             if (++cycle_breakdowns > m) ek::fail(EK_ENOCONV, "Lanczos: repeated breakdown within one cycle");
             L.inject(j1, ++injected);
             from = j1;
+        }
+        if (jconv > 0) {
+            HIPCHK(hipStreamSynchronize(s));
+            device_cycle_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
+            converged = true;
+            mf = jconv;
+            break;
         }
         const auto th = std::chrono::steady_clock::now();
         device_cycle_ms += std::chrono::duration<double, std::milli>(th - tc).count();
@@ -1042,7 +1153,11 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         }
         if (++restarts >= maxit) break;
         // implicit restart with the m-knew unwanted Ritz values as shifts
+        // (a fixed restart size of 8, 12 or 20 kept vectors, or a cap of 10-30,
+        // was no better over ibm01 / industry2 / ibm10 / the 1x synthetic and
+        // its largest component, and some sizes lost 3-12x on one of them)
         const int knew = nev_adjusted(nev, m, nconv, zl);
+        if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
         std::vector<double> Q(size_t(m) * m, 0.0), dd(d), ee(e);
         for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
         const auto tq0 = std::chrono::steady_clock::now();
@@ -1073,12 +1188,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                  nev, restarts);
     // Ritz vector of the wanted value (ascending: [0] is the null pair unless deflated)
     const int want = deflate ? 0 : 1;
-    std::vector<double> Z(size_t(m) * m);
-    ek::tridiag_eig(m, d.data(), e.data(), theta.data(), zl.data(), Z.data());
+    std::vector<double> Z(size_t(mf) * mf);
+    ek::tridiag_eig(mf, d.data(), e.data(), theta.data(), zl.data(), Z.data());
     const double lambda = theta[size_t(want)];
-    HIPCHK(hipMemcpyAsync(c->Qd.p, Z.data() + size_t(want) * m, size_t(m) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->Qd.p, Z.data() + size_t(want) * mf, size_t(mf) * 8, hipMemcpyHostToDevice, s));
     double* xloc = c->Vn.as<double>();
-    ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), 1, xloc);
+    ek::dev::gemm_vq(s, L.ldv, L.V(), mf, c->Qd.as<double>(), 1, xloc);
     // full vector on every rank; copied out through pinned staging kept by the
     // context (pageable copies of these 2 x 8n bytes cost ~0.5 ms a solve)
     const size_t need = size_t(n) + size_t(std::max<int64_t>(c->nrows, 1));

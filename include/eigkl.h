@@ -190,6 +190,10 @@ typedef struct {
     int32_t time_spmv;  /* 1: bracket every SpMV launch with HIP events (stats) */
     int32_t reorth;     /* 1 (default): three-term recurrence + one full classical
                            Gram-Schmidt pass; 2: CGS2 (twice) from the matvec */
+    int32_t check_every; /* after the first restart cycle, test Spectra's convergence
+                            criterion on the projected matrix every this many steps
+                            (and stop there) instead of at cycle ends only; 0: cycle
+                            ends only (Spectra's schedule).  Default 8. */
 } ek_lanczos_opts;
 
 typedef struct {

@@ -3,7 +3,7 @@ solve on the 1x seed-1 synthetic (and its largest connected component) a few
 times with the library named by EK_LIB_PATH (default: the in-tree build) and
 prints the device time per solve, the matvec count and a hash of the result
 bits, so builds that must be bit-identical can be compared run to run.
-Usage: EK_LIB_PATH=... python tools/lanczos_ab.py [reps]"""
+Usage: EK_LIB_PATH=... python tools/lanczos_ab.py [reps] [check_every]"""
 import hashlib
 import importlib.util
 import os
@@ -15,6 +15,7 @@ spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "e
 ek = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(ek)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+check_every = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 print(f"lib {ek.LIB_PATH}", flush=True)
 h1 = ek.Hypergraph.generate(1.0, 1)
 hl, _ = h1.largest_component()
@@ -25,7 +26,7 @@ for name, h in (("syn1", h1), ("syn1_lcc", hl)):
     ms = []
     for i in range(reps):
         t0 = time.time()
-        lam, v, st = ctx.lanczos_fiedler()
+        lam, v, st = ctx.lanczos_fiedler(check_every=check_every)
         ms.append((time.time() - t0) * 1e3)
     dig = hashlib.md5(v.tobytes()).hexdigest()[:12]
     print(f"{name}: wall ms {' '.join(f'{x:.2f}' for x in ms)}; device {st['total_ms']:.2f} ms, "
