@@ -83,6 +83,10 @@ inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::d
 struct ek_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // the KL graph's setup (ek_kl_graph_setup / ek_kl_nets_setup) runs on its
+    // own stream: ek_solve_file calls it from its host thread while the
+    // Lanczos solve occupies `stream`
+    hipStream_t kstream = nullptr;
     // RCCL, or the host-staged exchange of ek_comm_init_host
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -273,6 +277,7 @@ int ek_init(int device, ek_ctx** out) {
     c->device = device;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
     *out = c.release();
     return EK_OK;
     EK_CATCH
@@ -293,6 +298,8 @@ void ek_destroy(ek_ctx* c) {
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->up) (void)hipHostFree(c->up);
+    (void)hipStreamSynchronize(c->kstream);
+    (void)hipStreamDestroy(c->kstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1267,7 +1274,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
         if (rowptr[r + 1] < rowptr[r]) ek::fail(EK_EINVAL, "ek_kl_graph_setup: rowptr not monotone");
     for (int64_t p = 0; p < nnz; ++p)
         if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_kl_graph_setup: column out of range");
-    hipStream_t s = c->stream;
+    hipStream_t s = c->kstream;
     c->kl_n = n;
     c->kl_rowptr_h.assign(rowptr, rowptr + n + 1);
     Uploader up(c, s, (size_t(n) + 1) * 4 + size_t(nnz) * 8 + size_t(nnz) * 4);
@@ -1337,10 +1344,10 @@ int ek_kl_nets_setup(ek_ctx* c, int64_t nets, const int64_t* net_ptr, const int3
     check_ctx(c);
     if (nets < 0 || !net_ptr || (net_ptr[nets] > 0 && !pins)) ek::fail(EK_EINVAL, "ek_kl_nets_setup: bad argument");
     c->kl_nets = nets;
-    Uploader up(c, c->stream, (size_t(nets) + 1) * 8 + size_t(net_ptr[nets]) * 4);
+    Uploader up(c, c->kstream, (size_t(nets) + 1) * 8 + size_t(net_ptr[nets]) * 4);
     up.put(c->kl_netptr, net_ptr, size_t(nets) + 1);
     up.put(c->kl_pins, pins, size_t(net_ptr[nets]));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->kstream));
     return EK_OK;
     EK_CATCH
 }

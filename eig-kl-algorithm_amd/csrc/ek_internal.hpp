@@ -223,7 +223,10 @@ void encode_segments(hipStream_t s, int nblocks, const int32_t* desc, const int*
                      int colbits, uint32_t* seg, uint16_t* rel);
 
 // kernels_lanczos.hip
-constexpr int GT_ROWS = 1024;  // rows per gemv-T block; ldv is a multiple of this
+#ifndef EK_GT_ROWS
+#define EK_GT_ROWS 1024
+#endif
+constexpr int GT_ROWS = EK_GT_ROWS;  // rows per gemv-T block; ldv is a multiple of this
 constexpr int GT_COLS = 8;     // basis columns per gemv-T block (16: 18.9 vs 16.6 us, 204 VGPRs)
 constexpr int UPD_ROWS = 512;  // rows per update block
 constexpr int MAX_NCV = 128;

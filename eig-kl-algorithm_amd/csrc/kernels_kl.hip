@@ -788,19 +788,25 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             s_lock[B >> 5] |= 1u << (B & 31);
         }
         // G2b. publish merged keys of the other untagged chunks (every item of
-        // a chunk writes the same value) and the descriptor of the item that won
+        // a chunk writes the same value) and the descriptor of the item that
+        // won.  Two dependent LDS round trips: the item's chunk, key and
+        // descriptor together, then the merged key (the tag of its chunk is
+        // read only in a swap that tagged any: s_stop[3] holds the last
+        // iteration that did).
+        const bool any_tag = s_stop[3] == tag;
         for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
             const int cs = it_cs[i];
+            const u64 kn = it_key[i];
+            const KLInfo inf = it_info[i];
             if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
             const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
-            if ((s ? c == cB : c == cA) || (s ? dtag1 : dtag0)[c] == tag) continue;
+            if ((s ? c == cB : c == cA) || (any_tag && (s ? dtag1 : dtag0)[c] == tag)) continue;
             const u64 kmerged = (s ? ckn1 : ckn0)[c];
             (s ? ck1 : ck0)[c] = kmerged;
-            if (kmerged == it_key[i]) (s ? ci1 : ci0)[c] = it_info[i];
+            if (kmerged == kn) (s ? ci1 : ci0)[c] = inf;
         }
-        // G2c. full rescans of the tagged chunks (one wave each, claimed once);
-        // s_stop[3] holds the last iteration that tagged any
-        for (int i = wv; i < tot && s_stop[3] == tag; i += NW) {
+        // G2c. full rescans of the tagged chunks (one wave each, claimed once)
+        for (int i = wv; any_tag && i < tot; i += NW) {
             int cs;
             if (i < KL_ITEM_CAP) cs = it_cs[i];
             else {  // beyond the LDS item list (hubs): rederive
@@ -855,6 +861,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         out->prof[15] = PROF ? __builtin_amdgcn_s_memrealtime() - r_start : 0ull;
     }
 }
+
 
 // The swap loop with its state in global memory: the fallback for graphs
 // whose bitmaps and chunk tables do not fit in LDS (and the A/B reference,

@@ -31,7 +31,15 @@ struct KLHost {
     dvec<float> w;
 };
 
-KLHost kl_graph_host(const ek_hgr* h, int threads) {
+void chk(int rc) {
+    if (rc != EK_OK) throw Error{rc};  // ek_last_error() already holds the message
+}
+
+// The KL adjacency (cKL.cpp:84-149, hash-order emulation) built on host
+// threads, then uploaded with the nets (the device-side inline segments and
+// weight codes included) on the context's KL stream: all of it while the GPU
+// runs the Lanczos solve on the main stream.
+KLHost kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
     ThreadCap cap(threads);
     ek_csr G;
     build_kl_graph(*h, G);
@@ -39,11 +47,9 @@ KLHost kl_graph_host(const ek_hgr* h, int threads) {
     g.rowptr.swap(G.rowptr);
     g.col.swap(G.col);
     g.w.swap(G.val32);
+    chk(ek_kl_graph_setup(ctx, h->nodes, g.rowptr.data(), g.col.data(), g.w.data()));
+    chk(ek_kl_nets_setup(ctx, h->nets, h->net_ptr.data(), h->pins.data()));
     return g;
-}
-
-void chk(int rc) {
-    if (rc != EK_OK) throw Error{rc};  // ek_last_error() already holds the message
 }
 
 std::string join(const char* dir, const std::string& rel) {
@@ -94,7 +100,8 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     // (and the HIP runtime's) a few cores
     auto start_kl_graph = [&] {
         if (rank == 0)
-            kg = std::async(std::launch::async, kl_graph_host, &h, o.eig == 1 ? std::max(1, host_threads() - 4) : 0);
+            kg = std::async(std::launch::async, kl_graph_host, get_ctx(), &h,
+                            o.eig == 1 ? std::max(1, host_threads() - 4) : 0);
     };
     if (o.eig == 1) {
         std::vector<double> v;
@@ -139,11 +146,9 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     }
     ek_ctx* ctx = get_ctx();
     auto t = clk::now();
-    const KLHost g = kg.get();
+    const KLHost g = kg.get();  // graph and nets set up on the context (KL stream, synchronised)
     r.t_kl_graph_wait = since(t);
     t = clk::now();
-    chk(ek_kl_graph_setup(ctx, n, g.rowptr.data(), g.col.data(), g.w.data()));
-    chk(ek_kl_nets_setup(ctx, h.nets, h.net_ptr.data(), h.pins.data()));
     chk(ek_kl_set_partition(ctx, order0.data(), int64_t(order0.size()), order1.data(), int64_t(order1.size())));
     r.t_kl_setup = since(t);
     t = clk::now();
