@@ -125,7 +125,6 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
             r.t_total = since(t0);
             return;
         }
-        start_kl_graph();
         const auto t = clk::now();
         if (o.eig == 2) {  // cKL -EIG: pre_saved_EIG/<base>_out.txt (cKL.cpp:442, 155-174)
             const std::string eig_file = join(o.out_dir, "pre_saved_EIG/" + base + "_out.txt");
@@ -143,6 +142,8 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
             chk(ek_random_split(n, o.seed, order0.data(), order1.data()));
         }
         r.t_split = since(t);
+        // (after the split: a missing EIG file fails before the GPU is touched)
+        start_kl_graph();
     }
     ek_ctx* ctx = get_ctx();
     auto t = clk::now();
