@@ -194,11 +194,11 @@ def main():
     barrier()
     ctx.synchronize()
     t0 = time.time()
-    results, walls = [], []
+    results, step_walls = [], []
     for _ in range(args.steps):
         ts = time.time()
         results.append(step(time_spmv=True))
-        walls.append(time.time() - ts)
+        step_walls.append(time.time() - ts)
     ctx.synchronize()
     barrier()
     elapsed = max_over_ranks(time.time() - t0)
@@ -432,7 +432,7 @@ def main():
                    "initial_cut": last["kl"]["initial_cut"], "best_cut": last["kl"]["best_cut"],
                    "net_cut_best": last["kl"]["net_cut_best"], "net_cut_final": last["kl"]["net_cut_final"],
                    "best_iter": last["kl"]["best_iter"], "phases_median_s": phases,
-                   "step_walls_s": [round(w, 4) for w in walls],
+                   "step_walls_s": [round(w, 4) for w in step_walls],
                    "step_totals_s": [round(r[0]["t_total"], 4) for r in results],
                    "comm_ms_per_step": round(comm_ms, 3), "spmv_us_max_rank": round(spmv_us_max, 3),
                    "resident_solve": resident},

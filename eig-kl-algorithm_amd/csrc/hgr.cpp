@@ -42,15 +42,16 @@ inline bool parse_line(const char* p, const char* end, Emit&& emit) {
     return true;
 }
 
-std::string slurp(const char* path) {
+// the whole file (not zero-filled first: dvec leaves its elements uninitialised)
+ek::dvec<char> slurp(const char* path) {
     FILE* f = std::fopen(path, "rb");
     if (!f) ek::fail(EK_EIO, "cannot open %s: %s", path, std::strerror(errno));
-    std::string buf;
+    ek::dvec<char> buf;
     std::fseek(f, 0, SEEK_END);
     const long sz = std::ftell(f);
     std::fseek(f, 0, SEEK_SET);
     buf.resize(size_t(sz > 0 ? sz : 0));
-    const size_t got = sz > 0 ? std::fread(&buf[0], 1, size_t(sz), f) : 0;
+    const size_t got = sz > 0 ? std::fread(buf.data(), 1, size_t(sz), f) : 0;
     std::fclose(f);
     buf.resize(got);
     return buf;
@@ -103,8 +104,10 @@ extern "C" {
 int ek_hgr_read(const char* path, ek_hgr** out) {
     EK_TRY
     if (!path || !out) ek::fail(EK_EINVAL, "ek_hgr_read: null argument");
-    const std::string buf = slurp(path);
-    const char* b = buf.data();
+    ek::PhaseTimer pt("hgr_read");
+    const ek::dvec<char> buf = slurp(path);
+    pt.mark("slurp");
+    const char* b = buf.empty() ? "" : buf.data();  // (memchr must not see a null pointer)
     const char* e = b + buf.size();
     const char* nl = static_cast<const char*>(std::memchr(b, '\n', size_t(e - b)));
     const char* hend = nl ? nl : e;
@@ -119,49 +122,72 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     h->nets = int64_t(hv[0]);
     h->nodes = int64_t(hv[1]);
     if (h->nodes > INT32_MAX || h->nets > INT32_MAX) ek::fail(EK_EINVAL, "%s: sizes exceed int32", path);
-    // line starts of the next `nets` lines
-    std::vector<const char*> ls(size_t(h->nets) + 1, e);
-    const char* p = nl ? nl + 1 : e;
-    for (int64_t i = 0; i < h->nets; ++i) {
-        ls[size_t(i)] = p;
-        if (p >= e) {  // getline failure: empty net
-            continue;
+    const int64_t nets = h->nets;
+    // One parallel pass over whole-line byte chunks: each thread counts its
+    // lines (so it knows the net index of its first one), then parses them
+    // into its own pin list; the lists are concatenated in net order.  Lines
+    // past `nets` are ignored; nets past the last line are empty (getline
+    // failure).
+    const char* body = nl ? nl + 1 : e;
+    const int64_t bytes = int64_t(e - body);
+    const int T = int(std::max<int64_t>(1, std::min<int64_t>(ek::host_threads(), bytes / (256 * 1024))));
+    std::vector<const char*> cs(size_t(T) + 1, e);
+    cs[0] = body;
+    for (int t = 1; t < T; ++t) {  // chunk starts at line starts
+        const char* q = body + bytes * t / T;
+        if (q > cs[size_t(t) - 1]) {
+            const char* r = static_cast<const char*>(std::memchr(q - 1, '\n', size_t(e - (q - 1))));
+            q = r ? r + 1 : e;
         }
-        const char* q = static_cast<const char*>(std::memchr(p, '\n', size_t(e - p)));
-        p = q ? q + 1 : e;
+        cs[size_t(t)] = std::max(q, cs[size_t(t) - 1]);
     }
-    auto line_end = [&](int64_t i) {
-        const char* s = ls[size_t(i)];
-        if (s >= e) return e;
-        const char* q = static_cast<const char*>(std::memchr(s, '\n', size_t(e - s)));
-        return q ? q : e;
-    };
-    std::vector<int64_t> cnt(size_t(h->nets) + 1, 0);
+    std::vector<int64_t> lines(size_t(T) + 1, 0);  // lines starting in chunk t
+    ek::run_threads(T, [&](int t) {
+        int64_t c = 0;
+        for (const char* p = cs[size_t(t)]; p < cs[size_t(t) + 1];) {
+            const char* r = static_cast<const char*>(std::memchr(p, '\n', size_t(cs[size_t(t) + 1] - p)));
+            ++c;
+            p = r ? r + 1 : cs[size_t(t) + 1];
+        }
+        lines[size_t(t) + 1] = c;
+    });
+    for (int t = 0; t < T; ++t) lines[size_t(t) + 1] += lines[size_t(t)];
+    pt.mark("lines");
+    h->net_ptr.assign(size_t(nets) + 1, 0);
+    std::vector<ek::dvec<int32_t>> part(static_cast<size_t>(T));
     std::atomic<bool> bad{false};
-    ek::parallel_for(h->nets, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi; ++i) {
-            int64_t c = 0;
-            if (!parse_line(ls[size_t(i)], line_end(i), [&](uint64_t) { ++c; })) bad = true;
-            cnt[size_t(i) + 1] = c;
+    std::atomic<int64_t> bad_pin{-1};
+    ek::run_threads(T, [&](int t) {
+        int64_t net = lines[size_t(t)];
+        auto& pv = part[size_t(t)];
+        pv.reserve(size_t((cs[size_t(t) + 1] - cs[size_t(t)]) / 2 + 16));
+        const int64_t nodes = h->nodes;
+        for (const char* p = cs[size_t(t)]; p < cs[size_t(t) + 1] && net < nets; ++net) {
+            const char* r = static_cast<const char*>(std::memchr(p, '\n', size_t(cs[size_t(t) + 1] - p)));
+            const char* le = r ? r : cs[size_t(t) + 1];
+            const size_t before = pv.size();
+            if (!parse_line(p, le, [&](uint64_t v) {
+                    if (v < 1 || int64_t(v) > nodes) bad_pin = int64_t(v);
+                    pv.push_back(int32_t(v) - 1);
+                }))
+                bad = true;
+            h->net_ptr[size_t(net) + 1] = int64_t(pv.size() - before);
+            p = r ? r + 1 : cs[size_t(t) + 1];
         }
     });
     if (bad) ek::fail(EK_EINVAL, "%s: pin id overflows uint32", path);
-    h->net_ptr.assign(size_t(h->nets) + 1, 0);
-    for (int64_t i = 0; i < h->nets; ++i) h->net_ptr[size_t(i) + 1] = h->net_ptr[size_t(i)] + cnt[size_t(i) + 1];
-    h->pins.resize(size_t(h->net_ptr.back()));
-    std::atomic<int64_t> bad_pin{-1};
-    ek::parallel_for(h->nets, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi; ++i) {
-            int64_t q = h->net_ptr[size_t(i)];
-            parse_line(ls[size_t(i)], line_end(i), [&](uint64_t v) {
-                if (v < 1 || int64_t(v) > h->nodes) bad_pin = int64_t(v);
-                h->pins[size_t(q++)] = int32_t(v) - 1;
-            });
-        }
-    });
     if (bad_pin.load() >= 0)
         ek::fail(EK_EINVAL, "%s: pin id %lld outside [1, %lld]", path, (long long)bad_pin.load(),
                  (long long)h->nodes);
+    for (int64_t i = 0; i < nets; ++i) h->net_ptr[size_t(i) + 1] += h->net_ptr[size_t(i)];
+    h->pins.resize(size_t(h->net_ptr.back()));
+    std::vector<size_t> off(size_t(T) + 1, 0);
+    for (int t = 0; t < T; ++t) off[size_t(t) + 1] = off[size_t(t)] + part[size_t(t)].size();
+    ek::run_threads(T, [&](int t) {
+        if (!part[size_t(t)].empty())
+            std::memcpy(h->pins.data() + off[size_t(t)], part[size_t(t)].data(), part[size_t(t)].size() * 4);
+    });
+    pt.mark("parse");
     *out = h.release();
     return EK_OK;
     EK_CATCH

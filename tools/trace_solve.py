@@ -1,0 +1,22 @@
+"""Lab (not shipped): EK_TRACE phase marks of a few in-process solves of the
+1x synthetic written to a .hgr (bench.py's step).  usage:
+EK_TRACE=1 python tools/trace_solve.py [reps]"""
+import importlib.util
+import os
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
+ek = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(ek)
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+w = tempfile.mkdtemp()
+p = os.path.join(w, "syn1.hgr")
+ek.Hypergraph.generate(1.0, 1).write(p)
+ctx = ek.Context(0)
+for i in range(reps):
+    print(f"=== step {i}", file=sys.stderr, flush=True)
+    r, _ = ctx.solve_file(p, eig=1, out_dir=w)
+    print("=== " + " ".join(f"{k} {1e3 * r[k]:.2f}" for k in r if k.startswith("t_")), file=sys.stderr, flush=True)
+ctx.close()
