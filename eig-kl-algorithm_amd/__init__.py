@@ -491,7 +491,7 @@ class Context:
         o.sign_ref = os.fsencode(sign_ref) if sign_ref else None
         o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, 1,
                                 int(check_every))
-        log = np.zeros(max(int(log_cap), 1), SWAP_DTYPE)
+        log = np.empty(max(int(log_cap), 1), SWAP_DTYPE)  # the library writes the first `iterations` records
         r = SolveResult()
         _chk(_lib.ek_solve_file(self._c, os.fsencode(path), ctypes.byref(o), _p(log), int(log_cap), ctypes.byref(r)),
              f"solve_file {path}")

@@ -1,6 +1,9 @@
 // Error plumbing and host-thread sizing for libeigkl_hip.so.
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <exception>
 #include <new>
@@ -80,6 +83,69 @@ int host_threads() {
         return int(std::min(16u, std::max(1u, hw)));
     }();
     return g_thread_cap > 0 ? std::max(1, std::min(cached, g_thread_cap)) : cached;
+}
+
+// The host worker pool behind run_threads / parallel_for: workers are
+// created once and woken per parallel region (spawning 16 threads per region
+// cost ~0.3 ms, several times per solve).  One caller at a time; a second
+// concurrent caller (the KL graph thread beside the solve's thread) gets
+// spawned threads.  Workers run with exceptions unhandled, as std::thread's.
+namespace {
+struct Pool {
+    std::mutex run_mu;  // held by the caller of the current region
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<std::thread> th;
+    unsigned long long epoch = 0;
+    int active = 0, pending = 0;
+    void (*fn)(void*, int) = nullptr;
+    void* ctx = nullptr;
+    void loop(int w) {
+        unsigned long long seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return epoch != seen; });
+            seen = epoch;
+            if (w >= active) continue;
+            auto f = fn;
+            void* c = ctx;
+            lk.unlock();
+            f(c, w);
+            lk.lock();
+            if (--pending == 0) done_cv.notify_one();
+        }
+    }
+};
+}  // namespace
+
+void pool_run(int T, void (*fn)(void*, int), void* ctx) {
+    static Pool* P = new Pool;  // never destroyed: workers stay blocked until the process exits
+    std::unique_lock<std::mutex> rl(P->run_mu, std::try_to_lock);
+    if (!rl.owns_lock()) {
+        std::vector<std::thread> th;
+        th.reserve(size_t(T - 1));
+        for (int t = 1; t < T; ++t) th.emplace_back([fn, ctx, t] { fn(ctx, t); });
+        fn(ctx, 0);
+        for (auto& x : th) x.join();
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(P->mu);
+        while (int(P->th.size()) < T - 1) {
+            const int w = int(P->th.size()) + 1;
+            P->th.emplace_back([w] { P->loop(w); });
+            P->th.back().detach();
+        }
+        P->fn = fn;
+        P->ctx = ctx;
+        P->active = T;
+        P->pending = T - 1;
+        ++P->epoch;
+    }
+    P->cv.notify_all();
+    fn(ctx, 0);
+    std::unique_lock<std::mutex> lk(P->mu);
+    P->done_cv.wait(lk, [&] { return P->pending == 0; });
 }
 
 }  // namespace ek

@@ -125,6 +125,7 @@ struct ek_ctx {
     hipStream_t cstream = nullptr;
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
     double* chk_pin = nullptr;
+    double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1))
 };
 
 Uploader::Uploader(ek_ctx* ctx, hipStream_t st, size_t total) : c(ctx), s(st) {
@@ -295,6 +296,7 @@ void ek_destroy(ek_ctx* c) {
     }
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
+    if (c->q_pin) (void)hipHostFree(c->q_pin);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->up) (void)hipHostFree(c->up);
@@ -988,6 +990,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         }
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 3 * size_t(ek::dev::MAX_NCV + 2) * 8,
                              hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
+                             size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) * 8, hipHostMallocDefault));
     }
     if (L.time_spmv) {  // created once per context: ~200 creations per solve cost milliseconds
         while (c->spmv_ev.size() < size_t(2 * m)) {
@@ -1109,11 +1113,16 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             }
             L.collect_spmv_times(launched);
             if (jconv > 0) break;
-            if (j1 < 0) {  // the whole cycle ran: its projected matrix and residuals
-                HIPCHK(hipMemcpyAsync(alpha_h.data(), c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(offd_h.data(), c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(fn2_h.data(), c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
+            if (j1 < 0) {  // the whole cycle ran: its projected matrix and residuals (pinned slot 0:
+                           // no check copy is in flight at the cycle's end)
+                double* pin0 = L.chk_slot(0);
+                HIPCHK(hipMemcpyAsync(pin0, c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(pin0 + m, c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(pin0 + 2 * m, c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
+                std::copy(pin0, pin0 + m, alpha_h.begin());
+                std::copy(pin0 + m, pin0 + 2 * m, offd_h.begin());
+                std::copy(pin0 + 2 * m, pin0 + 3 * m + 1, fn2_h.begin());
                 for (int i = from; i < m; ++i) {
                     d[size_t(i)] = alpha_h[size_t(i)];
                     if (i > 0) e[size_t(i - 1)] = offd_h[size_t(i)];
@@ -1165,15 +1174,17 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // its largest component, and some sizes lost 3-12x on one of them)
         const int knew = nev_adjusted(nev, m, nconv, zl);
         if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
-        std::vector<double> Q(size_t(m) * m, 0.0), dd(d), ee(e);
+        double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
+        std::fill(Q, Q + size_t(m) * size_t(m), 0.0);
+        std::vector<double> dd(d), ee(e);
         for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
         const auto tq0 = std::chrono::steady_clock::now();
         for (int i = knew; i < m; ++i)  // Q starts as the identity: lower bandwidth i - knew
-            ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q.data(), i - knew);
+            ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q, i - knew);
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
         const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
         const double hk = ee[size_t(knew - 1)];                         // H(knew, knew-1)
-        HIPCHK(hipMemcpyAsync(c->Qd.p, Q.data(), size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
         ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>());
         ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
                             c->npart.as<double>());

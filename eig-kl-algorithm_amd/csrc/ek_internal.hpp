@@ -8,6 +8,7 @@
 #include <memory>
 #include <utility>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/eigkl.h"
@@ -43,6 +44,9 @@ template <class F>
 void parallel_for(int64_t n, F&& fn);  // fn(begin, end)
 template <class F>
 void run_threads(int T, F&& fn);  // fn(t) for t < T, t = 0 on the calling thread
+// fn(ctx, t) for t < T on a persistent worker pool (t = 0 on the caller);
+// spawned threads when another caller holds the pool
+void pool_run(int T, void (*fn)(void*, int), void* ctx);
 }  // namespace ek
 
 #define EK_TRY try {
@@ -362,20 +366,15 @@ void ek::parallel_for(int64_t n, F&& fn) {
         fn(int64_t(0), n);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve(T);
-    for (int64_t t = 0; t < T; ++t) {
-        const int64_t b = n * t / T, e = n * (t + 1) / T;
-        th.emplace_back([&fn, b, e] { fn(b, e); });
-    }
-    for (auto& x : th) x.join();
+    run_threads(int(T), [&](int t) { fn(n * t / T, n * (t + 1) / T); });
 }
 
 template <class F>
 void ek::run_threads(int T, F&& fn) {
-    std::vector<std::thread> th;
-    th.reserve(size_t(std::max(T - 1, 0)));
-    for (int t = 1; t < T; ++t) th.emplace_back([&fn, t] { fn(t); });
-    if (T >= 1) fn(0);
-    for (auto& x : th) x.join();
+    if (T <= 1) {
+        if (T == 1) fn(0);
+        return;
+    }
+    using Fn = std::remove_reference_t<F>;
+    pool_run(T, [](void* c, int t) { (*static_cast<Fn*>(c))(t); }, const_cast<void*>(static_cast<const void*>(&fn)));
 }

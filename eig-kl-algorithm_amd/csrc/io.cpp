@@ -31,15 +31,34 @@ int ek_median_split(int64_t n, const double* v, double* median_out, uint8_t* bit
         for (size_t k = 0; k < NS; ++k) smp[k] = v[size_t(k * size_t(n) / NS)];
         std::sort(smp.begin(), smp.end());
         const double plo = smp[NS / 2 - MARGIN], phi = smp[NS / 2 + MARGIN];
-        s.reserve(size_t(n) / 16);
-        bool nan = false;
-        for (int64_t i = 0; i < n; ++i) {
-            const double x = v[i];
-            if (x < plo) ++below;
-            else if (x <= phi) s.push_back(x);
-            else nan |= x != x;
+        // one pass on the host threads: each counts the values below the
+        // bracket and keeps those inside it (in index order, concatenated)
+        const int T = int(std::min<int64_t>(ek::host_threads(), std::max<int64_t>(1, n / 32768)));
+        std::vector<std::vector<double>> part(static_cast<size_t>(T));
+        std::vector<size_t> nb(static_cast<size_t>(T), 0);
+        std::vector<char> nan(static_cast<size_t>(T), 0);
+        ek::run_threads(T, [&](int t) {
+            const int64_t lo = n * t / T, hi2 = n * (t + 1) / T;
+            auto& ps = part[size_t(t)];
+            ps.reserve(size_t(hi2 - lo) / 16 + 16);
+            size_t b = 0;
+            bool bad = false;
+            for (int64_t i = lo; i < hi2; ++i) {
+                const double x = v[i];
+                if (x < plo) ++b;
+                else if (x <= phi) ps.push_back(x);
+                else bad |= x != x;
+            }
+            nb[size_t(t)] = b;
+            nan[size_t(t)] = bad;
+        });
+        bool any_nan = false;
+        for (int t = 0; t < T; ++t) {
+            below += nb[size_t(t)];
+            any_nan |= nan[size_t(t)] != 0;
+            s.insert(s.end(), part[size_t(t)].begin(), part[size_t(t)].end());
         }
-        bracketed = !nan && below <= rlo && hi < below + s.size();
+        bracketed = !any_nan && below <= rlo && hi < below + s.size();
     }
     if (!bracketed) {
         s.assign(v, v + n);
@@ -54,7 +73,9 @@ int ek_median_split(int64_t n, const double* v, double* median_out, uint8_t* bit
     }
     if (median_out) *median_out = med;
     if (bits_out)
-        for (int64_t i = 0; i < n; ++i) bits_out[i] = uint8_t(med > v[i]);
+        ek::parallel_for(n, [&](int64_t lo, int64_t hi2) {
+            for (int64_t i = lo; i < hi2; ++i) bits_out[i] = uint8_t(med > v[i]);
+        });
     return EK_OK;
     EK_CATCH
 }

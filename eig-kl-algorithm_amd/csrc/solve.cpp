@@ -121,9 +121,26 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
         const auto t = clk::now();
         std::vector<uint8_t> bits(static_cast<size_t>(n));
         chk(ek_median_split(n, v.data(), &r.median, bits.data()));
-        order0.reserve(size_t(n) / 2 + 1);
-        order1.reserve(size_t(n) / 2 + 1);
-        for (int64_t i = 0; i < n; ++i) (bits[size_t(i)] ? order1 : order0).push_back(int32_t(i));  // cKL.cpp:155-174
+        // remain[] lists in node order (cKL.cpp:155-174), built on the host
+        // threads: per-chunk counts, then each chunk fills its ranges
+        const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 32768)));
+        std::vector<int64_t> z(size_t(T) + 1, 0);
+        run_threads(T, [&](int t) {
+            int64_t c = 0;
+            for (int64_t i = n * t / T; i < n * (t + 1) / T; ++i) c += bits[size_t(i)] == 0;
+            z[size_t(t) + 1] = c;
+        });
+        for (int t = 0; t < T; ++t) z[size_t(t) + 1] += z[size_t(t)];
+        order0.resize(size_t(z[size_t(T)]));
+        order1.resize(size_t(n - z[size_t(T)]));
+        run_threads(T, [&](int t) {
+            const int64_t lo = n * t / T;
+            int64_t a = z[size_t(t)], b = lo - z[size_t(t)];
+            for (int64_t i = lo; i < n * (t + 1) / T; ++i) {
+                if (bits[size_t(i)]) order1[size_t(b++)] = int32_t(i);
+                else order0[size_t(a++)] = int32_t(i);
+            }
+        });
         r.t_split = since(t);
     } else {
         if (rank != 0) {  // the KL loop does not shard: other ranks have nothing to do
@@ -159,11 +176,19 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     r.t_kl_setup = since(t);
     t = clk::now();
     const int64_t lcap = int64_t(std::min(order0.size(), order1.size()));
-    std::vector<ek_swap> log(size_t(std::max<int64_t>(lcap, 1)));
-    chk(ek_kl_run(ctx, o.limit, log.data(), lcap, &r.kl));
+    // the swap log goes straight into the caller's buffer when it holds the
+    // whole run (no 32-B-per-node zeroed temporary and copy)
+    dvec<ek_swap> own;
+    ek_swap* log_buf = log_out;
+    if (!log_out || cap < lcap) {
+        own.resize(size_t(std::max<int64_t>(lcap, 1)));
+        log_buf = own.data();
+    }
+    chk(ek_kl_run(ctx, o.limit, log_buf, lcap, &r.kl));
     r.t_kl = since(t);
     const int64_t iters = std::min<int64_t>(r.kl.iterations, lcap);
-    if (log_out && cap > 0) std::copy(log.begin(), log.begin() + std::min(iters, cap), log_out);
+    if (log_out && log_buf != log_out && cap > 0) std::copy(log_buf, log_buf + std::min(iters, cap), log_out);
+    const ek_swap* log = log_buf;
     t = clk::now();
     if (o.write_results) {  // results/<base>_KL_CutSize[_EIG]_output.txt (cKL.cpp:438-444, 315, 380)
         std::error_code ec;  // results/ (and out_dir) created as needed, like the reference's createDir
@@ -196,7 +221,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
                 *p++ = '\n';
             }
             for (int64_t i = lo; i < hi; ++i) {
-                const ek_swap& sw = log[size_t(i)];
+                const ek_swap& sw = log[i];
                 p = std::to_chars(p, end, sw.iter).ptr;
                 *p++ = '\t';
                 p = put_g(p, end, sw.cut);
