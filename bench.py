@@ -391,7 +391,10 @@ def main():
             "bytes_rule": "SURVEY §8d: 12 nnz + 4 (n+1) + 8 n (x) + 8 n (y)",
             "avg_launch_us": round(spmv_us, 3), "launches_timed": spmv_timed,
             "timing": "HIP kernel start/end timestamps (hipExtLaunchKernelGGL events on the context stream) of every "
-                      "4th SpMV of each Lanczos cycle, inside the timed steps",
+                      "4th SpMV of each Lanczos cycle, inside the timed steps. The start event is a marker ahead of "
+                      "the dispatch, so this duration also holds the ~1.5 us kernel boundary before the SpMV: "
+                      "rocprofv3 --kernel-trace of the same command gives 11.8 us against 13.4 us here "
+                      "(profiles/r02/r02s_kernel_stats.csv); achieved and frac are therefore lower bounds",
             "fused_bytes_per_launch": int(fused_bytes),
             "fused_frac": round(fused_bytes / spmv_us / 1e3 / HBM_PEAK_GBS, 4),
             "stored_bytes_per_launch": int(stored),
