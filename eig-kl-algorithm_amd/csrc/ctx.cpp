@@ -1563,6 +1563,14 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
             std::fprintf(stderr, "\n");
             if (ho.prof[15])
                 std::fprintf(stderr, "[kl] in-loop shader clock %.0f MHz\n", double(ho.prof[14]) / (double(ho.prof[15]) * 0.01));
+            if (ho.warr[0] || ho.warr[8]) {
+                const double cyc_ns = ho.prof[15] ? double(ho.prof[15]) * 10.0 / double(ho.prof[14]) : 1.0 / 2.4;
+                const double f = 1e-3 * cyc_ns / double(std::max<long long>(1, ho.iterations));
+                std::fprintf(stderr, "[kl] per wave, us after its loop top: selection done / barrier 1 / G2a done / barrier 2:\n");
+                for (int w = 0; w < 8; ++w)
+                    std::fprintf(stderr, "[kl]   w%d %.3f %.3f %.3f %.3f\n", w, f * double(ho.warr[24 + w]),
+                                 f * double(ho.warr[w]), f * double(ho.warr[16 + w]), f * double(ho.warr[8 + w]));
+            }
         }
         res->total_ms = double(loop_ms) + double(prep_ms);
     }

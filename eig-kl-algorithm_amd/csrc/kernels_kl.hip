@@ -37,6 +37,9 @@
 
 #include "ek_internal.hpp"
 
+#ifndef EK_KL_PREFETCH
+#define EK_KL_PREFETCH 1  // provisional next pair's rows touched into L2 across barrier 2 (0: off, for A/B)
+#endif
 #ifndef EK_E_SLEEP
 #define EK_E_SLEEP 4  // early-rescan waves: s_sleep units before their loads (2: same, 8: +0.9 ms per solve)
 #endif
@@ -45,6 +48,8 @@ namespace ek {
 namespace dev {
 
 typedef unsigned long long u64;
+typedef int v4i __attribute__((ext_vector_type(4)));  // a clang vector: stays in registers where HIP's int4 struct may not
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t ord_f32(float g) {
     if (g == 0.0f) g = 0.0f;  // -0 == +0 under cKL's comparisons
@@ -61,49 +66,44 @@ __device__ __forceinline__ u64 key_min(float g, int pos) {
     if (!(g < FLT_MAX)) return 0ull;
     return (u64(ord_f32(-g)) << 32) | u64(~uint32_t(pos));
 }
-// wave64 max of a 64-bit key without LDS traffic: DPP quad_perm / row
-// (half-)mirror inside each 16-lane row, then gfx950's v_permlane16_swap and
-// v_permlane32_swap across rows and halves.  Every lane ends with the max.
+// wave64 max of a 64-bit key without LDS traffic, in two 32-bit passes: the
+// max of the high words, then the max of the low words of the lanes holding
+// it.  Each pass is DPP quad_perm / row (half-)mirror steps inside each
+// 16-lane row (v_max_u32 with a DPP source: one instruction per step), then
+// gfx950's v_permlane16_swap (and v_permlane32_swap) across rows and halves.
+// Every lane ends with the max.  (One 64-bit pass costs a compare and two
+// selects per step.)
 template <int CTRL>
-__device__ __forceinline__ u64 dpp_max(u64 v) {
-    const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
-    const unsigned lo2 = __builtin_amdgcn_update_dpp(0u, lo, CTRL, 0xf, 0xf, false);
-    const unsigned hi2 = __builtin_amdgcn_update_dpp(0u, hi, CTRL, 0xf, 0xf, false);
-    const u64 o = (u64(hi2) << 32) | lo2;
+__device__ __forceinline__ uint32_t dpp_max32(uint32_t v) {
+    const uint32_t o = __builtin_amdgcn_update_dpp(0u, v, CTRL, 0xf, 0xf, false);  // 0: max's identity
     return o > v ? o : v;
 }
+__device__ __forceinline__ uint32_t row_max32(uint32_t v) {
+    v = dpp_max32<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_max32<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = dpp_max32<0x141>(v);  // row_half_mirror
+    return dpp_max32<0x140>(v);  // row_mirror
+}
 // max within each 32-lane half of the wave (lanes 0-31 and 32-63 separately)
+__device__ __forceinline__ uint32_t half_max32(uint32_t v) {
+    v = row_max32(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return a[0] > a[1] ? a[0] : a[1];
+}
+__device__ __forceinline__ uint32_t wave_max32(uint32_t v) {
+    v = half_max32(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return a[0] > a[1] ? a[0] : a[1];
+}
 __device__ __forceinline__ u64 half_max_u64(u64 v) {
-    v = dpp_max<0xB1>(v);
-    v = dpp_max<0x4E>(v);
-    v = dpp_max<0x141>(v);
-    v = dpp_max<0x140>(v);
-    const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
-    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    const u64 x = (u64(b[0]) << 32) | a[0], y = (u64(b[1]) << 32) | a[1];
-    return x > y ? x : y;
+    const uint32_t hi = uint32_t(v >> 32), lo = uint32_t(v);
+    const uint32_t H = half_max32(hi);
+    return (u64(H) << 32) | half_max32(hi == H ? lo : 0u);
 }
 __device__ __forceinline__ u64 wave_max_u64(u64 v) {
-    v = dpp_max<0xB1>(v);   // quad_perm [1,0,3,2]
-    v = dpp_max<0x4E>(v);   // quad_perm [2,3,0,1]
-    v = dpp_max<0x141>(v);  // row_half_mirror
-    v = dpp_max<0x140>(v);  // row_mirror
-    {
-        const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
-        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-        const u64 x = (u64(b[0]) << 32) | a[0], y = (u64(b[1]) << 32) | a[1];
-        v = x > y ? x : y;
-    }
-    {
-        const unsigned lo = unsigned(v), hi = unsigned(v >> 32);
-        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-        const u64 x = (u64(b[0]) << 32) | a[0], y = (u64(b[1]) << 32) | a[1];
-        v = x > y ? x : y;
-    }
-    return v;
+    const uint32_t hi = uint32_t(v >> 32), lo = uint32_t(v);
+    const uint32_t H = wave_max32(hi);
+    return (u64(H) << 32) | wave_max32(hi == H ? lo : 0u);
 }
 
 // uniform broadcast of lane `l` (v_readlane: no LDS round trip, unlike __shfl)
@@ -210,6 +210,31 @@ __global__ __launch_bounds__(256) void k_cut_final(KLDev d, int nb) {
     if (threadIdx.x == 0) *d.cut0 = float((lds4[0] + lds4[1]) + (lds4[2] + lds4[3]));
 }
 
+// The lane's best of several positions p0 + 64 q (+ lane), compared as fp32
+// gains: the same winner as the largest key_max / key_min, since within a lane
+// positions rise with q, so a strict compare keeps the first of equal gains
+// (+0 and -0 compare equal), NaN never compares true and the invalid ends
+// (<= -FLT_MAX for list 0, >= FLT_MAX for list 1) never beat the initial
+// value.  One compare and two selects per position instead of building and
+// comparing a 64-bit key; the key is built once, for the lane's winner.
+// Returns the winner's q in *bq (-1: none).
+template <int NQ>
+__device__ __forceinline__ u64 lane_best(const float* g, int s, int p0, int lane, int skip, int* bq) {
+    float bg = s ? FLT_MAX : -FLT_MAX;
+    int q0 = -1;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const float gq = p0 + q * 64 + lane == skip ? __builtin_nanf("") : g[q];
+        const bool better = s ? gq < bg : gq > bg;
+        bg = better ? gq : bg;
+        q0 = better ? q : q0;
+    }
+    *bq = q0;
+    if (q0 < 0) return 0ull;
+    const int p = p0 + q0 * 64 + lane;
+    return s ? key_min(bg, p) : key_max(bg, p);
+}
+
 // Best key of one chunk together with its winner's row descriptor.  Gains and
 // descriptors are both read by position, so the winner needs no dependent
 // load.  Returns the key in every lane; the winner lane (or lane 0 for an
@@ -276,15 +301,19 @@ __host__ __device__ inline int kl_sel_pad(int nck0, int nck1) {
 // lanes of a wave (one per row) read 8 different bank groups instead of one
 constexpr int KL_STAGE_ROW = KL_SEG_LANES + 1;
 constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded, 8 plain)
+// updated rows that live in node1's / node2's own chunk, per list (more: the
+// chunk is rescanned).  A chunk holds 1024 of the list's positions, so most
+// swaps have none.
+constexpr int KL_AB_CAP = 16;
 
 size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t words = (size_t(d.n) + 31) / 32;
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
     // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * 2 (early rescans), as carved by the kernel
     constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
-    const size_t b = (nck + KL_ITEM_CAP + 4 + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
-                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4) * 8 +
-                     (2 * nck + KL_ITEM_CAP + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
+    const size_t b = (nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
+                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP) * 8 +
+                     (2 * nck + KL_ITEM_CAP + 4 + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
     return b <= 152 * 1024 ? b : 0;
 }
 
@@ -298,17 +327,9 @@ __device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const 
     float g[KL_CHUNK / 64];
 #pragma unroll
     for (int q = 0; q < KL_CHUNK / 64; ++q) g[q] = gp[c * KL_CHUNK + q * 64 + lane];
-    u64 k = 0ull;
-    int bp = 0;
-#pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) {
-        const int p = c * KL_CHUNK + q * 64 + lane;
-        const u64 kk = p == skip ? 0ull : (s ? key_min(g[q], p) : key_max(g[q], p));
-        if (kk > k) {
-            k = kk;
-            bp = p;
-        }
-    }
+    int bq;
+    const u64 k = lane_best<KL_CHUNK / 64>(g, s, c * KL_CHUNK, lane, skip, &bq);
+    const int bp = c * KL_CHUNK + (bq < 0 ? 0 : bq) * 64 + lane;
     const u64 m = wave_max_u64(k);
     const u64 bal = __ballot(m != 0ull && k == m);  // keys carry the position: one lane at most
     *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
@@ -336,17 +357,24 @@ __device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const
         g[q] = gp[p];
         pi[q] = *reinterpret_cast<const int4*>(pinfo + p);
     }
-    u64 k = 0ull;
+    // lane_best's compare, carrying the winner's descriptor along (a select by
+    // the winning index afterwards becomes a dynamically indexed array: scratch)
+    float bg = s ? FLT_MAX : -FLT_MAX;
+    int bq = -1;
     int4 bi = make_int4(0, 0, 0, 0);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const int p = p0 + q * 64 + lane;
-        const u64 kk = p == skip ? 0ull : (s ? key_min(g[q], p) : key_max(g[q], p));
-        if (kk > k) {
-            k = kk;
-            bi = pi[q];
-        }
+        const float gq = p0 + q * 64 + lane == skip ? __builtin_nanf("") : g[q];
+        const bool better = s ? gq < bg : gq > bg;
+        bg = better ? gq : bg;
+        bq = better ? q : bq;
+        bi.x = better ? pi[q].x : bi.x;
+        bi.y = better ? pi[q].y : bi.y;
+        bi.z = better ? pi[q].z : bi.z;
+        bi.w = better ? pi[q].w : bi.w;
     }
+    const int bp = p0 + (bq < 0 ? 0 : bq) * 64 + lane;
+    const u64 k = bq < 0 ? 0ull : (s ? key_min(bg, bp) : key_max(bg, bp));
     const u64 m = wave_max_u64(k);
     const u64 bal = __ballot(m != 0ull && k == m);
     *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
@@ -387,6 +415,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     // waves 0 .. NG-1 run the gain updates
     constexpr int E_PARTS = 2, NQ_E = KL_CHUNK / 64 / E_PARTS;
     constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
+    constexpr int W_PF = W_W;  // also runs P, the prefetch of the provisional next pair
+    constexpr int W_FLIP = W_EA - 1;  // flips the side / lock bitmaps after barrier 1 (an early-rescan wave)
     static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * 2, "kl_loop_lds_bytes reserves staging for NG gain waves");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -398,20 +428,23 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     KLInfo* ci1 = ci0 + d.nck0;
     KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
     KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2][E_PARTS] early-rescan winners
-    int4* sg_stage = reinterpret_cast<int4*>(er_info + 2 * E_PARTS);  // [NG][KL_STAGE_ROWS][KL_STAGE_ROW] G1 staging
+    KLInfo* ab_info = er_info + 2 * E_PARTS;  // [2][KL_AB_CAP] updated rows in node1's / node2's chunk
+    int4* sg_stage = reinterpret_cast<int4*>(ab_info + 2 * KL_AB_CAP);  // [NG][KL_STAGE_ROWS][KL_STAGE_ROW] G1 staging
     u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * KL_STAGE_ROWS * KL_STAGE_ROW);  // chunk keys (zero-padded to nsel)
     u64* ck1 = ck0 + nsel;
     u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
     u64* ckn1 = ckn0 + d.nck0;
     u64* it_key = ckn1 + d.nck1;           // per updated row: its new key
     u64* er_key = it_key + KL_ITEM_CAP;     // [2][E_PARTS] early-rescan keys
-    int* dtag0 = reinterpret_cast<int*>(er_key + 2 * E_PARTS);  // iteration that tagged a late rescan
+    u64* ab_key = er_key + 2 * E_PARTS;     // [2][KL_AB_CAP] their new keys
+    int* dtag0 = reinterpret_cast<int*>(ab_key + 2 * KL_AB_CAP);  // iteration that tagged a late rescan
     int* dtag1 = dtag0 + d.nck0;
     int* ctag0 = dtag1 + d.nck1;  // iteration that claimed it
     int* ctag1 = ctag0 + d.nck0;
     int* it_cs = ctag1 + d.nck1;  // per updated row: list << 31 | chunk (-1: locked)
     int* s_stop = it_cs + KL_ITEM_CAP;  // [4], by iteration parity
-    uint32_t* s_side = reinterpret_cast<uint32_t*>(s_stop + 4);
+    int* ab_cnt = s_stop + 4;  // [2] (+2 pad): rows appended to ab_* this swap, reset by G2a
+    uint32_t* s_side = reinterpret_cast<uint32_t*>(ab_cnt + 4);
     uint32_t* s_lock = s_side + words;
     float* s_wd = reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
     if constexpr (SEGC)
@@ -435,11 +468,20 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         s_lock[i] = 0u;
     }
     if (tid < 4) s_stop[tid] = tid == 3 ? -1 : 0;
+    if (tid < 4) ab_cnt[tid] = 0;
     __syncthreads();
     float cut = *d.cut0, best = cut;  // loop-carried scalars: the W wave's lane 0 only
     long long best_it = 0, it = 0;
     unsigned term = 0;
     unsigned long long tph[12] = {}, tstamp = 0;  // diagnostic build only (PROF)
+    // P (wave W_PF): the provisional next pair's descriptor, read before
+    // barrier 2, and the lines its rows' loads touched (consumed one swap
+    // later, after that wave's own rescan loads, so nothing waits for them)
+    int4 pf_inf = make_int4(0, 0, 0, 0);
+    int4 pf_seg = make_int4(0, 0, 0, 0), pf_seg2 = make_int4(0, 0, 0, 0), pf_aux = make_int4(0, 0, 0, 0);
+    int pf_col = 0;
+    float pf_w = 0.0f;
+    uint32_t pf_sink = 0u;
     const unsigned long long c_start = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long r_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
     auto stamp = [&](int ph) {
@@ -451,8 +493,35 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
         }
     };
+    unsigned long long w_top = 0, w_arr1 = 0, w_arr2 = 0, w_g2a = 0, w_sel = 0;  // PROF: this wave's timeline
     for (;; ++it) {
         stamp(-1);
+        if constexpr (PROF) w_top = __builtin_amdgcn_s_memtime();
+        if constexpr (EK_KL_PREFETCH) {
+            if (wv == W_PF) {
+                // P. touch the provisional pair's rows (one lane per row line:
+                // lanes 0-31 node1's, 32-63 node2's; clamped addresses): the
+                // W wave's weight lookup and the gain waves' segment and
+                // descriptor loads after the selection then hit L2 instead
+                // of the MALL
+                const int rp = __builtin_amdgcn_readlane(pf_inf.y, 0), ln = __builtin_amdgcn_readlane(pf_inf.z, 0);
+                const int rq = __builtin_amdgcn_readlane(pf_inf.y, 32), lq = __builtin_amdgcn_readlane(pf_inf.z, 32);
+                const int r0 = half ? rq : rp, l0 = half ? lq : ln;
+                if (l0 > 0) {
+                    const int last = r0 + l0 - 1;
+                    const int rs = min(r0 + hl, last);
+                    if constexpr (SEGC) {
+                        pf_seg = *reinterpret_cast<const int4*>(d.segc + size_t(rs) * KL_SEGC_PIECES);
+                    } else if (d.seg) {
+                        pf_seg = *reinterpret_cast<const int4*>(d.seg + size_t(rs) * KL_SEG_LANES);
+                        pf_seg2 = *reinterpret_cast<const int4*>(d.seg + size_t(rs) * KL_SEG_LANES + KL_SEG_LANES / 2);
+                    }
+                    pf_aux = *reinterpret_cast<const int4*>(d.aux + min(r0 + 8 * hl, last));
+                    pf_col = d.col[min(r0 + 32 * hl, last)];
+                    pf_w = d.w[min(r0 + 32 * hl, last)];
+                }
+            }
+        }
         // S. selection (cKL.cpp:341-355): lanes 0-31 reduce remain[0]'s keys,
         // 32-63 remain[1]'s; identical in every wave
         u64 k = 0ull;
@@ -460,12 +529,20 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // 8 keys per lane read together (clamped index: duplicates do not
             // change a max); one read per trip waited for each LDS round trip
             const u64* ck = half ? ck1 : ck0;
-            for (int c0 = hl; c0 < nsel; c0 += 8 * 32) {
-                u64 kv[8];
+            if (nsel <= 4 * 32) {  // up to 128 chunks a list (~130k positions): 4 keys a lane
+                u64 kv[4];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) kv[u] = ck[min(c0 + 32 * u, nsel - 1)];
+                for (int u = 0; u < 4; ++u) kv[u] = ck[min(hl + 32 * u, nsel - 1)];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) k = kv[u] > k ? kv[u] : k;
+                for (int u = 0; u < 4; ++u) k = kv[u] > k ? kv[u] : k;
+            } else {
+                for (int c0 = hl; c0 < nsel; c0 += 8 * 32) {
+                    u64 kv[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) kv[u] = ck[min(c0 + 32 * u, nsel - 1)];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) k = kv[u] > k ? kv[u] : k;
+                }
             }
             k = half_max_u64(k);
         }
@@ -476,6 +553,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         const KLInfo ia = ci0[cA], ib = ci1[cB];
         const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
         stamp(0);
+        if constexpr (PROF) {
+            if (A == -7) s_stop[2] = 0;  // keeps the descriptor read ahead of the stamp
+            w_sel += __builtin_amdgcn_s_memtime() - w_top;
+        }
         // swap + erase (swip, cKL.cpp:274-286): the bitmaps are flipped after
         // the first barrier (G2, W wave); until then every lookup reads the
         // pre-swap bitmaps and applies the swap itself: node1 and node2 (never
@@ -486,6 +567,11 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         auto locked_now = [&](int x) -> bool { return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B; };
         const int tot = la + lb;
         const int tag = int(it);
+        // G1 lanes: the last row each summed ({list << 31 | chunk} or -1, new
+        // key, descriptor), published from registers after barrier 1
+        int my_cs = -1;
+        u64 my_kn = 0ull;
+        int4 my_inf = make_int4(0, 0, 0, 0);
         if (wv == W_W) {
             // W. w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
             float gA = 0.f, gB = 0.f;
@@ -522,6 +608,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 if (it + 1 >= d.n0 || it + 1 >= d.n1) stop = 1;  // a remain[] list is exhausted
                 s_stop[it & 1] = stop;
             }
+            if constexpr (EK_KL_PREFETCH)
+                pf_sink ^= uint32_t(pf_seg.x ^ pf_seg.w ^ pf_seg2.x ^ pf_aux.x ^ pf_col) ^ __float_as_uint(pf_w);
         } else if (wv > W_EB - E_PARTS) {
             // E. early rescan of the chunk node1 (node2) leaves, E_PARTS waves
             // each taking a contiguous part of it
@@ -640,18 +728,22 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     if (SEGC || d.seg) {
                         // 8 entries per block; a block no row of this wave reaches
                         // is skipped as a whole (wave-uniform branch): the loop is
-                        // issue-bound, and the zero padding would add exact zeros
+                        // issue-bound, and the zero padding would add exact zeros.
+                        // (internal, external) advance together in one packed fp32
+                        // add per entry (v_pk_add_f32: two IEEE fp32 adds, the same
+                        // bits as two v_add_f32), each strictly in row order
+                        v2f ie = {0.0f, 0.0f};
 #pragma unroll
                         for (int b = 0; b < KL_SEG_LANES / 4; ++b) {
                             if (!__ballot(len > 8 * b)) break;
 #pragma unroll
                             for (int j = 4 * b; j < 4 * b + 4; ++j) {  // strictly in row order
-                                internal += __int_as_float(sg[j].x);
-                                external += __int_as_float(sg[j].y);
-                                internal += __int_as_float(sg[j].z);
-                                external += __int_as_float(sg[j].w);
+                                ie += v2f{__int_as_float(sg[j].x), __int_as_float(sg[j].y)};
+                                ie += v2f{__int_as_float(sg[j].z), __int_as_float(sg[j].w)};
                             }
                         }
+                        internal = ie.x;
+                        external = ie.y;
                         q = 2 * KL_SEG_LANES;
                     }
                     if constexpr (PROF) {
@@ -686,7 +778,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     const int s = ls;
                     (s ? d.gp1 : d.gp0)[pp] = g;
                     kn = s ? key_min(g, pp) : key_max(g, pp);
-                    if (!ab) {
+                    if (ab) {  // node1's / node2's chunk: resolved by G2a from this short list
+                        const int slot = atomicAdd(&ab_cnt[s], 1);
+                        if (slot < KL_AB_CAP) {
+                            ab_key[s * KL_AB_CAP + slot] = kn;
+                            ab_info[s * KL_AB_CAP + slot] = KLInfo{u, rp, len, pp};
+                        }
+                    } else {
                         if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(pp) && kn < K) {
                             (s ? dtag1 : dtag0)[c] = tag;  // the winner fell: rescan
                             s_stop[3] = tag;
@@ -706,63 +804,78 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     it_cs[i] = cs;
                     it_info[i] = inf;
                 }
+                my_cs = cs;
+                my_kn = kn;
+                my_inf = make_int4(inf.a, inf.b, inf.c, inf.d);
             }
         }
         stamp(1);
+        if constexpr (PROF) w_arr1 += __builtin_amdgcn_s_memtime() - w_top;
         __syncthreads();  // (1) gains, early rescans, merged keys and tags visible
         stamp(2);
+        // the last iteration that tagged a chunk, read first so its round trip
+        // overlaps the G2a / P / G2b reads (G2c runs only when it is this one)
+        const bool any_tag = s_stop[3] == tag;
         // G2a. node1's and node2's chunks: one wave (lanes 0-31 list 0, 32-63
         // list 1), beside G2b/G2c in the others
+#ifdef EK_LAB_NO_G2A
+        if (false) {
+#else
         if (wv == W_EA) {
+#endif
             const int s = half, cS = s ? cB : cA;
-            u64 R = 0ull;  // the early rescan's key: the best of its parts
-            int rpart = 0;
+            // one LDS round trip: the early rescan's parts (keys and winners),
+            // the list of updated rows in the chunk and their count
+            u64 rk[E_PARTS];
+            v4i rf[E_PARTS];
 #pragma unroll
-            for (int q = 0; q < E_PARTS; ++q)
-                if (er_key[s * E_PARTS + q] > R) {
-                    R = er_key[s * E_PARTS + q];
-                    rpart = q;
-                }
+            for (int q = 0; q < E_PARTS; ++q) {
+                rk[q] = er_key[s * E_PARTS + q];
+                rf[q] = *reinterpret_cast<const v4i*>(er_info + s * E_PARTS + q);
+            }
+            // (the list entries are read whatever the count, so all of it is one
+            // round trip; slots beyond the count hold stale rows and are masked)
+            const int cnt = ab_cnt[s];
+            const int hs = hl < KL_AB_CAP ? hl : KL_AB_CAP - 1;
+            const u64 bk_raw = ab_key[s * KL_AB_CAP + hs];
+            const v4i bf = *reinterpret_cast<const v4i*>(ab_info + s * KL_AB_CAP + hs);
+            const bool have = hl < cnt && hl < KL_AB_CAP;
+            const u64 bk = have ? bk_raw : 0ull;
+            if (hl == 0) ab_cnt[s] = 0;  // after the read (in order within the wave); G1 appends after barrier 2
+            u64 R = rk[0];  // the early rescan's key: the best of its parts
+            v4i Rf = rf[0];
+#pragma unroll
+            for (int q = 1; q < E_PARTS; ++q) {  // component selects (a conditional vector copy went to scratch)
+                const bool b = rk[q] > R;
+                R = b ? rk[q] : R;
+                Rf.x = b ? rf[q].x : Rf.x;
+                Rf.y = b ? rf[q].y : Rf.y;
+                Rf.z = b ? rf[q].z : Rf.z;
+                Rf.w = b ? rf[q].w : Rf.w;
+            }
             const int Rpos = int(~uint32_t(R & 0xffffffffull));  // meaningless when R == 0 (never matched)
-            u64 bk = 0ull;
-            int bi = 0;
-            bool stale = false;
-            const int ni = tot < KL_ITEM_CAP ? tot : KL_ITEM_CAP;
-            for (int i = hl; i < ni; i += 32) {
-                const int cs = it_cs[i];
-                if (cs == -1 || int(uint32_t(cs) >> 31) != s || (cs & 0x7fffffff) != cS) continue;
-                const u64 kn = it_key[i];
-                if (R != 0ull && it_info[i].d == Rpos && kn < R) stale = true;
-                if (kn > bk) {
-                    bk = kn;
-                    bi = i;
-                }
-            }
-            const u64 m = half_max_u64(bk);
+            // the early rescan saw the old gain of an updated row that then fell
+            const bool stale = have && R != 0ull && bf.w == Rpos && bk < R;
             const u64 hmask = s ? 0xffffffff00000000ull : 0x00000000ffffffffull;
-            const bool st = (__ballot(stale) & hmask) != 0ull || tot > KL_ITEM_CAP;
-            // readlane needs a wave-uniform lane: take both halves' winners, then pick
-            const u64 wb = __ballot(m != 0ull && bk == m);
-            const u64 wb0 = wb & 0x00000000ffffffffull, wb1 = wb & 0xffffffff00000000ull;
-            const int wbi0 = __builtin_amdgcn_readlane(bi, wb0 ? __ffsll((long long)wb0) - 1 : 0);
-            const int wbi1 = __builtin_amdgcn_readlane(bi, wb1 ? __ffsll((long long)wb1) - 1 : 32);
-            const int wbi = s ? wbi1 : wbi0;
-            if (hl == 0 && !st) {
-                u64 nk;
-                KLInfo nf;
+            const bool st = (__ballot(stale) & hmask) != 0ull || cnt > KL_AB_CAP;
+            u64 m = 0ull;
+            if (__ballot(cnt > 0)) m = half_max_u64(bk);  // (most swaps: no updated row in either chunk)
+            if (!st) {
+                // keys carry the position: at most one lane holds m
                 if (m > R) {
-                    nk = m;
-                    nf = it_info[wbi];
-                } else {
-                    nk = R;
-                    nf = er_info[s * E_PARTS + rpart];
+                    if (have && bk == m) {
+                        (s ? ck1 : ck0)[cS] = m;
+                        (s ? ckn1 : ckn0)[cS] = m;
+                        *reinterpret_cast<v4i*>((s ? ci1 : ci0) + cS) = bf;
+                    }
+                } else if (hl == 0) {
+                    (s ? ck1 : ck0)[cS] = R;
+                    (s ? ckn1 : ckn0)[cS] = R;
+                    *reinterpret_cast<v4i*>((s ? ci1 : ci0) + cS) = Rf;
                 }
-                (s ? ck1 : ck0)[cS] = nk;
-                (s ? ckn1 : ckn0)[cS] = nk;
-                (s ? ci1 : ci0)[cS] = nf;
             }
-            // a stale early rescan (or a hub beyond the item list): full
-            // rescan now that every new gain (and node1/node2's NaN) is stored
+            // a stale early rescan (or more updated rows than the list
+            // holds): full rescan now that every new gain (and node1/node2's NaN) is stored
             const bool stA = __builtin_amdgcn_readlane(int(st), 0) != 0, stB = __builtin_amdgcn_readlane(int(st), 32) != 0;
             if constexpr (PROF) {
                 if (lane == 0) atomicAdd(&s_stop[2], 1000000 * (int(stA) + int(stB)));  // stale counts in the high digits
@@ -781,29 +894,72 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
         }
         stamp(3);
-        if (wv == W_W && lane == 0) {  // the swap itself, for the next swap's lookups (barrier 2)
-            s_side[A >> 5] |= 1u << (A & 31);
-            s_side[B >> 5] &= ~(1u << (B & 31));
-            s_lock[A >> 5] |= 1u << (A & 31);
-            s_lock[B >> 5] |= 1u << (B & 31);
+        if constexpr (PROF) w_g2a += __builtin_amdgcn_s_memtime() - w_top;
+        if (wv == W_FLIP && lane == 0) {  // the swap itself, for the next swap's lookups (barrier 2)
+            // LDS atomics without return: four independent operations instead
+            // of four dependent read-modify-write round trips
+            atomicOr(&s_side[A >> 5], 1u << (A & 31));
+            atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
+            atomicOr(&s_lock[A >> 5], 1u << (A & 31));
+            atomicOr(&s_lock[B >> 5], 1u << (B & 31));
+        }
+        if constexpr (EK_KL_PREFETCH) {
+            if (wv == W_PF) {
+                // P. provisional next pair (a prefetch hint, never a result):
+                // per list the best shadow key outside node1's / node2's chunk
+                // against that chunk's early rescan.  Its descriptor is read
+                // now and used after barrier 2 (the bitmap flip runs in another
+                // wave: the wait the compiler puts ahead of its LDS reads would
+                // hold this one at barrier 2 for the load)
+                const u64* ckn = half ? ckn1 : ckn0;
+                const int nck = half ? d.nck1 : d.nck0, cS = half ? cB : cA;
+                u64 k = 0ull;
+                for (int c0 = hl; c0 < nck; c0 += 4 * 32) {
+                    u64 kv[4];  // all four reads in flight, then masked (no per-read branch)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) kv[u] = ckn[min(c0 + 32 * u, nck - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const u64 v = kv[u] & (min(c0 + 32 * u, nck - 1) == cS ? 0ull : ~0ull);
+                        k = v > k ? v : k;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < E_PARTS; ++q) {
+                    const u64 v = er_key[half * E_PARTS + q];
+                    k = v > k ? v : k;
+                }
+                k = half_max_u64(k);
+                pf_inf = make_int4(0, 0, 0, 0);
+                if (k != 0ull && hl == 0)
+                    pf_inf = *reinterpret_cast<const int4*>((half ? d.pinfo1 : d.pinfo0) + int(~uint32_t(k & 0xffffffffull)));
+            }
         }
         // G2b. publish merged keys of the other untagged chunks (every item of
         // a chunk writes the same value) and the descriptor of the item that
-        // won.  Two dependent LDS round trips: the item's chunk, key and
-        // descriptor together, then the merged key (the tag of its chunk is
-        // read only in a swap that tagged any: s_stop[3] holds the last
-        // iteration that did).
-        const bool any_tag = s_stop[3] == tag;
-        for (int i = tid; i < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
-            const int cs = it_cs[i];
-            const u64 kn = it_key[i];
-            const KLInfo inf = it_info[i];
-            if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
+        // won.  The G1 lanes publish the last row each summed from registers
+        // (one LDS round trip: the merged key and the chunk's tag); rows of
+        // earlier G1 passes (tot > NG rows per wave pass) go through the
+        // item list.
+        auto publish = [&](int cs, u64 kn, int4 inf) {
             const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
-            if ((s ? c == cB : c == cA) || (any_tag && (s ? dtag1 : dtag0)[c] == tag)) continue;
             const u64 kmerged = (s ? ckn1 : ckn0)[c];
+            const int dt = (s ? dtag1 : dtag0)[c];
+            if ((s ? c == cB : c == cA) || dt == tag) return;
             (s ? ck1 : ck0)[c] = kmerged;
-            if (kmerged == kn) (s ? ci1 : ci0)[c] = inf;
+            if (kmerged == kn) *reinterpret_cast<int4*>((s ? ci1 : ci0) + c) = inf;
+        };
+        if (wv < NG && my_cs != -1) publish(my_cs, my_kn, my_inf);
+        {
+            constexpr int PASS = NG * (SEGC ? 16 : 8);  // rows per G1 pass over the gain waves
+            for (int i = tid; i + PASS < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
+                const int cs = it_cs[i];
+                const u64 kn = it_key[i];
+                // a vector, not a KLInfo: the struct copied under a condition went
+                // through scratch (and a vmcnt(0) wait) in every swap
+                const int4 inf = *reinterpret_cast<const int4*>(it_info + i);
+                if (cs != -1) publish(cs, kn, inf);  // (list-1 chunk ids have bit 31 set: negative as int)
+            }
         }
         // G2c. full rescans of the tagged chunks (one wave each, claimed once)
         for (int i = wv; any_tag && i < tot; i += NW) {
@@ -834,6 +990,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
         }
         stamp(4);
+        if constexpr (PROF) w_arr2 += __builtin_amdgcn_s_memtime() - w_top;
         __syncthreads();  // (2) keys visible to the next selection
         stamp(5);
         if (s_stop[it & 1]) {
@@ -843,6 +1000,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     }
     __syncthreads();
     for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
+    if (EK_KL_PREFETCH && wv == W_PF && lane == 0 && pf_sink == 0x5a5a5a5au) out->prof[12] = 1ull;  // keeps P's loads
+    if (lane == 0) {
+        out->warr[wv] = w_arr1;
+        out->warr[8 + wv] = w_arr2;
+        out->warr[16 + wv] = w_g2a;
+        out->warr[24 + wv] = w_sel;
+    }
     if (wv == W_W && lane == 0) {
         out->iterations = it;
         out->best_iter = best_it;
