@@ -1568,8 +1568,9 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
                 const double f = 1e-3 * cyc_ns / double(std::max<long long>(1, ho.iterations));
                 std::fprintf(stderr, "[kl] per wave, us after its loop top: selection done / barrier 1 / G2a done / barrier 2:\n");
                 for (int w = 0; w < 8; ++w)
-                    std::fprintf(stderr, "[kl]   w%d %.3f %.3f %.3f %.3f\n", w, f * double(ho.warr[24 + w]),
-                                 f * double(ho.warr[w]), f * double(ho.warr[16 + w]), f * double(ho.warr[8 + w]));
+                    std::fprintf(stderr, "[kl]   w%d %.3f %.3f %.3f %.3f  (G2a reads consumed %.3f)\n", w,
+                                 f * double(ho.warr[24 + w]), f * double(ho.warr[w]), f * double(ho.warr[16 + w]),
+                                 f * double(ho.warr[8 + w]), f * double(ho.warr[32 + w]));
             }
         }
         res->total_ms = double(loop_ms) + double(prep_ms);

@@ -338,6 +338,11 @@ __device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const 
         const int4 x = *reinterpret_cast<const int4*>(pinfo + bp);
         inf = KLInfo{x.x, x.y, x.z, x.w};
     }
+    // wait for that load here, on this (rare) path: left pending, the
+    // compiler's wait tracking carries it past the join, and every later
+    // write of those registers in the common path then waits vmcnt(0) —
+    // i.e. for the acks of the gain stores of the swap
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) alone (gfx9 encoding)
     *info = inf;
     return m;
 }
@@ -493,7 +498,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
         }
     };
-    unsigned long long w_top = 0, w_arr1 = 0, w_arr2 = 0, w_g2a = 0, w_sel = 0;  // PROF: this wave's timeline
+    unsigned long long w_top = 0, w_arr1 = 0, w_arr2 = 0, w_g2a = 0, w_sel = 0, w_g2r = 0;  // PROF: this wave's timeline
     for (;; ++it) {
         stamp(-1);
         if constexpr (PROF) w_top = __builtin_amdgcn_s_memtime();
@@ -567,11 +572,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         auto locked_now = [&](int x) -> bool { return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B; };
         const int tot = la + lb;
         const int tag = int(it);
-        // G1 lanes: the last row each summed ({list << 31 | chunk} or -1, new
-        // key, descriptor), published from registers after barrier 1
-        int my_cs = -1;
-        u64 my_kn = 0ull;
-        int4 my_inf = make_int4(0, 0, 0, 0);
         if (wv == W_W) {
             // W. w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
             float gA = 0.f, gB = 0.f;
@@ -804,9 +804,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     it_cs[i] = cs;
                     it_info[i] = inf;
                 }
-                my_cs = cs;
-                my_kn = kn;
-                my_inf = make_int4(inf.a, inf.b, inf.c, inf.d);
             }
         }
         stamp(1);
@@ -818,11 +815,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         const bool any_tag = s_stop[3] == tag;
         // G2a. node1's and node2's chunks: one wave (lanes 0-31 list 0, 32-63
         // list 1), beside G2b/G2c in the others
-#ifdef EK_LAB_NO_G2A
-        if (false) {
-#else
         if (wv == W_EA) {
-#endif
             const int s = half, cS = s ? cB : cA;
             // one LDS round trip: the early rescan's parts (keys and winners),
             // the list of updated rows in the chunk and their count
@@ -856,6 +849,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             const int Rpos = int(~uint32_t(R & 0xffffffffull));  // meaningless when R == 0 (never matched)
             // the early rescan saw the old gain of an updated row that then fell
             const bool stale = have && R != 0ull && bf.w == Rpos && bk < R;
+            if constexpr (PROF) {
+                if (stale && bf.x == -7) s_stop[2] = 0;  // keeps the reads ahead of the stamp
+                w_g2r += __builtin_amdgcn_s_memtime() - w_top;
+            }
             const u64 hmask = s ? 0xffffffff00000000ull : 0x00000000ffffffffull;
             const bool st = (__ballot(stale) & hmask) != 0ull || cnt > KL_AB_CAP;
             u64 m = 0ull;
@@ -937,28 +934,25 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         }
         // G2b. publish merged keys of the other untagged chunks (every item of
         // a chunk writes the same value) and the descriptor of the item that
-        // won.  The G1 lanes publish the last row each summed from registers
-        // (one LDS round trip: the merged key and the chunk's tag); rows of
-        // earlier G1 passes (tot > NG rows per wave pass) go through the
-        // item list.
-        auto publish = [&](int cs, u64 kn, int4 inf) {
-            const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
-            const u64 kmerged = (s ? ckn1 : ckn0)[c];
-            const int dt = (s ? dtag1 : dtag0)[c];
-            if ((s ? c == cB : c == cA) || dt == tag) return;
-            (s ? ck1 : ck0)[c] = kmerged;
-            if (kmerged == kn) *reinterpret_cast<int4*>((s ? ci1 : ci0) + c) = inf;
-        };
-        if (wv < NG && my_cs != -1) publish(my_cs, my_kn, my_inf);
-        {
-            constexpr int PASS = NG * (SEGC ? 16 : 8);  // rows per G1 pass over the gain waves
-            for (int i = tid; i + PASS < tot && i < KL_ITEM_CAP; i += KL_LOOP_THREADS) {
+        // won: the two early-rescan waves of list 1, from the item list (two
+        // LDS round trips: the item, then the merged key and the chunk's tag).
+        // Not the gain waves: the compiler puts waits for their gain stores'
+        // acks ahead of register writes in this code (measured 2.20 -> 2.13 us
+        // per swap at ibm18 shape).
+        if (wv == W_EB || wv == W_EB - 1) {
+            for (int i = (W_EB - wv) * 64 + lane; i < tot && i < KL_ITEM_CAP; i += 128) {
                 const int cs = it_cs[i];
                 const u64 kn = it_key[i];
                 // a vector, not a KLInfo: the struct copied under a condition went
                 // through scratch (and a vmcnt(0) wait) in every swap
                 const int4 inf = *reinterpret_cast<const int4*>(it_info + i);
-                if (cs != -1) publish(cs, kn, inf);  // (list-1 chunk ids have bit 31 set: negative as int)
+                if (cs == -1) continue;  // (list-1 chunk ids have bit 31 set: negative as int)
+                const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
+                const u64 kmerged = (s ? ckn1 : ckn0)[c];
+                const int dt = (s ? dtag1 : dtag0)[c];
+                if ((s ? c == cB : c == cA) || dt == tag) continue;
+                (s ? ck1 : ck0)[c] = kmerged;
+                if (kmerged == kn) *reinterpret_cast<int4*>((s ? ci1 : ci0) + c) = inf;
             }
         }
         // G2c. full rescans of the tagged chunks (one wave each, claimed once)
@@ -1006,6 +1000,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         out->warr[8 + wv] = w_arr2;
         out->warr[16 + wv] = w_g2a;
         out->warr[24 + wv] = w_sel;
+        out->warr[32 + wv] = w_g2r;
     }
     if (wv == W_W && lane == 0) {
         out->iterations = it;
