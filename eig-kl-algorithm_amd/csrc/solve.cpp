@@ -27,11 +27,6 @@ namespace {
 using clk = std::chrono::steady_clock;
 double since(clk::time_point t) { return std::chrono::duration<double>(clk::now() - t).count(); }
 
-struct KLHost {
-    dvec<int32_t> rowptr, col;
-    dvec<float> w;
-};
-
 void chk(int rc) {
     if (rc != EK_OK) throw Error{rc};  // ek_last_error() already holds the message
 }
@@ -39,22 +34,19 @@ void chk(int rc) {
 // The KL adjacency (cKL.cpp:84-149, hash-order emulation) built on host
 // threads, then uploaded with the nets (the device-side inline segments and
 // weight codes included) on the context's KL stream: all of it while the GPU
-// runs the Lanczos solve on the main stream.
-KLHost kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
+// runs the Lanczos solve on the main stream.  The host copy is freed here
+// too, off the solve's path (freeing ~10 MB that several threads touched
+// cost the solve's thread ~2.5 ms at the end of a step).
+void kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
     PhaseTimer pt("kl_thread");
     ThreadCap cap(threads);
     ek_csr G;
     build_kl_graph(*h, G);
-    KLHost g;
-    g.rowptr.swap(G.rowptr);
-    g.col.swap(G.col);
-    g.w.swap(G.val32);
     pt.mark("graph built");
-    chk(ek_kl_graph_setup(ctx, h->nodes, g.rowptr.data(), g.col.data(), g.w.data()));
+    chk(ek_kl_graph_setup(ctx, h->nodes, G.rowptr.data(), G.col.data(), G.val32.data()));
     pt.mark("graph set up");
     chk(ek_kl_nets_setup(ctx, h->nets, h->net_ptr.data(), h->pins.data()));
     pt.mark("nets set up");
-    return g;
 }
 
 std::string join(const char* dir, const std::string& rel) {
@@ -100,7 +92,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     if (n < 2) fail(EK_EINVAL, "%s: %lld nodes, nothing to partition", base.c_str(), (long long)n);
     // initial partition (shuffleSparceMatrix, cKL.cpp:151-197)
     std::vector<int32_t> order0, order1;
-    std::future<KLHost> kg;
+    std::future<void> kg;
     // while the GPU solves, the KL adjacency leaves the solve's host thread
     // (and the HIP runtime's) a few cores
     auto start_kl_graph = [&] {
@@ -169,7 +161,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     }
     ek_ctx* ctx = get_ctx();
     auto t = clk::now();
-    const KLHost g = kg.get();  // graph and nets set up on the context (KL stream, synchronised)
+    kg.get();  // graph and nets set up on the context (KL stream, synchronised)
     r.t_kl_graph_wait = since(t);
     t = clk::now();
     chk(ek_kl_set_partition(ctx, order0.data(), int64_t(order0.size()), order1.data(), int64_t(order1.size())));
@@ -272,8 +264,12 @@ int ek_solve_file(ek_ctx* ctx, const char* path, const ek_solve_opts* opts, ek_s
     if (const int rc = ek_hgr_read(path, &h); rc != EK_OK) throw ek::Error{rc};
     std::unique_ptr<ek_hgr, void (*)(ek_hgr*)> hg(h, ek_hgr_free);
     r.t_read = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    ek::PhaseTimer pt("solve_file");
     ek::solve([ctx] { return ctx; }, rank, nranks, *h, std::filesystem::path(path).filename().string(), o, log_out,
               cap, r);
+    pt.mark("solve returned (its locals freed)");
+    hg.reset();
+    pt.mark("hgr freed");
     r.t_total += r.t_read;
     if (res) *res = r;
     return EK_OK;
