@@ -262,6 +262,7 @@ void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double*
                 const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp);
 // out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device)
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out);
+void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long nrows, unsigned long long st0);
 // f = f*sigma + x*hk ; per-block sum of f^2 -> npart
 void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart);
 // x = x / sqrt(*n2) ... and deflate helpers

@@ -484,6 +484,33 @@ void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double*
                        bov_i, fp);
 }
 
+// The breakdown restart vector (ctx.cpp inject): element g of the global
+// sequence st_{g} = st0 * 48271^(g+1) mod (2^31 - 1), as double(st) / p - 0.5
+// — the host loop's values, each lane jumping ahead by square-and-multiply
+// (operands < 2^31, so every product fits 64 bits).  Padding rows get 0.
+__global__ __launch_bounds__(256) void k_inject(double* __restrict__ f, int ldv, long long row0, long long nrows,
+                                                unsigned long long st0) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ldv) return;
+    if (i >= nrows) {
+        f[i] = 0.0;
+        return;
+    }
+    constexpr unsigned long long P = 2147483647ull;
+    unsigned long long e = (unsigned long long)(row0 + i) + 1ull, b = 48271ull, pw = 1ull;
+    while (e) {
+        if (e & 1ull) pw = pw * b % P;
+        b = b * b % P;
+        e >>= 1;
+    }
+    const unsigned long long st = st0 * pw % P;
+    f[i] = double(st) / 2147483647.0 - 0.5;
+}
+
+void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long nrows, unsigned long long st0) {
+    hipLaunchKernelGGL(k_inject, dim3((ldv + 255) / 256), dim3(256), 0, s, f, ldv, row0, nrows, st0);
+}
+
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out) {
     hipLaunchKernelGGL(k_gemm_vq, dim3(ldv / UPD_ROWS, (kk + 7) / 8), dim3(256), 0, s, ldv, V, m, Q, kk, out);
 }
