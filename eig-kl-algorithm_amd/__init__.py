@@ -135,6 +135,7 @@ _sig("ek_kl_graph_setup", ctypes.c_int, _P, _I64, _P, _P, _P)
 _sig("ek_kl_nets_setup", ctypes.c_int, _P, _I64, _P, _P)
 _sig("ek_kl_set_partition", ctypes.c_int, _P, _P, _I64, _P, _I64)
 _sig("ek_kl_set_partition_bits", ctypes.c_int, _P, _I64, _P)
+_sig("ek_kl_set_partition_fiedler", ctypes.c_int, _P, _P, _P, _P)
 _sig("ek_kl_run", ctypes.c_int, _P, _I32, _P, _I64, ctypes.POINTER(KLResult))
 _sig("ek_kl_sides", ctypes.c_int, _P, _I32, _P)
 _sig("ek_cli_main", ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p))
@@ -471,6 +472,16 @@ class Context:
         _chk(_lib.ek_kl_set_partition_bits(self._c, len(bits), _p(bits)), "kl_set_partition_bits")
         n1 = int(np.count_nonzero(bits))
         self._n01 = (len(bits) - n1, n1)
+
+    def kl_set_partition_fiedler(self):
+        """The -EIG split on the device from the Fiedler vector the last lanczos_fiedler left on this context:
+        median and the remain[] lists of median_split + kl_set_partition_bits.  Returns (median, n0, n1)."""
+        med = ctypes.c_double()
+        n0, n1 = ctypes.c_int64(), ctypes.c_int64()
+        _chk(_lib.ek_kl_set_partition_fiedler(self._c, ctypes.byref(med), ctypes.byref(n0), ctypes.byref(n1)),
+             "kl_set_partition_fiedler")
+        self._n01 = (n0.value, n1.value)
+        return med.value, n0.value, n1.value
 
     def kl_run(self, limit=-1, cap=None):
         cap = min(self._n01) if cap is None else cap

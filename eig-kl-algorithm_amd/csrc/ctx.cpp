@@ -126,6 +126,10 @@ struct ek_ctx {
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
     double* chk_pin = nullptr;
     double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1))
+    // the last Fiedler vector as returned (normalised, sign fixed), kept on
+    // the device for ek_kl_set_partition_fiedler, and that split's scratch
+    DBuf fied, sp_sorted, sp_flag, sp_pos, sp_tmp;
+    int64_t fied_n = 0;
 };
 
 Uploader::Uploader(ek_ctx* ctx, hipStream_t st, size_t total) : c(ctx), s(st) {
@@ -1252,6 +1256,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     for (int64_t i = 1; i < n; ++i)
         if (std::fabs(v[i]) > std::fabs(v[imax])) imax = i;
     const double sgn = v[imax] < 0 ? -inv : inv;
+    c->fied.ensure(size_t(n) * 8);
+    ek::dev::fiedler_scale(s, xg, sgn, int(n), c->fied.as<double>());
+    HIPCHK(hipGetLastError());
+    c->fied_n = n;
     if (lambda_out) *lambda_out = lambda;
     if (v_out)
         for (int64_t i = 0; i < n; ++i) v_out[i] = v[i] * sgn;
@@ -1360,6 +1368,52 @@ int ek_kl_nets_setup(ek_ctx* c, int64_t nets, const int64_t* net_ptr, const int3
     EK_CATCH
 }
 
+}  // extern "C"
+
+namespace {
+// The rest of the partition setup once remain[] lists, plist and the initial
+// sides are on the device (uploaded, or split there from the Fiedler vector)
+void partition_on_device(ek_ctx* c, int64_t n0, int64_t n1) {
+    hipStream_t s = c->stream;
+    const int64_t n = c->kl_n;
+    c->kl_n0 = n0;
+    c->kl_n1 = n1;
+    // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr,
+    // rowlen, plist}, built on the device from the lists just uploaded (the
+    // by-position arrays are padded to whole chunks with zero descriptors, and
+    // the gains with NaN = invalid keys, so the chunk scans load unconditionally)
+    {
+        c->kl_pinfo0.ensure(size_t(chunk_pad(n0)) * sizeof(ek::dev::KLInfo));
+        c->kl_pinfo1.ensure(size_t(chunk_pad(n1)) * sizeof(ek::dev::KLInfo));
+        c->kl_nd.ensure(size_t(std::max<int64_t>(n, 1)) * sizeof(ek::dev::KLInfo));
+        ek::dev::kl_build_desc(s, int(n), int(n0), int(n1), int(chunk_pad(n0)), int(chunk_pad(n1)),
+                               c->kl_order0.as<int32_t>(), c->kl_order1.as<int32_t>(), c->kl_plist.as<uint32_t>(),
+                               c->kl_rowptr.as<int32_t>(), c->kl_pinfo0.as<ek::dev::KLInfo>(),
+                               c->kl_pinfo1.as<ek::dev::KLInfo>(), c->kl_nd.as<ek::dev::KLInfo>());
+        HIPCHK(hipGetLastError());
+        const int64_t nnz = c->kl_rowptr_h[size_t(n)];
+        c->kl_aux.ensure(size_t(std::max<int64_t>(nnz, 1)) * sizeof(ek::dev::KLInfo));
+        ek::dev::kl_build_aux(s, nnz, c->kl_col.as<int32_t>(), c->kl_nd.as<ek::dev::KLInfo>(),
+                              c->kl_aux.as<ek::dev::KLInfo>());
+        HIPCHK(hipGetLastError());
+        c->kl_cinfo0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
+        c->kl_cinfo1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
+    }
+    c->kl_gp0.ensure(size_t(chunk_pad(n0)) * 4);
+    c->kl_gp1.ensure(size_t(chunk_pad(n1)) * 4);
+    HIPCHK(hipMemsetAsync(c->kl_gp0.p, 0xFF, c->kl_gp0.bytes, s));  // NaN padding
+    HIPCHK(hipMemsetAsync(c->kl_gp1.p, 0xFF, c->kl_gp1.bytes, s));
+    c->kl_ckey0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
+    c->kl_ckey1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
+    c->kl_log.ensure(size_t(std::max<int64_t>(1, std::min(n0, n1))) * sizeof(ek_swap));
+    HIPCHK(hipStreamSynchronize(s));
+    c->kl_part_ready = true;
+}
+
+}  // namespace
+
+extern "C" {
+
 int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int32_t* order1, int64_t n1) {
     EK_TRY
     check_ctx(c);
@@ -1382,44 +1436,59 @@ int ek_kl_set_partition(ek_ctx* c, const int32_t* order0, int64_t n0, const int3
         plist[size_t(u)] = uint32_t(i) | 0x80000000u;
     }
     hipStream_t s = c->stream;
-    c->kl_n0 = n0;
-    c->kl_n1 = n1;
     Uploader up(c, s, size_t(n0) * 4 + size_t(n1) * 4 + size_t(n) + size_t(n) * 4);
     up.put(c->kl_order0, order0, size_t(n0));
     up.put(c->kl_order1, order1, size_t(n1));
     up.put(c->kl_side_init, side.data(), size_t(n));
     up.put(c->kl_plist, plist.data(), size_t(n));
-    // row descriptors: by position {node, rowptr, rowlen} and by node {rowptr,
-    // rowlen, plist}, built on the device from the lists just uploaded (the
-    // by-position arrays are padded to whole chunks with zero descriptors, and
-    // the gains with NaN = invalid keys, so the chunk scans load unconditionally)
-    {
-        c->kl_pinfo0.ensure(size_t(chunk_pad(n0)) * sizeof(ek::dev::KLInfo));
-        c->kl_pinfo1.ensure(size_t(chunk_pad(n1)) * sizeof(ek::dev::KLInfo));
-        c->kl_nd.ensure(size_t(std::max<int64_t>(n, 1)) * sizeof(ek::dev::KLInfo));
-        ek::dev::kl_build_desc(s, int(n), int(n0), int(n1), int(chunk_pad(n0)), int(chunk_pad(n1)),
-                               c->kl_order0.as<int32_t>(), c->kl_order1.as<int32_t>(), c->kl_plist.as<uint32_t>(),
-                               c->kl_rowptr.as<int32_t>(), c->kl_pinfo0.as<ek::dev::KLInfo>(),
-                               c->kl_pinfo1.as<ek::dev::KLInfo>(), c->kl_nd.as<ek::dev::KLInfo>());
-        HIPCHK(hipGetLastError());
-        const int64_t nnz = c->kl_rowptr_h[size_t(n)];
-        c->kl_aux.ensure(size_t(std::max<int64_t>(nnz, 1)) * sizeof(ek::dev::KLInfo));
-        ek::dev::kl_build_aux(s, nnz, c->kl_col.as<int32_t>(), c->kl_nd.as<ek::dev::KLInfo>(),
-                              c->kl_aux.as<ek::dev::KLInfo>());
-        HIPCHK(hipGetLastError());
-        c->kl_cinfo0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
-        c->kl_cinfo1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * sizeof(ek::dev::KLInfo));
-        HIPCHK(hipStreamSynchronize(s));  // side / plist (host temporaries) have been copied
-    }
-    c->kl_gp0.ensure(size_t(chunk_pad(n0)) * 4);
-    c->kl_gp1.ensure(size_t(chunk_pad(n1)) * 4);
-    HIPCHK(hipMemsetAsync(c->kl_gp0.p, 0xFF, c->kl_gp0.bytes, s));  // NaN padding
-    HIPCHK(hipMemsetAsync(c->kl_gp1.p, 0xFF, c->kl_gp1.bytes, s));
-    c->kl_ckey0.ensure(size_t((n0 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
-    c->kl_ckey1.ensure(size_t((n1 + ek::dev::KL_CHUNK - 1) / ek::dev::KL_CHUNK + 1) * 8);
-    c->kl_log.ensure(size_t(std::max<int64_t>(1, std::min(n0, n1))) * sizeof(ek_swap));
+    partition_on_device(c, n0, n1);
+    return EK_OK;
+    EK_CATCH
+}
+
+int ek_kl_set_partition_fiedler(ek_ctx* c, double* median_out, int64_t* n0_out, int64_t* n1_out) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->kl_graph_ready) ek::fail(EK_ESTATE, "ek_kl_set_partition_fiedler before ek_kl_graph_setup");
+    const int64_t n = c->kl_n;
+    if (c->fied_n != n || n < 1)
+        ek::fail(EK_ESTATE, "ek_kl_set_partition_fiedler: no Fiedler vector of %lld entries on this context",
+                 (long long)n);
+    if (n > INT32_MAX - 1) ek::fail(EK_EINVAL, "ek_kl_set_partition_fiedler: %lld nodes", (long long)n);
+    hipStream_t s = c->stream;
+    const int ni = int(n);
+    const double* v = c->fied.as<double>();
+    c->sp_sorted.ensure(size_t(n) * 8);
+    c->sp_flag.ensure(size_t(n) * 4);
+    c->sp_pos.ensure(size_t(n) * 4);
+    const size_t tb = ek::dev::split_tmp_bytes(ni);
+    c->sp_tmp.ensure(tb);
+    // the median: ranks n/2 (and n/2 - 1 for even n, their mean), the values
+    // nth_element gives ek_median_split
+    ek::dev::split_sort(s, c->sp_tmp.p, tb, v, c->sp_sorted.as<double>(), ni);
+    const size_t hi = size_t(n / 2);
+    double mid[2] = {0.0, 0.0};
+    HIPCHK(hipMemcpyAsync(mid, c->sp_sorted.as<double>() + (n % 2 == 0 ? hi - 1 : hi), 2 * 8,
+                          hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    c->kl_part_ready = true;
+    const double med = n % 2 == 0 ? (mid[0] + mid[1]) / 2.0 : mid[0];
+    c->kl_order0.ensure(size_t(n) * 4);
+    c->kl_order1.ensure(size_t(n) * 4);
+    c->kl_side_init.ensure(size_t(n));
+    c->kl_plist.ensure(size_t(n) * 4);
+    ek::dev::split_flags_scan(s, c->sp_tmp.p, tb, v, ni, med, c->sp_flag.as<uint32_t>(), c->sp_pos.as<uint32_t>());
+    ek::dev::split_scatter(s, v, c->sp_pos.as<uint32_t>(), ni, med, c->kl_order0.as<int32_t>(),
+                           c->kl_order1.as<int32_t>(), c->kl_plist.as<uint32_t>(), c->kl_side_init.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    uint32_t last[2] = {0, 0};  // pos0[n-1], flag0[n-1]
+    HIPCHK(hipMemcpyAsync(&last[0], c->sp_pos.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&last[1], c->sp_flag.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t n0 = int64_t(last[0]) + int64_t(last[1]);
+    partition_on_device(c, n0, n - n0);
+    if (median_out) *median_out = med;
+    if (n0_out) *n0_out = n0;
+    if (n1_out) *n1_out = n - n0;
     return EK_OK;
     EK_CATCH
 }

@@ -125,7 +125,8 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
            const ek_solve_opts& o, ek_swap* log_out, int64_t cap, ek_solve_result& r);
 void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek_solve_opts& o, double& lambda,
                     std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
-                    const std::function<void()>& after_laplacian = {}, double* t_spmv_setup = nullptr);
+                    const std::function<void()>& after_laplacian = {}, double* t_spmv_setup = nullptr,
+                    bool host_v = true);
 }  // namespace ek
 
 // ---------------------------------------------------------------------------
@@ -263,6 +264,14 @@ void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double*
 // out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device)
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out);
 void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long nrows, unsigned long long st0);
+// device median split of the Fiedler vector (kernels_kl.hip)
+size_t split_tmp_bytes(int n);
+void fiedler_scale(hipStream_t s, const double* x, double sgn, int n, double* out);
+void split_sort(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, double* sorted, int n);
+void split_flags_scan(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, int n, double med, uint32_t* flag0,
+                      uint32_t* pos0);
+void split_scatter(hipStream_t s, const double* v, const uint32_t* pos0, int n, double med, int32_t* order0,
+                   int32_t* order1, uint32_t* plist, uint8_t* side);
 // f = f*sigma + x*hk ; per-block sum of f^2 -> npart
 void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart);
 // x = x / sqrt(*n2) ... and deflate helpers

@@ -29,6 +29,7 @@
 //                     N(node1) u N(node2) (one lane per row), re-key only the
 //                     chunks those nodes live in.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <cfloat>
 #include <algorithm>
@@ -1416,6 +1417,84 @@ void net_cut(hipStream_t s, int64_t nets, const int64_t* net_ptr, const int32_t*
     if (nets <= 0) return;
     hipLaunchKernelGGL(k_net_cut, dim3(unsigned((nets + 255) / 256)), dim3(256), 0, s, (long long)nets, net_ptr, pins,
                        side, count);
+}
+
+
+// ---------------------------------------------------------------------------
+// Median split of the Fiedler vector on the device (ek_kl_set_partition_fiedler):
+// the same values ek_median_split and the remain[] lists of ek_solve_file give
+// on the host (io.cpp, solve.cpp), without the vector's round trip.
+
+// out = x * sgn: the normalised, sign-fixed Ritz vector, the same IEEE
+// products as the host's v_out[i] = v[i] * sgn (ctx.cpp)
+__global__ __launch_bounds__(256) void k_fiedler_scale(const double* __restrict__ x, double sgn, int n,
+                                                       double* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = x[i] * sgn;
+}
+
+// flag0[i] = 1 for a node on side 0: !(med > v[i]) is bit 0 of ek_median_split
+__global__ __launch_bounds__(256) void k_split_flags(const double* __restrict__ v, int n, double med,
+                                                     uint32_t* __restrict__ flag0) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) flag0[i] = med > v[i] ? 0u : 1u;
+}
+
+// remain[] lists in node order (cKL.cpp:155-174) from the exclusive scan of
+// the side-0 flags: position pos0[i] in list 0, or i - pos0[i] in list 1;
+// plist and the initial sides as ek_kl_set_partition builds them
+__global__ __launch_bounds__(256) void k_split_scatter(const double* __restrict__ v, const uint32_t* __restrict__ pos0,
+                                                       int n, double med, int32_t* __restrict__ order0,
+                                                       int32_t* __restrict__ order1, uint32_t* __restrict__ plist,
+                                                       uint8_t* __restrict__ side) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const bool one = med > v[i];
+    const uint32_t p0 = pos0[i];
+    if (one) {
+        const uint32_t p1 = uint32_t(i) - p0;
+        order1[p1] = i;
+        plist[i] = p1 | 0x80000000u;
+    } else {
+        order0[p0] = i;
+        plist[i] = p0;
+    }
+    side[i] = one ? 1 : 0;
+}
+
+#define SPLIT_CHK(call)                                                                            \
+    do {                                                                                           \
+        const hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess) ek::fail(EK_EHIP, "%s failed: %s", #call, hipGetErrorString(e_));    \
+    } while (0)
+
+size_t split_tmp_bytes(int n) {
+    size_t a = 0, b = 0;
+    SPLIT_CHK(hipcub::DeviceRadixSort::SortKeys(nullptr, a, static_cast<const double*>(nullptr),
+                                             static_cast<double*>(nullptr), n));
+    SPLIT_CHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<const uint32_t*>(nullptr),
+                                            static_cast<uint32_t*>(nullptr), n));
+    return std::max(a, b);
+}
+
+void fiedler_scale(hipStream_t s, const double* x, double sgn, int n, double* out) {
+    hipLaunchKernelGGL(k_fiedler_scale, dim3((n + 255) / 256), dim3(256), 0, s, x, sgn, n, out);
+}
+
+void split_sort(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, double* sorted, int n) {
+    SPLIT_CHK(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, v, sorted, n, 0, 64, s));
+}
+
+void split_flags_scan(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, int n, double med, uint32_t* flag0,
+                      uint32_t* pos0) {
+    hipLaunchKernelGGL(k_split_flags, dim3((n + 255) / 256), dim3(256), 0, s, v, n, med, flag0);
+    SPLIT_CHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, flag0, pos0, n, s));
+}
+
+void split_scatter(hipStream_t s, const double* v, const uint32_t* pos0, int n, double med, int32_t* order0,
+                   int32_t* order1, uint32_t* plist, uint8_t* side) {
+    hipLaunchKernelGGL(k_split_scatter, dim3((n + 255) / 256), dim3(256), 0, s, v, pos0, n, med, order0, order1, plist,
+                       side);
 }
 
 }  // namespace dev

@@ -60,7 +60,7 @@ std::string join(const char* dir, const std::string& rel) {
 // on the host, uploaded, Lanczos on the GPU; the full vector on every rank.
 void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek_solve_opts& o, double& lambda,
                     std::vector<double>& v, ek_lanczos_stats& st, double* t_laplacian, double* t_lanczos,
-                    const std::function<void()>& after_laplacian, double* t_spmv_setup) {
+                    const std::function<void()>& after_laplacian, double* t_spmv_setup, bool host_v) {
     const int64_t n = h.nodes;
     (void)rank;
     (void)nranks;
@@ -72,9 +72,10 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
     if (t_spmv_setup) *t_spmv_setup = 0.0;
     if (after_laplacian) after_laplacian();
     t = clk::now();
-    v.assign(size_t(n), 0.0);
-    chk(ek_lanczos_fiedler(ctx, &o.lanczos, &lambda, v.data(), &st));
-    if (o.sign_ref && o.sign_ref[0]) {
+    // (host_v false: the vector stays on the device for ek_kl_set_partition_fiedler)
+    if (host_v) v.assign(size_t(n), 0.0);
+    chk(ek_lanczos_fiedler(ctx, &o.lanczos, &lambda, host_v ? v.data() : nullptr, &st));
+    if (host_v && o.sign_ref && o.sign_ref[0]) {
         std::vector<double> ref(static_cast<size_t>(n));
         chk(ek_eig_read(o.sign_ref, n, nullptr, nullptr, nullptr, ref.data(), nullptr, nullptr, nullptr, nullptr));
         chk(ek_align_sign(n, v.data(), ref.data()));
@@ -100,16 +101,22 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
             kg = std::async(std::launch::async, kl_graph_host, get_ctx(), &h,
                             o.eig == 1 ? std::max(1, host_threads() - 4) : 0);
     };
+    // -EIG without a sign reference: the median split runs on the device,
+    // from the Fiedler vector the Lanczos solve left there, once the KL graph
+    // is set up (ek_kl_set_partition_fiedler: the same lists, no host round trip)
+    const bool dev_split = o.eig == 1 && !(o.sign_ref && o.sign_ref[0]);
+    std::vector<double> v;  // (host split only)
     if (o.eig == 1) {
-        std::vector<double> v;
         // the KL adjacency starts once the Laplacian rows are built (both use
         // every host thread), and runs while the GPU solves
         fiedler_vector(get_ctx(), rank, nranks, h, o, r.lambda, v, r.lanczos, &r.t_laplacian, &r.t_lanczos,
-                       start_kl_graph, &r.t_spmv_setup);
+                       start_kl_graph, &r.t_spmv_setup, !dev_split);
         if (rank != 0) {
             r.t_total = since(t0);
             return;
         }
+    }
+    if (o.eig == 1 && !dev_split) {
         const auto t = clk::now();
         std::vector<uint8_t> bits(static_cast<size_t>(n));
         chk(ek_median_split(n, v.data(), &r.median, bits.data()));
@@ -134,7 +141,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
             }
         });
         r.t_split = since(t);
-    } else {
+    } else if (o.eig != 1) {
         if (rank != 0) {  // the KL loop does not shard: other ranks have nothing to do
             r.t_total = since(t0);
             return;
@@ -164,10 +171,16 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     kg.get();  // graph and nets set up on the context (KL stream, synchronised)
     r.t_kl_graph_wait = since(t);
     t = clk::now();
-    chk(ek_kl_set_partition(ctx, order0.data(), int64_t(order0.size()), order1.data(), int64_t(order1.size())));
-    r.t_kl_setup = since(t);
+    int64_t n0 = int64_t(order0.size()), n1 = int64_t(order1.size());
+    if (dev_split) {
+        chk(ek_kl_set_partition_fiedler(ctx, &r.median, &n0, &n1));
+        r.t_split = since(t);  // (split and partition setup together)
+    } else {
+        chk(ek_kl_set_partition(ctx, order0.data(), n0, order1.data(), n1));
+        r.t_kl_setup = since(t);
+    }
     t = clk::now();
-    const int64_t lcap = int64_t(std::min(order0.size(), order1.size()));
+    const int64_t lcap = std::min(n0, n1);
     // the swap log goes straight into the caller's buffer when it holds the
     // whole run (no 32-B-per-node zeroed temporary and copy)
     dvec<ek_swap> own;

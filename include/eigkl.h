@@ -267,6 +267,13 @@ int ek_random_split(int64_t n, uint32_t seed, int32_t* order0, int32_t* order1);
 /* The -EIG branch of shuffleSparceMatrix (cKL.cpp:155-174): node i goes to
  * split[bits[i]] in ascending node order (the EIG file's line order). */
 int ek_kl_set_partition_bits(ek_ctx* ctx, int64_t n, const uint8_t* bits);
+/* The -EIG branch of ek_solve_file on the device: the median split of the
+ * Fiedler vector the last ek_lanczos_fiedler on this context returned (kept
+ * on the device, normalised and sign-fixed as v_out), with the remain[]
+ * lists in node order — the lists ek_median_split + ek_kl_set_partition_bits
+ * give on the host (cEIG.cpp:204-209 median, cKL.cpp:155-174 lists), without
+ * the vector's round trip.  median_out, n0_out, n1_out may be null. */
+int ek_kl_set_partition_fiedler(ek_ctx* ctx, double* median_out, int64_t* n0_out, int64_t* n1_out);
 /* Run the swap loop to termination on the device (one persistent
  * workgroup; no host round trip per iteration).  limit < 0: floor(log2 n)+5
  * (cKL.cpp:303).  log_out may be NULL. */

@@ -26,7 +26,7 @@ int ek_init(int, ek_ctx** out) {
 void ek_destroy(ek_ctx*) {}
 void ek_lanczos_default_opts(ek_lanczos_opts* o) {
     if (!o) return;
-    *o = ek_lanczos_opts{0, 1000, 1e-10, 1, 0, 1};
+    *o = ek_lanczos_opts{0, 1000, 1e-10, 1, 0, 1, 8};
 }
 int ek_spmv_setup(ek_ctx*, int64_t, int64_t, int64_t, const int32_t*, const int32_t*, const double*) {
     return absent("ek_spmv_setup");
@@ -40,5 +40,6 @@ int ek_lanczos_fiedler(ek_ctx*, const ek_lanczos_opts*, double*, double*, ek_lan
 int ek_kl_graph_setup(ek_ctx*, int64_t, const int32_t*, const int32_t*, const float*) { return absent("kl"); }
 int ek_kl_nets_setup(ek_ctx*, int64_t, const int64_t*, const int32_t*) { return absent("kl"); }
 int ek_kl_set_partition(ek_ctx*, const int32_t*, int64_t, const int32_t*, int64_t) { return absent("kl"); }
+int ek_kl_set_partition_fiedler(ek_ctx*, double*, int64_t*, int64_t*) { return absent("kl"); }
 int ek_kl_run(ek_ctx*, int32_t, ek_swap*, int64_t, ek_kl_result*) { return absent("kl"); }
 }

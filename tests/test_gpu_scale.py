@@ -132,3 +132,34 @@ def test_cli_random_init_matches_seeded_reference(tmp_path, name, seed):
     assert r.returncode == 0, r.stderr
     mine = (tmp_path / "results" / f"{name}.hgr_KL_CutSize_output.txt").read_text()
     compare_results_text(mine, open(os.path.join(GOLD, "ref_results_seed", f"{name}.seed{seed}.txt")).read())
+
+
+@pytest.mark.parametrize("case", ["syn1", "ibm01", "odd"])
+def test_device_fiedler_split_equals_host_split(ek, ctx, case):
+    """ek_kl_set_partition_fiedler (ek_solve_file's -EIG split on the device)
+    gives ek_median_split's median and the remain[] lists of
+    kl_set_partition_bits: same counts, same KL run (swap log and sides).
+    Cases: the 1x synthetic (disconnected: long runs of equal entries around
+    the median), ibm01, and an odd node count (the median is one entry)."""
+    if case == "syn1":
+        h = ek.Hypergraph.generate(1.0, 1)
+    elif case == "ibm01":
+        h = ek.Hypergraph.read(circuit_path("ibm01"))
+    else:
+        h = next(g for g in (ek.Hypergraph.generate(0.05, s).largest_component()[0] for s in range(3, 40))
+                 if g.nodes % 2 == 1)
+    lam, v, st, bits = _fiedler_bits(ek, ctx, h)
+    med_h, _ = ek.median_split(v)
+    ctx.kl_graph_setup(h.kl_graph())
+    ctx.kl_nets_setup(*h.pins())
+    ctx.kl_set_partition_bits(bits)
+    log_h, res_h = ctx.kl_run()
+    sides_h = ctx.kl_sides(0)
+    med_d, n0, n1 = ctx.kl_set_partition_fiedler()
+    assert med_d == med_h
+    assert (n0, n1) == (int(np.count_nonzero(bits == 0)), int(np.count_nonzero(bits)))
+    assert np.array_equal(ctx.kl_sides(0), sides_h)
+    log_d, res_d = ctx.kl_run()
+    swap_fields_equal(log_d, log_h)
+    for k in ("iterations", "best_iter", "initial_cut", "best_cut", "final_cut", "net_cut_best"):
+        assert res_d[k] == res_h[k], k
