@@ -107,6 +107,17 @@ __device__ __forceinline__ u64 wave_max_u64(u64 v) {
     return (u64(H) << 32) | wave_max32(hi == H ? lo : 0u);
 }
 
+// value of lane t of each 4-lane quad, in every lane of the quad (DPP
+// quad_perm [t,t,t,t]; t a compile-time constant once the caller is unrolled)
+__device__ __forceinline__ float quad_bcast(float v, int t) {
+    switch (t) {
+        case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x00, 0xf, 0xf, false));
+        case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x55, 0xf, 0xf, false));
+        case 2: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xAA, 0xf, 0xf, false));
+        default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xFF, 0xf, 0xf, false));
+    }
+}
+
 // uniform broadcast of lane `l` (v_readlane: no LDS round trip, unlike __shfl)
 __device__ __forceinline__ u64 readlane_u64(u64 v, int l) {
     const unsigned lo = __builtin_amdgcn_readlane(unsigned(v), l), hi = __builtin_amdgcn_readlane(unsigned(v >> 32), l);
@@ -665,30 +676,38 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     if (tid == 0 && (piece[0].x == -12345 || a.x == -12345)) s_stop[2] = 0;  // waits for the loads
                 }
                 stamp(10);
+                v2f ie_seg = {0.0f, 0.0f};  // SEGC: the row's inline-segment sums (internal, external)
                 if constexpr (SEGC) {
-                    // piece q = j8 + LPR*r holds entries 4q .. 4q+3: the same
-                    // (internal, external) pairs the plain segments stage, in
-                    // staging pieces 2q and 2q+1
+                    // piece q = j8 + LPR*r holds entries 4q .. 4q+3.  Each lane
+                    // decodes its entries' (internal, external) contributions;
+                    // the sums then run strictly in row order through the row's
+                    // quad of lanes: at step t (entries 4t .. 4t+3) the lane
+                    // holding them adds its four, and a DPP quad broadcast hands
+                    // the pair to the next step.  No LDS staging round trip.
                     const uint32_t cmask = (1u << d.wcolbits) - 1u;
+                    v2f cc[PPL][4];
 #pragma unroll
                     for (int r = 0; r < PPL; ++r) {
-                        const int q = j8 + LPR * r;
                         const uint32_t wv4[4] = {uint32_t(piece[r].x), uint32_t(piece[r].y), uint32_t(piece[r].z),
                                                  uint32_t(piece[r].w)};
-                        float wk[4];
-                        bool ek4[4];
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            wk[k] = s_wd[wv4[k] >> d.wcolbits];
-                            ek4[k] = side_now(int(wv4[k] & cmask));
+                            const float wk = s_wd[wv4[k] >> d.wcolbits];
+                            const bool ek = side_now(int(wv4[k] & cmask));
+                            cc[r][k] = v2f{ek ? 0.0f : wk, ek ? wk : 0.0f};
                         }
+                    }
+                    // a block of 4 entries no row of this wave reaches ends the
+                    // chain (the zero padding would add exact zeros)
+                    const int lenq = a.z;  // (the row's first lane; 0 in the others)
 #pragma unroll
-                        for (int h2 = 0; h2 < 2; ++h2)
-                            stage[srow * KL_STAGE_ROW + 2 * q + h2] = make_int4(
-                                __float_as_int(ek4[2 * h2] ? 0.0f : wk[2 * h2]),
-                                __float_as_int(ek4[2 * h2] ? wk[2 * h2] : 0.0f),
-                                __float_as_int(ek4[2 * h2 + 1] ? 0.0f : wk[2 * h2 + 1]),
-                                __float_as_int(ek4[2 * h2 + 1] ? wk[2 * h2 + 1] : 0.0f));
+                    for (int st = 0; st < 4 * PPL; ++st) {
+                        if (!__ballot(lenq > 4 * st)) break;
+                        v2f x = ie_seg;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) x += cc[st / 4][k];  // v_pk_add_f32, in row order
+                        ie_seg.x = quad_bcast(x.x, st % 4);
+                        ie_seg.y = quad_bcast(x.y, st % 4);
                     }
                 } else if (d.seg) {
                     // each lane looks up the sides of its own entries (4 LDS reads
@@ -709,7 +728,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 if (j8 != 0 || gi >= tot) continue;  // the row's first lane sums it
                 const int i = gi;
                 int4 sg[KL_SEG_LANES];  // per entry pair: (internal, external) contributions
-                if (SEGC || d.seg) {
+                if (!SEGC && d.seg) {
 #pragma unroll
                     for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[srow * KL_STAGE_ROW + j];
                 }
@@ -726,7 +745,11 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 {  // summed whether or not u is locked: a branch on `act` would let the
                    // compiler sink the segment loads behind the descriptor's round trip
                     int q = 0;
-                    if (SEGC || d.seg) {
+                    if constexpr (SEGC) {
+                        internal = ie_seg.x;
+                        external = ie_seg.y;
+                        q = 2 * KL_SEG_LANES;
+                    } else if (d.seg) {
                         // 8 entries per block; a block no row of this wave reaches
                         // is skipped as a whole (wave-uniform branch): the loop is
                         // issue-bound, and the zero padding would add exact zeros.
