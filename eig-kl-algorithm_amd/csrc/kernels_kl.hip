@@ -801,7 +801,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     const float g = external - internal;
                     const int s = ls;
                     (s ? d.gp1 : d.gp0)[pp] = g;
-                    kn = s ? key_min(g, pp) : key_max(g, pp);
+                    kn = key_max(s ? -g : g, pp);  // = key_min(g, pp) for list 1, without a branch
                     if (ab) {  // node1's / node2's chunk: resolved by G2a from this short list
                         const int slot = atomicAdd(&ab_cnt[s], 1);
                         if (slot < KL_AB_CAP) {
