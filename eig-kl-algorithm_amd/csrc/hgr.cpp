@@ -13,6 +13,7 @@
 #include <memory>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <random>
 
 #include "ek_internal.hpp"
@@ -43,10 +44,9 @@ inline bool parse_line(const char* p, const char* end, Emit&& emit) {
 }
 
 // the whole file (not zero-filled first: dvec leaves its elements uninitialised)
-ek::dvec<char> slurp(const char* path) {
+void slurp(const char* path, ek::dvec<char>& buf) {
     FILE* f = std::fopen(path, "rb");
     if (!f) ek::fail(EK_EIO, "cannot open %s: %s", path, std::strerror(errno));
-    ek::dvec<char> buf;
     std::fseek(f, 0, SEEK_END);
     const long sz = std::ftell(f);
     std::fseek(f, 0, SEEK_SET);
@@ -54,7 +54,20 @@ ek::dvec<char> slurp(const char* path) {
     const size_t got = sz > 0 ? std::fread(buf.data(), 1, size_t(sz), f) : 0;
     std::fclose(f);
     buf.resize(got);
-    return buf;
+}
+
+// The file buffer and the per-thread pin lists of ek_hgr_read, kept across
+// calls (a service re-reading circuits of similar size): fresh ones cost a
+// page fault per 4 KB on first touch, ~1 ms a read of the ibm18-shape file.
+// One caller at a time uses them; a concurrent read gets its own.
+struct ReadCache {
+    std::mutex mu;
+    ek::dvec<char> buf;
+    std::vector<ek::dvec<int32_t>> part;
+};
+ReadCache& read_cache() {
+    static ReadCache c;
+    return c;
 }
 
 // xoshiro256** seeded by splitmix64: the generator's only RNG (seeded, unlike
@@ -105,7 +118,12 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     EK_TRY
     if (!path || !out) ek::fail(EK_EINVAL, "ek_hgr_read: null argument");
     ek::PhaseTimer pt("hgr_read");
-    const ek::dvec<char> buf = slurp(path);
+    std::unique_lock<std::mutex> cache_lk(read_cache().mu, std::try_to_lock);
+    ek::dvec<char> own_buf;
+    std::vector<ek::dvec<int32_t>> own_part;
+    ek::dvec<char>& buf = cache_lk.owns_lock() ? read_cache().buf : own_buf;
+    std::vector<ek::dvec<int32_t>>& part = cache_lk.owns_lock() ? read_cache().part : own_part;
+    slurp(path, buf);
     pt.mark("slurp");
     const char* b = buf.empty() ? "" : buf.data();  // (memchr must not see a null pointer)
     const char* e = b + buf.size();
@@ -154,7 +172,8 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     for (int t = 0; t < T; ++t) lines[size_t(t) + 1] += lines[size_t(t)];
     pt.mark("lines");
     h->net_ptr.assign(size_t(nets) + 1, 0);
-    std::vector<ek::dvec<int32_t>> part(static_cast<size_t>(T));
+    if (part.size() < size_t(T)) part.resize(size_t(T));
+    for (int t = 0; t < T; ++t) part[size_t(t)].clear();  // (capacity kept)
     std::atomic<bool> bad{false};
     std::atomic<int64_t> bad_pin{-1};
     ek::run_threads(T, [&](int t) {
@@ -187,6 +206,9 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
         if (!part[size_t(t)].empty())
             std::memcpy(h->pins.data() + off[size_t(t)], part[size_t(t)].data(), part[size_t(t)].size() * 4);
     });
+    // (a file far smaller than the cached buffers would keep them: shrink
+    // what exceeds 4x this read's needs)
+    if (buf.capacity() > 4 * buf.size() + (size_t(1) << 20)) ek::dvec<char>().swap(buf);
     pt.mark("parse");
     *out = h.release();
     return EK_OK;

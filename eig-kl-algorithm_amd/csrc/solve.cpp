@@ -65,12 +65,15 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
     (void)rank;
     (void)nranks;
     auto t = clk::now();
+    // the KL adjacency's host thread starts first: the Laplacian rows are
+    // assembled on the GPU, and the adjacency (~25 ms on 12 threads) must
+    // finish within the Lanczos solve (~28 ms) not to stall the KL phase
+    if (after_laplacian) after_laplacian();
     // this rank's rows, assembled on the GPU from the pins into the SpMV's
     // coded form (the host build only as ek_spmv_setup_pins' fallback)
     chk(ek_spmv_setup_pins(ctx, n, h.nets, h.net_ptr.data(), h.pins.data(), nullptr));
     if (t_laplacian) *t_laplacian = since(t);
     if (t_spmv_setup) *t_spmv_setup = 0.0;
-    if (after_laplacian) after_laplacian();
     t = clk::now();
     // (host_v false: the vector stays on the device for ek_kl_set_partition_fiedler)
     if (host_v) v.assign(size_t(n), 0.0);
@@ -107,8 +110,8 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     const bool dev_split = o.eig == 1 && !(o.sign_ref && o.sign_ref[0]);
     std::vector<double> v;  // (host split only)
     if (o.eig == 1) {
-        // the KL adjacency starts once the Laplacian rows are built (both use
-        // every host thread), and runs while the GPU solves
+        // the KL adjacency starts on its host thread before the Laplacian
+        // rows are assembled on the GPU, and runs while the GPU solves
         fiedler_vector(get_ctx(), rank, nranks, h, o, r.lambda, v, r.lanczos, &r.t_laplacian, &r.t_lanczos,
                        start_kl_graph, &r.t_spmv_setup, !dev_split);
         if (rank != 0) {
