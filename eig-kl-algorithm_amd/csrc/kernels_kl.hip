@@ -33,6 +33,7 @@
 
 #include <cfloat>
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
@@ -1308,32 +1309,69 @@ bool kl_weight_codes(int64_t n, int64_t nnz, const int32_t* col, const float* w,
     if (wcolbits > 28) return false;
     const size_t max_codes = std::min<size_t>(size_t(1) << (32 - wcolbits), size_t(KL_WDICT_CAP));
     const size_t cap = 2 * size_t(KL_WDICT_CAP);  // power of two, at least twice the codes
-    std::vector<uint32_t> keys(cap);
-    std::vector<int32_t> slot(cap, -1);
-    auto find = [&](uint32_t k) -> size_t {
-        size_t h = size_t((k * 0x9E3779B1u) >> 19) & (cap - 1);
-        while (slot[h] >= 0 && keys[h] != k) h = (h + 1) & (cap - 1);
-        return h;
+    struct Table {  // open addressing over the fp32 bit patterns
+        std::vector<uint32_t> keys;
+        std::vector<int32_t> slot;
+        size_t cap;
+        explicit Table(size_t c) : keys(c), slot(c, -1), cap(c) {}
+        size_t find(uint32_t k) const {
+            size_t h = size_t((k * 0x9E3779B1u) >> 19) & (cap - 1);
+            while (slot[h] >= 0 && keys[h] != k) h = (h + 1) & (cap - 1);
+            return h;
+        }
     };
+    // 1. each thread's distinct weights (in first-occurrence order), in
+    // parallel; 2. their union, code 0 = 0.0f then in thread order; 3. every
+    // entry encoded in parallel.  The codes only index the table the swap
+    // loop decodes through, so their order does not change any result.
+    const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, nnz / 65536)));
+    std::vector<std::vector<uint32_t>> seen(static_cast<size_t>(T));
+    std::atomic<bool> over{false};
+    run_threads(T, [&](int t) {
+        Table loc(cap);
+        auto& sv = seen[size_t(t)];
+        for (int64_t p = nnz * t / T; p < nnz * (t + 1) / T && !over.load(std::memory_order_relaxed); ++p) {
+            uint32_t k;
+            std::memcpy(&k, &w[p], 4);
+            const size_t h = loc.find(k);
+            if (loc.slot[h] < 0) {
+                if (sv.size() >= max_codes) {
+                    over = true;
+                    break;
+                }
+                loc.slot[h] = int32_t(sv.size());
+                loc.keys[h] = k;
+                sv.push_back(k);
+            }
+        }
+    });
+    if (over) return false;
+    Table glob(cap);
     wdict.assign(1, 0.0f);
     {
-        const size_t h = find(0u);
-        slot[h] = 0;
-        keys[h] = 0u;
+        const size_t h = glob.find(0u);
+        glob.slot[h] = 0;
+        glob.keys[h] = 0u;
     }
-    kw.resize(size_t(std::max<int64_t>(nnz, 0)));
-    for (int64_t p = 0; p < nnz; ++p) {
-        uint32_t k;
-        std::memcpy(&k, &w[p], 4);
-        const size_t h = find(k);
-        if (slot[h] < 0) {
+    for (const auto& sv : seen)
+        for (const uint32_t k : sv) {
+            const size_t h = glob.find(k);
+            if (glob.slot[h] >= 0) continue;
             if (wdict.size() >= max_codes) return false;
-            slot[h] = int32_t(wdict.size());
-            keys[h] = k;
-            wdict.push_back(w[p]);
+            glob.slot[h] = int32_t(wdict.size());
+            glob.keys[h] = k;
+            float f;
+            std::memcpy(&f, &k, 4);
+            wdict.push_back(f);
         }
-        kw[size_t(p)] = (uint32_t(slot[h]) << wcolbits) | uint32_t(col[p]);
-    }
+    kw.resize(size_t(std::max<int64_t>(nnz, 0)));
+    run_threads(T, [&](int t) {
+        for (int64_t p = nnz * t / T; p < nnz * (t + 1) / T; ++p) {
+            uint32_t k;
+            std::memcpy(&k, &w[p], 4);
+            kw[size_t(p)] = (uint32_t(glob.slot[glob.find(k)]) << wcolbits) | uint32_t(col[p]);
+        }
+    });
     return true;
 }
 
