@@ -42,8 +42,11 @@
 #ifndef EK_KL_PREFETCH
 #define EK_KL_PREFETCH 1  // provisional next pair's rows touched into L2 across barrier 2 (0: off, for A/B)
 #endif
+#ifndef EK_E_TWO_TRIPS
+#define EK_E_TWO_TRIPS 1  // early rescans: gains, then the winner's descriptor (0: both in one trip, A/B; 2.03 vs 2.00 us/swap)
+#endif
 #ifndef EK_E_SLEEP
-#define EK_E_SLEEP 4  // early-rescan waves: s_sleep units before their loads (2: same, 8: +0.9 ms per solve)
+#define EK_E_SLEEP 0  // early-rescan waves: s_sleep units before their loads (two-trip rescans: 0 best, 4: +0.01 us/swap)
 #endif
 
 namespace ek {
@@ -360,6 +363,28 @@ __device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const 
     return m;
 }
 
+// chunk_rescan over one part: gains first, then the winner's descriptor (two
+// round trips, 2 KB a wave instead of 10 KB beside the gain waves' loads)
+template <int NQ>
+__device__ __forceinline__ u64 chunk_rescan2(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
+                                             int p0, int skip, int lane, KLInfo* info, bool* mine) {
+    float g[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) g[q] = gp[p0 + q * 64 + lane];
+    int bq;
+    const u64 k = lane_best<NQ>(g, s, p0, lane, skip, &bq);
+    const u64 m = wave_max_u64(k);
+    const u64 bal = __ballot(m != 0ull && k == m);  // keys carry the position: one lane at most
+    *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
+    KLInfo inf{0, 0, 0, 0};
+    if (bal && *mine) {
+        const int4 x = *reinterpret_cast<const int4*>(pinfo + p0 + bq * 64 + lane);
+        inf = KLInfo{x.x, x.y, x.z, x.w};
+    }
+    *info = inf;
+    return m;
+}
+
 // chunk_rescan with every position's descriptor loaded beside its gain: one
 // round trip instead of two (the early rescans run beside the gain updates and
 // must not outlast them)
@@ -628,13 +653,18 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // each taking a contiguous part of it
             const int s = wv <= W_EB ? 1 : 0, part = (s ? W_EB : W_EA) - wv;
             const int p0 = (s ? cB : cA) * KL_CHUNK + part * NQ_E * 64;
-            // let the gain-update waves' few row loads enter the CU's memory
-            // pipeline ahead of these 16 KB (they are on the critical path)
-            __builtin_amdgcn_s_sleep(EK_E_SLEEP);
+            // (with both trips' 2 KB a wave instead of 10 KB, the gain-update
+            // waves' row loads no longer need a head start: EK_E_SLEEP 0)
+            if constexpr (EK_E_SLEEP > 0) __builtin_amdgcn_s_sleep(EK_E_SLEEP);
             KLInfo info;
             bool mine;
+#if EK_E_TWO_TRIPS
+            const u64 kk = s ? chunk_rescan2<NQ_E>(d.gp1, d.pinfo1, 1, p0, posB, lane, &info, &mine)
+                             : chunk_rescan2<NQ_E>(d.gp0, d.pinfo0, 0, p0, posA, lane, &info, &mine);
+#else
             const u64 kk = s ? chunk_rescan1<NQ_E>(d.gp1, d.pinfo1, 1, p0, posB, lane, &info, &mine)
                              : chunk_rescan1<NQ_E>(d.gp0, d.pinfo0, 0, p0, posA, lane, &info, &mine);
+#endif
             if (mine) {
                 er_key[s * E_PARTS + part] = kk;
                 er_info[s * E_PARTS + part] = info;
