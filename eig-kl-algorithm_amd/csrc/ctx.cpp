@@ -1644,6 +1644,9 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
                 const double cyc_ns = ho.prof[15] ? double(ho.prof[15]) * 10.0 / double(ho.prof[14]) : 1.0 / 2.4;
                 const double f = 1e-3 * cyc_ns / double(std::max<long long>(1, ho.iterations));
                 std::fprintf(stderr, "[kl] per wave, us after its loop top: selection done / barrier 1 / G2a done / barrier 2:\n");
+                std::fprintf(stderr, "[kl] prefetch predicted node1 in %.1f %%, node2 in %.1f %% of swaps\n",
+                             100.0 * double(ho.warr[40]) / double(std::max<long long>(1, ho.iterations)),
+                             100.0 * double(ho.warr[41]) / double(std::max<long long>(1, ho.iterations)));
                 for (int w = 0; w < 8; ++w)
                     std::fprintf(stderr, "[kl]   w%d %.3f %.3f %.3f %.3f  (G2a reads consumed %.3f)\n", w,
                                  f * double(ho.warr[24 + w]), f * double(ho.warr[w]), f * double(ho.warr[16 + w]),

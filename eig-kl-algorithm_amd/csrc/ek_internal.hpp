@@ -340,9 +340,10 @@ struct KLOut {
     unsigned long long prof[16];  // EK_KL_PROF: [0..11] 100 MHz ticks per loop phase (thread 0's view)
                                   // or event counts x100, [14] shader cycles, [15] 100 MHz ticks of the loop;
                                   // [8] shader cycles, [9] 100 MHz ticks of the whole loop
-    unsigned long long warr[40];  // EK_KL_PROF: per wave, shader cycles from its loop top to its arrival
+    unsigned long long warr[42];  // EK_KL_PROF: per wave, shader cycles from its loop top to its arrival
                                   // at barrier 1 ([wave]) and barrier 2 ([8 + wave]), to the end of G2a
-                                  // ([16 + wave]), to the end of the selection ([24 + wave]) and to G2a's reads consumed ([32 + wave])
+                                  // ([16 + wave]), to the end of the selection ([24 + wave]) and to G2a's reads consumed ([32 + wave]);
+                                  // [40], [41]: swaps whose node1 / node2 the prefetch predicted
 };
 void kl_prepare(hipStream_t s, const KLDev& d);  // gains, initial cut, chunk keys
 // aux[p] = {col[p], nd[col[p]].{rowptr, len, plist}} for p < nnz (after the partition is set)

@@ -525,6 +525,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     int pf_col = 0;
     float pf_w = 0.0f;
     uint32_t pf_sink = 0u;
+    unsigned long long pf_hit_a = 0, pf_hit_b = 0;  // PROF
     const unsigned long long c_start = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const unsigned long long r_start = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
     auto stamp = [&](int ph) {
@@ -595,6 +596,12 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         const int cA = posA / KL_CHUNK, cB = posB / KL_CHUNK;
         const KLInfo ia = ci0[cA], ib = ci1[cB];
         const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
+        if constexpr (PROF && EK_KL_PREFETCH) {  // how often the provisional pair was the pair
+            if (wv == W_PF) {
+                pf_hit_a += __builtin_amdgcn_readlane(pf_inf.x, 0) == A && __builtin_amdgcn_readlane(pf_inf.z, 0) > 0;
+                pf_hit_b += __builtin_amdgcn_readlane(pf_inf.x, 32) == B && __builtin_amdgcn_readlane(pf_inf.z, 32) > 0;
+            }
+        }
         stamp(0);
         if constexpr (PROF) {
             if (A == -7) s_stop[2] = 0;  // keeps the descriptor read ahead of the stamp
@@ -1056,6 +1063,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         out->warr[16 + wv] = w_g2a;
         out->warr[24 + wv] = w_sel;
         out->warr[32 + wv] = w_g2r;
+        if (wv == W_PF) {
+            out->warr[40] = pf_hit_a;
+            out->warr[41] = pf_hit_b;
+        }
     }
     if (wv == W_W && lane == 0) {
         out->iterations = it;
