@@ -67,9 +67,14 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // which on freshly parsed arrays costs milliseconds; a memcpy into pinned
 // memory and an async DMA do not.  The caller sizes the arena for all the
 // uploads of one setup call and drains the stream before the next call.
+// The main stream and the KL stream each have an arena of their own: the KL
+// graph setup runs on ek_solve_file's host thread while the main thread
+// uploads the pins for the Laplacian build.
 struct Uploader {
     ek_ctx* c;
     hipStream_t s;
+    unsigned char*& buf;  // c->up (main stream) or c->kup (KL stream)
+    size_t& cap;
     size_t off = 0;
     Uploader(ek_ctx* ctx, hipStream_t st, size_t total);
     template <class T>
@@ -96,8 +101,10 @@ struct ek_ctx {
     void* host_user = nullptr;
     double* stage = nullptr;  // pinned staging of the host-staged exchange
     size_t stage_doubles = 0;
-    unsigned char* up = nullptr;  // pinned staging of the setup uploads (see Uploader)
+    unsigned char* up = nullptr;  // pinned staging of the setup uploads on `stream` (see Uploader)
     size_t up_bytes = 0;
+    unsigned char* kup = nullptr;  // ... and on `kstream`
+    size_t kup_bytes = 0;
     double comm_ms = 0.0;     // host-observed time inside collectives (current solve)
     // Laplacian rows owned by this context
     int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
@@ -133,14 +140,16 @@ struct ek_ctx {
     int64_t fied_n = 0;
 };
 
-Uploader::Uploader(ek_ctx* ctx, hipStream_t st, size_t total) : c(ctx), s(st) {
+Uploader::Uploader(ek_ctx* ctx, hipStream_t st, size_t total)
+    : c(ctx), s(st), buf(st == ctx->kstream ? ctx->kup : ctx->up), cap(st == ctx->kstream ? ctx->kup_bytes : ctx->up_bytes) {
     total = (total + 64) * 2;  // alignment slack
-    if (c->up_bytes < total) {
-        if (c->up) HIPCHK(hipHostFree(c->up));
-        c->up = nullptr;
-        c->up_bytes = 0;
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->up), total, hipHostMallocDefault));
-        c->up_bytes = total;
+    if (cap < total) {
+        // the arena's previous user drained its stream before returning
+        if (buf) HIPCHK(hipHostFree(buf));
+        buf = nullptr;
+        cap = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&buf), total, hipHostMallocDefault));
+        cap = total;
     }
 }
 
@@ -149,9 +158,9 @@ void Uploader::put(DBuf& d, const T* h, size_t n) {
     d.ensure(n * sizeof(T));
     if (!n) return;
     off = (off + 63) / 64 * 64;
-    if (off + n * sizeof(T) > c->up_bytes) ek::fail(EK_EINVAL, "upload staging overflow");
-    std::memcpy(c->up + off, h, n * sizeof(T));
-    HIPCHK(hipMemcpyAsync(d.p, c->up + off, n * sizeof(T), hipMemcpyHostToDevice, s));
+    if (off + n * sizeof(T) > cap) ek::fail(EK_EINVAL, "upload staging overflow");
+    std::memcpy(buf + off, h, n * sizeof(T));
+    HIPCHK(hipMemcpyAsync(d.p, buf + off, n * sizeof(T), hipMemcpyHostToDevice, s));
     off += n * sizeof(T);
 }
 
@@ -292,7 +301,11 @@ int ek_init(int device, ek_ctx** out) {
 void ek_destroy(ek_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    // drain every stream before anything it may still copy from is freed
+    // (an error exit can leave async copies of the pinned buffers queued)
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->kstream);
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {
@@ -300,14 +313,14 @@ void ek_destroy(ek_ctx* c) {
         if (c->chk_copied[i]) (void)hipEventDestroy(c->chk_copied[i]);
     }
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    (void)hipStreamDestroy(c->kstream);
+    (void)hipStreamDestroy(c->stream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
     if (c->q_pin) (void)hipHostFree(c->q_pin);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->up) (void)hipHostFree(c->up);
-    (void)hipStreamSynchronize(c->kstream);
-    (void)hipStreamDestroy(c->kstream);
-    (void)hipStreamDestroy(c->stream);
+    if (c->kup) (void)hipHostFree(c->kup);
     delete c;
 }
 
@@ -1298,6 +1311,10 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
         if (bad) ek::fail(EK_EINVAL, "ek_kl_graph_setup: column out of range");
     }
     hipStream_t s = c->kstream;
+    // not ready until this setup has finished: a failure part-way must not
+    // leave the previous graph's flags over this one's sizes
+    c->kl_graph_ready = false;
+    c->kl_part_ready = false;
     c->kl_n = n;
     c->kl_rowptr_h.assign(rowptr, rowptr + n + 1);
     Uploader up(c, s, (size_t(n) + 1) * 4 + size_t(nnz) * 8 + size_t(nnz) * 4);
@@ -1309,7 +1326,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     HIPCHK(hipMemsetAsync(c->kl_w.as<float>() + nnz, 0, 16 * 4, s));
     if (nnz) {
         // (the staging copies on the host threads: ~9 MB at ibm18 shape)
-        unsigned char* const dc = c->up + up.off;
+        unsigned char* const dc = up.buf + up.off;
         unsigned char* const dw = dc + size_t(nnz) * 4;
         ek::parallel_for(nnz, [&](int64_t lo, int64_t hi) {
             std::memcpy(dc + size_t(lo) * 4, col + lo, size_t(hi - lo) * 4);

@@ -38,16 +38,29 @@ void chk(int rc) {
 // runs the Lanczos solve on the main stream.  The host copy is freed here
 // too, off the solve's path (freeing ~10 MB that several threads touched
 // cost the solve's thread ~2.5 ms at the end of a step).
-void kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
-    PhaseTimer pt("kl_thread");
-    ThreadCap cap(threads);
-    ek_csr G;
-    build_kl_graph(*h, G);
-    pt.mark("graph built");
-    chk(ek_kl_graph_setup(ctx, h->nodes, G.rowptr.data(), G.col.data(), G.val32.data()));
-    pt.mark("graph set up");
-    chk(ek_kl_nets_setup(ctx, h->nets, h->net_ptr.data(), h->pins.data()));
-    pt.mark("nets set up");
+// Its errors come back as {status, message}: the message was written to this
+// thread's ek_last_error(), which the caller's thread cannot see.
+struct ThreadStatus {
+    int code = EK_OK;
+    std::string msg;
+};
+ThreadStatus kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
+    ThreadStatus st;
+    try {
+        PhaseTimer pt("kl_thread");
+        ThreadCap cap(threads);
+        ek_csr G;
+        build_kl_graph(*h, G);
+        pt.mark("graph built");
+        chk(ek_kl_graph_setup(ctx, h->nodes, G.rowptr.data(), G.col.data(), G.val32.data()));
+        pt.mark("graph set up");
+        chk(ek_kl_nets_setup(ctx, h->nets, h->net_ptr.data(), h->pins.data()));
+        pt.mark("nets set up");
+    } catch (...) {
+        st.code = guard_exceptions();
+        st.msg = ek_last_error();
+    }
+    return st;
 }
 
 // the results file's text buffer, kept across calls (one caller at a time)
@@ -107,7 +120,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     if (n < 2) fail(EK_EINVAL, "%s: %lld nodes, nothing to partition", base.c_str(), (long long)n);
     // initial partition (shuffleSparceMatrix, cKL.cpp:151-197)
     std::vector<int32_t> order0, order1;
-    std::future<void> kg;
+    std::future<ThreadStatus> kg;
     // while the GPU solves, the KL adjacency leaves the solve's host thread
     // (and the HIP runtime's) a few cores
     auto start_kl_graph = [&] {
@@ -182,7 +195,9 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     }
     ek_ctx* ctx = get_ctx();
     auto t = clk::now();
-    kg.get();  // graph and nets set up on the context (KL stream, synchronised)
+    // graph and nets set up on the context (KL stream, synchronised); a
+    // failure there is re-raised here with its message
+    if (const ThreadStatus st = kg.get(); st.code != EK_OK) fail(st.code, "KL graph setup: %s", st.msg.c_str());
     r.t_kl_graph_wait = since(t);
     t = clk::now();
     int64_t n0 = int64_t(order0.size()), n1 = int64_t(order1.size());

@@ -225,6 +225,32 @@ def test_lanczos_golden(ek, ctx, name, deflate, reorth):
     assert abs(np.linalg.norm(v) - 1) < 1e-12 and abs(v.sum()) < 1e-8
 
 
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2", "ibm10"])
+def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
+    """The mid-cycle convergence test (check_every > 0) may stop a cycle early
+    and take the Ritz pair from a j < ncv projection; check_every=0 is
+    Spectra's end-of-cycle-only test.  Both must give the same median split
+    wherever the entry is not within 1e-8 of the median, and both must meet
+    the golden's tolerances (ibm10's golden is unconverged: residual only)."""
+    h = ek.Hypergraph.read(circuit_path(name))
+    L = h.laplacian()
+    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    lam_a, v_a, st_a = ctx.lanczos_fiedler(check_every=8)
+    lam_b, v_b, st_b = ctx.lanczos_fiedler(check_every=0)
+    assert st_a["converged"] and st_b["converged"]
+    assert st_a["residual"] < 1e-9 and st_b["residual"] < 1e-9
+    assert abs(lam_a - lam_b) <= 1e-10
+    v_b = v_b * np.sign(v_a @ v_b)
+    assert np.abs(v_a - v_b).max() <= 1e-8
+    med_a, bits_a = ek.median_split(v_a)
+    med_b, bits_b = ek.median_split(v_b)
+    mask = (np.abs(v_a - med_a) > 1e-8) & (np.abs(v_b - med_b) > 1e-8)
+    assert np.array_equal(bits_a[mask], bits_b[mask])
+    if name != "ibm10":
+        lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
+        _fiedler_parity(name, lam_b, v_b, lam_ref, med_ref, bits_ref, v_ref, ek)
+
+
 def test_lanczos_multirank_step_sequence_on_one_gpu(ek, tmp_path):
     """The step sequence the sharded path runs (separate alpha / projection /
     finalize launches with the all-reduce points between them; RCCL is a no-op

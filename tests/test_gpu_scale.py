@@ -97,6 +97,35 @@ def test_solve_file_equals_resident_path(ek, ctx, tmp_path):
     assert rows[-1] == f"{log[-1]['iter']}\t{float(log[-1]['cut']):g}\t{float(log[-1]['gain']):g}"
 
 
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
+def test_solve_file_fresh_context_small(ek, tmp_path, name):
+    """ek_solve_file -EIG on a FRESH context (no pinned staging yet) with a
+    small circuit: the KL graph thread (KL stream) and the pins upload (main
+    stream) run at once and each stage through their own pinned arena.  The
+    results file must equal the reference cKL's from the golden split, and
+    two more solves on the same context must repeat it byte for byte."""
+    import shutil
+    from conftest import eig_path, ref_results_path
+    shutil.copy(circuit_path(name), tmp_path)
+    os.makedirs(tmp_path / "pre_saved_EIG")
+    shutil.copy(eig_path(name), tmp_path / "pre_saved_EIG")
+    out = tmp_path / "results" / f"{name}.hgr_KL_CutSize_EIG_output.txt"
+    # odd n (fract, industry2): the golden's sign fixes which half is larger
+    # (host split); even n (ibm01): the device split
+    sign_ref = str(tmp_path / "pre_saved_EIG" / f"{name}.hgr_out.txt") if name != "ibm01" else None
+    c = ek.Context(0)
+    try:
+        texts = []
+        for _ in range(3):
+            r, _ = c.solve_file(str(tmp_path / f"{name}.hgr"), eig=1, out_dir=str(tmp_path), sign_ref=sign_ref)
+            assert r["kl"]["iterations"] > 0
+            texts.append(out.read_text())
+        compare_results_text(texts[0], open(ref_results_path(name)).read())
+        assert texts[1] == texts[0] and texts[2] == texts[0]
+    finally:
+        c.close()
+
+
 def test_lcc_fiedler_and_kl_vs_reference(ek, oracle, ctx):
     d = os.path.join(GOLD, "syn1_lcc")
     meta = json.load(open(os.path.join(d, "meta.json")))
