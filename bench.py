@@ -215,7 +215,8 @@ def main():
               ("t_read", "t_laplacian", "t_spmv_setup", "t_lanczos", "t_split", "t_kl_graph_wait", "t_kl_setup",
                "t_kl", "t_write", "t_total")}
     phases["lanczos_device_ms"] = round(float(np.median([x["total_ms"] for x in lz])), 3)
-    row0, nrows, _ = ek.shard_rows(n, world, rank)
+    off = ek.shard_map(h, world)  # the nnz-balanced map ek_solve_file's device build used
+    row0, nrows = int(off[rank]), int(off[rank + 1] - off[rank])
     alg_bytes = ctx.spmv_bytes(fused=False)  # 12 nnz + 4(nrows+1) + 8n (x) + 8 nrows (y)
     fused_bytes = ctx.spmv_bytes(fused=True)  # + the fused epilogue's f read and basis-column write
     packed, stored = ctx.spmv_format(fused=True)
@@ -262,11 +263,9 @@ def main():
     if not args.no_extras:
         h10 = ek.Hypergraph.generate(10.0, 10)
         n10 = h10.nodes
-        r0, nr, _ = ek.shard_rows(n10, world, rank)
         c10 = ctx
-        L10 = h10.laplacian_rows(r0, r0 + nr)
-        c10.spmv_setup(n10, r0, L10.rowptr, L10.col, L10.val)
-        del L10
+        c10.spmv_setup_pins(h10)  # this rank's nnz-balanced rows, built on the device
+        _, r0, nr = c10.spmv_dims()
         st10 = None
         tt = []
         for i in range(2):

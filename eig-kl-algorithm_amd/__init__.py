@@ -48,7 +48,7 @@ class LanczosOpts(ctypes.Structure):
 class LanczosStats(ctypes.Structure):
     _fields_ = [("restarts", _I32), ("matvecs", _I32), ("converged", _I32), ("residual", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double), ("spmv_timed", _I32),
-                ("comm_ms", ctypes.c_double)]
+                ("comm_ms", ctypes.c_double), ("allgathers", _I32), ("allreduces", _I32)]
 
 
 class KLResult(ctypes.Structure):
@@ -103,6 +103,7 @@ _sig("ek_csr_copy", ctypes.c_int, _P, _P, _P, _P, _P)
 _sig("ek_csr_free", None, _P)
 _sig("ek_shard_rows", ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I64),
      ctypes.POINTER(_I64), ctypes.POINTER(_I64))
+_sig("ek_shard_map", ctypes.c_int, _I64, _I64, _P, _P, ctypes.c_int, _P)
 _sig("ek_device_count", ctypes.c_int, ctypes.POINTER(ctypes.c_int))
 _sig("ek_init", ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P))
 _sig("ek_destroy", None, _P)
@@ -276,6 +277,16 @@ def shard_rows(n, nranks, rank):
     _chk(_lib.ek_shard_rows(int(n), int(nranks), int(rank), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
          "shard_rows")
     return a.value, b.value, c.value
+
+
+def shard_map(hgr, nranks):
+    """nnz-balanced row offsets (nranks + 1) of the sharded Lanczos (ek_shard_map): rank r owns
+    [off[r], off[r+1]); the map ek_spmv_setup_pins uses."""
+    net_ptr, pins = hgr.pins()
+    off = np.empty(int(nranks) + 1, np.int64)
+    _chk(_lib.ek_shard_map(int(hgr.nodes), len(net_ptr) - 1, _p(net_ptr), _p(pins), int(nranks), _p(off)),
+         "shard_map")
+    return off
 
 
 def median_split(v):

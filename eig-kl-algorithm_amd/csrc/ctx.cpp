@@ -106,8 +106,16 @@ struct ek_ctx {
     unsigned char* kup = nullptr;  // ... and on `kstream`
     size_t kup_bytes = 0;
     double comm_ms = 0.0;     // host-observed time inside collectives (current solve)
-    // Laplacian rows owned by this context
+    int64_t n_ag = 0, n_ar = 0;  // collectives issued (current solve; sharded contexts)
+    // Laplacian rows owned by this context.  Sharded: rank r owns
+    // [shard_off[r], shard_off[r+1]) (nnz-balanced, so the slices differ);
+    // nloc = the largest slice; each rank's f is all-gathered into a slot of
+    // `slot` doubles (its rows, zero padding, its ||f||^2 partial at [ldv]),
+    // and the matrix's columns are remapped to that padded layout.
     int64_t n = 0, row0 = 0, nrows = 0, nloc = 0, nnz = 0;
+    std::vector<int64_t> shard_off;
+    int64_t slot = 0;
+    DBuf off_d, xexp;
     int block_nnz = 1024, nrb_spmv = 0;
     DBuf rb, rowptr, col, val, pk, rel, dict;
     int colbits = 0;  // > 0: the dictionary-coded matrix (pk, dict) is the one the SpMV reads
@@ -224,6 +232,7 @@ namespace {
 // operand staged through pinned memory around the caller's collective.
 void allreduce(ek_ctx* c, double* p, size_t count) {
     if (c->nranks <= 1 || !count) return;
+    ++c->n_ar;
     if (c->comm) {
         NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, c->comm, c->stream));
         return;
@@ -239,6 +248,7 @@ void allreduce(ek_ctx* c, double* p, size_t count) {
 
 // recv[r*count .. (r+1)*count) = rank r's send block (rank-major), on the stream.
 void allgather(ek_ctx* c, const double* send, size_t count, double* recv) {
+    ++c->n_ag;
     if (c->comm) {
         NCCLCHK(ncclAllGather(send, recv, count, ncclDouble, c->comm, c->stream));
         return;
@@ -383,14 +393,53 @@ int ek_comm_init_host(ek_ctx* c, int nranks, int rank, ek_allgather_fn ag, ek_al
     EK_CATCH
 }
 
-// ---------------------------------------------------------------------------
-// SpMV seam (SparseSymMatProd::perform_op, cEIG.cpp:194)
-int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr, const int32_t* col,
-                  const double* val) {
-    EK_TRY
-    check_ctx(c);
-    if (n <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > n || !rowptr || (nrows && (!col || !val)))
-        ek::fail(EK_EINVAL, "ek_spmv_setup: bad argument");
+}  // extern "C"
+
+namespace {
+
+inline int64_t gt_round(int64_t x) { return round_up(std::max<int64_t>(x, 1), ek::dev::GT_ROWS); }
+
+// The shard map `off` (nranks + 1 offsets tiling [0, n)) becomes the
+// context's: its rows, the largest slice (nloc) and the all-gather slot.
+void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
+    if (int(off.size()) != c->nranks + 1 || off[0] != 0 || off.back() != n)
+        ek::fail(EK_EINVAL, "shard map does not tile [0, %lld)", (long long)n);
+    int64_t mx = 0;
+    for (int r = 0; r < c->nranks; ++r) {
+        if (off[size_t(r) + 1] < off[size_t(r)]) ek::fail(EK_EINVAL, "shard map not monotone");
+        mx = std::max(mx, off[size_t(r) + 1] - off[size_t(r)]);
+    }
+    c->shard_off = off;
+    c->row0 = off[size_t(c->rank)];
+    c->nrows = off[size_t(c->rank) + 1] - c->row0;
+    c->nloc = c->nranks > 1 ? mx : n;
+    // sharded: the Lanczos vectors' rows (ldv) + 64, the rank's ||f||^2 at [ldv]
+    c->slot = c->nranks > 1 ? gt_round(mx) + 64 : n;
+    if (c->nranks > 1 && c->slot * c->nranks > INT32_MAX) ek::fail(EK_EINVAL, "sharded vector layout exceeds int32");
+}
+
+// The column space the SpMV reads: global ids, or the padded all-gather layout
+int64_t x_extent(const ek_ctx* c) { return c->nranks > 1 ? c->slot * c->nranks : c->n; }
+
+// Global column -> the all-gather layout (host copy of k_remap_cols)
+void remap_cols_host(const ek_ctx* c, const int32_t* col, int64_t nnz, std::vector<int32_t>& out) {
+    out.resize(size_t(nnz));
+    const auto& off = c->shard_off;
+    ek::parallel_for(nnz, [&](int64_t lo, int64_t hi) {
+        for (int64_t p = lo; p < hi; ++p) {
+            const int64_t g = col[p];
+            const int r = int(std::upper_bound(off.begin() + 1, off.end() - 1, g) - (off.begin() + 1));
+            out[size_t(p)] = int32_t(r * c->slot + (g - off[size_t(r)]));
+        }
+    });
+}
+
+// ek_spmv_setup's body, the shard map given (no collective: also the
+// device build's host fallback, which one rank may take alone)
+void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, const int32_t* rowptr, const int32_t* col,
+                     const double* val) {
+    set_shard(c, n, off);
+    const int64_t nrows = c->nrows;
     if (rowptr[0] != 0) ek::fail(EK_EINVAL, "ek_spmv_setup: rowptr[0] must be 0 (local rows)");
     ek::PhaseTimer pt("spmv_setup");
     const int64_t nnz = rowptr[nrows];
@@ -398,15 +447,12 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
         if (rowptr[r + 1] < rowptr[r]) ek::fail(EK_EINVAL, "ek_spmv_setup: rowptr not monotone");
     for (int64_t p = 0; p < nnz; ++p)
         if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup: column %d out of range", col[p]);
-    int64_t row0_expect = 0, nrows_expect = 0, nloc = 0;
-    ek_shard_rows(n, c->nranks, c->rank, &row0_expect, &nrows_expect, &nloc);
-    if (c->nranks > 1 && (row0 != row0_expect || nrows != nrows_expect))
-        ek::fail(EK_EINVAL, "ek_spmv_setup: rank %d must own rows [%lld,+%lld) (ek_shard_rows)", c->rank,
-                 (long long)row0_expect, (long long)nrows_expect);
+    std::vector<int32_t> colx;  // sharded: the columns in the all-gather layout
+    if (c->nranks > 1) {
+        remap_cols_host(c, col, nnz, colx);
+        col = colx.data();
+    }
     c->n = n;
-    c->row0 = row0;
-    c->nrows = nrows;
-    c->nloc = c->nranks > 1 ? nloc : n;
     c->nnz = nnz;
     // dictionary-coded entries unless EK_SPMV_PLAIN is set or the values do not fit
     std::vector<uint32_t> pkv;
@@ -414,7 +460,8 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     int colbits = 0;
     const char* plain = std::getenv("EK_SPMV_PLAIN");
     pt.mark("validate");
-    const bool packed = !(plain && plain[0] && plain[0] != '0') && ek::dev::spmv_pack(n, nnz, col, val, pkv, dictv, colbits);
+    const bool packed = !(plain && plain[0] && plain[0] != '0') &&
+                        ek::dev::spmv_pack(x_extent(c), nnz, col, val, pkv, dictv, colbits);
     pt.mark("pack");
     // 512-nnz blocks (tools/spmv_lab.hip for plain CSR; for the coded form,
     // 1024-nnz segments measured 14.3 against 12.7 us inside the solve)
@@ -447,6 +494,45 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     upload(c->rb, rbv.data(), rbv.size(), c->stream);
     HIPCHK(hipStreamSynchronize(c->stream));
     pt.mark("upload");
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// SpMV seam (SparseSymMatProd::perform_op, cEIG.cpp:194)
+// Sharded: the ranks' row ranges are learned with one all-gather of
+// (row0, nrows) over the comm seam and must tile [0, n) in rank order (equal
+// blocks from ek_shard_rows or the nnz-balanced ek_shard_map alike).
+int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr, const int32_t* col,
+                  const double* val) {
+    EK_TRY
+    check_ctx(c);
+    if (n <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > n || !rowptr || (nrows && (!col || !val)))
+        ek::fail(EK_EINVAL, "ek_spmv_setup: bad argument");
+    std::vector<int64_t> off{0, n};
+    if (c->nranks > 1) {
+        c->scal.ensure(64);
+        c->xexp.ensure(size_t(2 * c->nranks) * 8);
+        const double mine[2] = {double(row0), double(nrows)};
+        HIPCHK(hipMemcpyAsync(c->scal.p, mine, 16, hipMemcpyHostToDevice, c->stream));
+        allgather(c, c->scal.as<double>(), 2, c->xexp.as<double>());
+        std::vector<double> all(size_t(2 * c->nranks));
+        HIPCHK(hipMemcpyAsync(all.data(), c->xexp.p, all.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        off.assign(size_t(c->nranks) + 1, 0);
+        for (int r = 0; r < c->nranks; ++r) {
+            if (int64_t(all[size_t(2 * r)]) != off[size_t(r)])
+                ek::fail(EK_EINVAL, "ek_spmv_setup: rank %d's rows start at %lld, not where rank %d's end (%lld)", r,
+                         (long long)all[size_t(2 * r)], r - 1, (long long)off[size_t(r)]);
+            off[size_t(r) + 1] = off[size_t(r)] + int64_t(all[size_t(2 * r) + 1]);
+        }
+        if (off.back() != n) ek::fail(EK_EINVAL, "ek_spmv_setup: the ranks' rows cover %lld of %lld", (long long)off.back(), (long long)n);
+    } else if (row0 != 0 || nrows != n) {
+        ek::fail(EK_EINVAL, "ek_spmv_setup: a single context owns all %lld rows", (long long)n);
+    }
+    spmv_setup_rows(c, n, off, rowptr, col, val);
     return EK_OK;
     EK_CATCH
 }
@@ -475,8 +561,15 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         if (k < 0) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: net_ptr not monotone");
         if (k >= 2) raw_bound += k * (k - 1);
     }
-    int64_t row0 = 0, nrows = n, nloc = n;
-    ek_shard_rows(n, c->nranks, c->rank, &row0, &nrows, &nloc);
+    // this rank's rows: the nnz-balanced shard map, computed from the pins
+    // identically on every rank (no collective)
+    std::vector<int64_t> off(size_t(c->nranks) + 1, 0);
+    off[1] = n;
+    if (c->nranks > 1) {
+        const int rc = ek_shard_map(n, nets, net_ptr, pins, c->nranks, off.data());
+        if (rc != EK_OK) throw ek::Error{rc};
+    }
+    const int64_t row0 = off[size_t(c->rank)], nrows = off[size_t(c->rank) + 1] - row0;
     ek::PhaseTimer pt("spmv_setup_pins");
     hipStream_t s = c->stream;
     auto host_fallback = [&](const char* why) {
@@ -488,8 +581,7 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         h.pins.assign(pins, pins + npins);
         ek_csr L;
         ek::build_laplacian_rows(h, row0, row0 + nrows, L);
-        const int rc = ek_spmv_setup(c, n, row0, nrows, L.rowptr.data(), L.col.data(), L.val64.data());
-        if (rc != EK_OK) throw ek::Error{rc};
+        spmv_setup_rows(c, n, off, L.rowptr.data(), L.col.data(), L.val64.data());
         if (on_device) *on_device = 0;
     };
     if (std::getenv("EK_HOST_LAPLACIAN")) {
@@ -572,14 +664,17 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         return EK_OK;
     }
     const int64_t nnz = rowptr[nr];
+    set_shard(c, n, off);
     c->n = n;
-    c->row0 = row0;
-    c->nrows = nrows;
-    c->nloc = c->nranks > 1 ? nloc : n;
     c->nnz = nnz;
+    const std::vector<long long> offll(off.begin(), off.end());  // (alive until the stream is drained below)
+    if (c->nranks > 1) {  // global columns -> the all-gather layout (monotone: rows stay sorted)
+        upload(c->off_d, offll.data(), offll.size(), s);
+        ek::dev::remap_cols(s, nnz, c->col.as<int>(), c->off_d.as<long long>(), c->nranks, c->slot);
+    }
     // the same greedy row blocks as the host path (ek_spmv_setup)
     int colbits = 1;
-    while (colbits < 31 && (int64_t(1) << colbits) < n) ++colbits;
+    while (colbits < 31 && (int64_t(1) << colbits) < x_extent(c)) ++colbits;
     const char* plain_env = std::getenv("EK_SPMV_PLAIN");
     bool packed = !(plain_env && plain_env[0] && plain_env[0] != '0') && colbits <= 28;
     int64_t ncodes = 0;
@@ -632,12 +727,25 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
     EK_CATCH
 }
 
+// x is the global n-vector; a sharded context reads it through its padded
+// all-gather layout, so the ranks' slices are copied into that first
 int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
     EK_TRY
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv before ek_spmv_setup");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-    ek::dev::spmv(s, spmv_mat(c), x, y, nullptr, nullptr, nullptr, nullptr);
+    const double* xs = x;
+    if (c->nranks > 1) {
+        c->xexp.ensure(size_t(x_extent(c)) * 8);
+        for (int r = 0; r < c->nranks; ++r) {
+            const int64_t a = c->shard_off[size_t(r)], b = c->shard_off[size_t(r) + 1];
+            if (b > a)
+                HIPCHK(hipMemcpyAsync(c->xexp.as<double>() + r * c->slot, x + a, size_t(b - a) * 8,
+                                      hipMemcpyDeviceToDevice, s));
+        }
+        xs = c->xexp.as<double>();
+    }
+    ek::dev::spmv(s, spmv_mat(c), xs, y, nullptr, nullptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
     return EK_OK;
     EK_CATCH
@@ -648,7 +756,14 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_host before ek_spmv_setup");
     DBuf dx, dy;
-    upload(dx, x, size_t(c->n), c->stream);
+    std::vector<double> xp;  // sharded: the padded all-gather layout
+    if (c->nranks > 1) {
+        xp.assign(size_t(x_extent(c)), 0.0);
+        for (int r = 0; r < c->nranks; ++r)
+            std::copy(x + c->shard_off[size_t(r)], x + c->shard_off[size_t(r) + 1], xp.begin() + r * c->slot);
+        x = xp.data();
+    }
+    upload(dx, x, size_t(x_extent(c)), c->stream);
     dy.ensure(size_t(std::max<int64_t>(c->nrows, 1)) * 8);
     ek::dev::spmv(c->stream, spmv_mat(c), dx.as<double>(), dy.as<double>(), nullptr, nullptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
@@ -767,10 +882,11 @@ struct Lanczos {
     double* V() { return c->V.as<double>(); }
     double* col(int j) { return V() + size_t(j) * ldv; }
 
-    // x for the matvec: the full vector (gathered when sharded)
+    // x for the matvec: the full vector (gathered when sharded, in the padded
+    // slot layout the matrix's columns were remapped to)
     const double* gather_f() {
         if (c->nranks == 1) return c->f.as<double>();
-        allgather(c, c->f.as<double>(), size_t(c->nloc), c->xfull.as<double>());
+        allgather(c, c->f.as<double>(), size_t(c->slot), c->xfull.as<double>());
         return c->xfull.as<double>();
     }
 
@@ -792,41 +908,20 @@ struct Lanczos {
     // steps [k, kend) of a run that started at seg0 (the driver enqueues a
     // cycle in chunks to check convergence between them)
     void factorize(int k, int kend) {
-        // EK_LANCZOS_UNFUSED: run the multi-rank step sequence on one GPU (tests)
+        // EK_LANCZOS_UNFUSED: run the sharded step sequence on one GPU (tests)
         static const bool unfused = std::getenv("EK_LANCZOS_UNFUSED") != nullptr;
-        if (c->nranks == 1 && reorth == 1 && !unfused) return factorize_fused(k, kend);
+        if (reorth == 1) {
+            if (c->nranks == 1 && !unfused) return factorize_fused(k, kend);
+            return factorize_mr(k, kend);
+        }
         double* fn2 = c->fn2.as<double>();
-        for (int i = k; i < kend; ++i) {
+        for (int i = k; i < kend; ++i) {  // reorth 2: CGS2 from the matvec
             const double* x = gather_f();
             const bool timed = spmv_timed_step(i);
-            ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
-                          reorth == 1 ? c->apart.as<double>() : nullptr, nullptr,
+            ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i), nullptr, nullptr,
                           timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
             ++matvecs;
             const int nc = i + 1, tot = nc + has_u0;
-            if (reorth == 1) {
-                double* a3 = c->scal.as<double>() + 2;
-                const double* bov = c->bov.as<double>() + i;
-                if (c->nranks == 1) {
-                    ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
-                                        i > 0 ? col(i - 1) : nullptr, fn2 + i, bov, c->f.as<double>());
-                } else {
-                    ek::dev::finalize_step(s, c->apart.as<double>(), c->nrb_spmv, a3, nullptr, nullptr, -1, nullptr,
-                                           nullptr);
-                    allreduce(c, a3, 1);
-                    ek::dev::three_term(s, ldv, nullptr, 0, a3, c->w.as<double>(), col(i),
-                                        i > 0 ? col(i - 1) : nullptr, fn2 + i, bov, c->f.as<double>());
-                }
-                ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
-                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot, c->h2.as<double>());
-                allreduce(c, c->h2.as<double>(), size_t(tot));
-                ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>());
-                ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + i + 1, nullptr, c->h2.as<double>(), i,
-                                       c->alpha.as<double>(), c->offd.as<double>(), a3, fn2 + i, bov);
-                allreduce(c, fn2 + i + 1, 1);
-                continue;
-            }
             ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), c->part.as<double>());
             ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot, c->h1.as<double>());
             allreduce(c, c->h1.as<double>(), size_t(tot));
@@ -841,6 +936,56 @@ struct Lanczos {
                                    c->h2.as<double>(), i, c->alpha.as<double>(), c->offd.as<double>());
             allreduce(c, fn2 + i + 1, 1);
         }
+        HIPCHK(hipGetLastError());
+    }
+
+    // The sharded step (reorth 1), ONE all-gather and ONE all-reduce:
+    //  1. the rank's ||f||^2 partial goes into its all-gather slot (f[ldv]);
+    //  2. all-gather f -> x (every rank's rows + every rank's ||f||^2);
+    //  3. SpMV on the owned rows; its prologue sums the ranks' ||f||^2 in rank
+    //     order (the same bits on every rank): w = L f/||f||, v_i = f/||f||;
+    //  4. gemvt3: V^T w, V^T v_i, V^T v_{i-1} in one sweep of V;
+    //  5. ONE all-reduce of the three column-sum vectors;
+    //  6. update_mr: alpha = (V^T w)_i, f' = w - alpha v_i - beta v_{i-1},
+    //     h = V^T w - alpha V^T v_i - beta V^T v_{i-1} (= V^T f'),
+    //     f = f' - V h, and H's alpha[i], offd[i].
+    // The single-GPU step reduces alpha before forming f' and projects f'
+    // itself (two dependent reductions); here V^T f' comes from the linearity
+    // of the projection, computed from the same sweep, so its error is
+    // eps ||w|| instead of eps ||f'|| (the orthogonality of f to V is then a
+    // few ulps x ||w||/||f||; it does not compound, because f' is still formed
+    // by direct subtraction).  Not bit-identical to the single-GPU step; within
+    // the Fiedler tolerances on every golden (tests).
+    void factorize_mr(int k, int kend) {
+        double* fn2 = c->fn2.as<double>();
+        double* f = c->f.as<double>();
+        const bool sharded = c->nranks > 1;
+        for (int i = k; i < kend; ++i) {
+            ek::dev::finalize_step(s, c->npart.as<double>(), nub, f + ldv, nullptr, nullptr, -1, nullptr, nullptr);
+            const double* x = f;
+            if (sharded) {
+                allgather(c, f, size_t(c->slot), c->xfull.as<double>());
+                x = c->xfull.as<double>();
+            }
+            ek::dev::StepFin fin;
+            fin.npart = x + ldv;
+            fin.nb = c->nranks;
+            fin.nstride = int(c->slot);
+            fin.fn2_out = fn2 + i;
+            const bool timed = spmv_timed_step(i);
+            ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), nullptr, f, col(i), nullptr, &fin,
+                          timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
+            ++matvecs;
+            const int nc = i + 1, tot = nc + has_u0;
+            ek::dev::gemvt3(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), col(i),
+                            i > 0 ? col(i - 1) : col(i), c->part.as<double>());
+            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, 3 * tot, c->h2.as<double>());
+            allreduce(c, c->h2.as<double>(), size_t(3 * tot));
+            ek::dev::update_mr(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->w.as<double>(), col(i),
+                               i > 0 ? col(i - 1) : nullptr, fn2 + i, c->bov.as<double>() + i, f,
+                               c->npart.as<double>(), c->alpha.as<double>(), c->offd.as<double>());
+        }
+        if (kend == m) reduce_scalar(fn2 + m);  // the cycle's last residual norm
         HIPCHK(hipGetLastError());
     }
 
@@ -950,6 +1095,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     if (opts) o = *opts;
     const auto t0 = std::chrono::steady_clock::now();
     c->comm_ms = 0.0;
+    c->n_ag = c->n_ar = 0;
     const int64_t n = c->n;
     const bool deflate = o.deflate != 0;
     const int nev = deflate ? 1 : 2;
@@ -979,12 +1125,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);
     c->Vn.ensure(ldv * size_t(m + 1) * 8);
-    c->f.ensure(ldv * 8);
+    // f: + 64 (the sharded step's all-gather slot carries the rank's ||f||^2 at [ldv])
+    if (c->nranks > 1 && c->slot != int64_t(ldv) + 64) ek::fail(EK_ESTATE, "shard slot %lld != ldv + 64", (long long)c->slot);
+    c->f.ensure((ldv + 64) * 8);
     c->w.ensure(ldv * 8);
-    if (c->nranks > 1) c->xfull.ensure(size_t(c->nloc) * size_t(c->nranks) * 8);
-    c->part.ensure(size_t(m + 2) * size_t(L.nrb) * 8);
+    if (c->nranks > 1) c->xfull.ensure(size_t(c->slot) * size_t(c->nranks) * 8);
+    c->part.ensure(3 * size_t(m + 2) * size_t(L.nrb) * 8);  // x 3: gemvt3 (sharded step)
     c->h1.ensure(size_t(m + 2) * 8);
-    c->h2.ensure(size_t(m + 2) * 8);
+    c->h2.ensure(3 * size_t(m + 2) * 8);
     c->alpha.ensure(size_t(m + 1) * 8);
     c->offd.ensure(size_t(m + 1) * 8);
     c->fn2.ensure(size_t(m + 2) * 8);
@@ -996,6 +1144,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     HIPCHK(hipMemsetAsync(c->V.p, 0, c->V.bytes, s));  // padded rows must stay exactly 0
     HIPCHK(hipMemsetAsync(c->Vn.p, 0, c->Vn.bytes, s));
     HIPCHK(hipMemsetAsync(c->w.p, 0, c->w.bytes, s));
+    HIPCHK(hipMemsetAsync(c->f.p, 0, c->f.bytes, s));
     if (c->nranks > 1) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
     if (!c->cstream) {  // mid-cycle check resources, created once per context
         HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
@@ -1239,12 +1388,20 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     }
     double* v = c->pin;
     double* y = c->pin + n;
-    double* xg = xloc;
-    if (c->nranks > 1) {
-        allgather(c, xloc, size_t(c->nloc), c->xfull.as<double>());
+    double* xg = xloc;   // the vector as the SpMV reads it
+    double* xc = xloc;   // ... and contiguous over the global rows
+    if (c->nranks > 1) {  // the padded slot layout, then compacted
+        allgather(c, xloc, size_t(c->slot), c->xfull.as<double>());
         xg = c->xfull.as<double>();
+        c->xexp.ensure(size_t(n) * 8);
+        xc = c->xexp.as<double>();
+        for (int r = 0; r < c->nranks; ++r) {
+            const int64_t a = c->shard_off[size_t(r)], b = c->shard_off[size_t(r) + 1];
+            if (b > a)
+                HIPCHK(hipMemcpyAsync(xc + a, xg + r * c->slot, size_t(b - a) * 8, hipMemcpyDeviceToDevice, s));
+        }
     }
-    HIPCHK(hipMemcpyAsync(v, xg, size_t(n) * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(v, xc, size_t(n) * 8, hipMemcpyDeviceToHost, s));
     // residual ||L x - lambda x|| on the owned rows
     ek::dev::spmv(s, spmv_mat(c), xg, c->w.as<double>(), nullptr, nullptr, nullptr, nullptr);
     if (c->nrows) HIPCHK(hipMemcpyAsync(y, c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
@@ -1271,7 +1428,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         if (std::fabs(v[i]) > std::fabs(v[imax])) imax = i;
     const double sgn = v[imax] < 0 ? -inv : inv;
     c->fied.ensure(size_t(n) * 8);
-    ek::dev::fiedler_scale(s, xg, sgn, int(n), c->fied.as<double>());
+    ek::dev::fiedler_scale(s, xc, sgn, int(n), c->fied.as<double>());
     HIPCHK(hipGetLastError());
     c->fied_n = n;
     if (lambda_out) *lambda_out = lambda;
@@ -1286,6 +1443,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         stats->spmv_ms = L.spmv_ms;
         stats->spmv_timed = L.spmv_timed;
         stats->comm_ms = c->comm_ms;
+        stats->allgathers = int32_t(c->n_ag);
+        stats->allreduces = int32_t(c->n_ar);
     }
     return EK_OK;
     EK_CATCH

@@ -154,6 +154,7 @@ struct StepFin {
     const double* a3 = nullptr;
     const double* fn2_i = nullptr;
     const double* bov_i = nullptr;
+    int nstride = 1;  // npart[k * nstride], k < nb (the sharded step: each rank's ||f||^2 in its all-gather slot)
 };
 
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
@@ -227,6 +228,10 @@ void encode_segments(hipStream_t s, int nblocks, const int32_t* desc, const int*
                      const double* val, const unsigned long long* table, int tsize, const long long* code_of_slot,
                      int colbits, uint32_t* seg, uint16_t* rel);
 
+// col[p] (global ids) -> r * slot + (col - off[r]) for the owner r of col
+// (off: nranks + 1 row offsets of the shard map): the all-gather slot layout
+void remap_cols(hipStream_t s, long long nnz, int* col, const long long* off, int nranks, long long slot);
+
 // kernels_lanczos.hip
 #ifndef EK_GT_ROWS
 #define EK_GT_ROWS 1024
@@ -239,6 +244,18 @@ constexpr int MAX_NCV = 128;
 // the implicit deflation vector u0 (value u0val on rows < nreal) if has_u0.
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val,
            int nreal, const double* w, double* part);
+// the sharded step (ctx.cpp factorize_mr): part for three vectors w, va, vb at
+// once, part[(k*tot + j)*nrb + b], tot = ncols + has_u0
+void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
+            const double* w, const double* va, const double* vb, double* part);
+// hall = the all-reduced column sums of gemvt3 (3 x tot): alpha = hall[i],
+// h = hall[0:tot] - alpha hall[tot:2tot] - beta hall[2tot:3tot] (i = ncols-1),
+// dst = w - alpha vi - beta vim1 - V h - u0 h[ncols] (+ ||dst||^2 partials);
+// block 0 writes alpha[i] = alpha + h[i] and offd[i] = beta_i + h[i-1].
+// beta = sqrt(*fn2_i) unless the override *bov_i is not NaN; vim1 null: 0.
+void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
+               const double* hall, const double* w, const double* vi, const double* vim1, const double* fn2_i,
+               const double* bov_i, double* dst, double* npart, double* alpha, double* offd);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 

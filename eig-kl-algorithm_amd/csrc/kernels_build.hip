@@ -445,5 +445,28 @@ void encode_segments(hipStream_t s, int nblocks, const int32_t* desc, const int*
                            val, table, unsigned(tsize - 1), code_of_slot, colbits, seg, rel);
 }
 
+// The sharded Lanczos all-gathers each rank's slice of f into a slot of S
+// doubles (rank-major, padded: the slices are nnz-balanced and unequal), so a
+// global column c owned by rank r (off[r] <= c < off[r+1]) is read at
+// r * S + (c - off[r]).  Monotone in c: sorted rows stay sorted.
+__global__ __launch_bounds__(BT) void k_remap_cols(long long nnz, int* __restrict__ col,
+                                                   const long long* __restrict__ off, int nranks, long long slot) {
+    const long long p = (long long)blockIdx.x * BT + threadIdx.x;
+    if (p >= nnz) return;
+    const long long c = col[p];
+    int lo = 0, hi = nranks - 1;  // largest r with off[r] <= c
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= c) lo = mid;
+        else hi = mid - 1;
+    }
+    col[p] = int(lo * slot + (c - off[lo]));
+}
+
+void remap_cols(hipStream_t s, long long nnz, int* col, const long long* off, int nranks, long long slot) {
+    if (nnz > 0)
+        hipLaunchKernelGGL(k_remap_cols, dim3(grid_of(nnz)), dim3(BT), 0, s, nnz, col, off, nranks, slot);
+}
+
 }  // namespace dev
 }  // namespace ek

@@ -144,6 +144,97 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
         part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
 }
 
+// The sharded step's projection (ctx.cpp Lanczos::factorize_mr): the partial
+// dot products of THREE vectors with the same basis columns in one sweep of
+// V — w = L v_i, v_i and v_{i-1} — so the three-term coefficient alpha and the
+// Gram-Schmidt coefficients of f' = w - alpha v_i - beta v_{i-1} come out of
+// ONE all-reduce: V^T f' = V^T w - alpha V^T v_i - beta V^T v_{i-1}, with
+// alpha = (V^T w)_i.  part[(k * tot + j) * nrb + b] for vector k (0: w, 1: v_i,
+// 2: v_{i-1}), column j < tot = ncols + has_u0 (column ncols = u0).  Same
+// tiling, XCD remap and fixed-shape reductions as k_gemvt.
+__global__ __launch_bounds__(256) void k_gemvt3(int ldv, int nrb, const double* __restrict__ V, int ncols,
+                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
+                                                const double* __restrict__ va, const double* __restrict__ vb,
+                                                double* __restrict__ part) {
+    __shared__ double red[3][4][GT_COLS];
+    const int t = threadIdx.x;
+    const int tot = ncols + has_u0;
+    const int ncg = (tot + GT_COLS - 1) / GT_COLS;
+    const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+    const int v = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+    const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
+    const size_t nr = size_t(nreal);
+    constexpr int KR = GT_ROWS / 512;
+    const int jmax = ncols > 0 ? ncols - 1 : 0;
+    double2 xs[3][KR], vs[KR][GT_COLS];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+        xs[0][k] = *reinterpret_cast<const double2*>(w + r);
+        xs[1][k] = *reinterpret_cast<const double2*>(va + r);
+        xs[2][k] = *reinterpret_cast<const double2*>(vb + r);
+#pragma unroll
+        for (int jj = 0; jj < GT_COLS; ++jj)
+            vs[k][jj] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+    }
+    double acc[3][GT_COLS];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int jj = 0; jj < GT_COLS; ++jj) acc[m][jj] = 0.0;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const double2 x = xs[m][k];
+#pragma unroll
+            for (int jj = 0; jj < GT_COLS; ++jj) {
+                const int j = j0 + jj;
+                if (j < ncols) {
+                    const double2 vv = vs[k][jj];
+                    acc[m][jj] += vv.x * x.x + vv.y * x.y;
+                } else if (has_u0 && j == ncols) {
+                    acc[m][jj] += u0val * ((r < nr ? x.x : 0.0) + (r + 1 < nr ? x.y : 0.0));
+                }
+            }
+        }
+    }
+    // the reduce-scatter of k_gemvt, once per vector
+    const int lane = t & 63;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        double a4[4], a2[2];
+        {
+            const bool hi = lane & 32;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                a4[k] = (hi ? acc[m][k + 4] : acc[m][k]) + __shfl_xor(hi ? acc[m][k] : acc[m][k + 4], 32, 64);
+        }
+        {
+            const bool hi = lane & 16;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) a2[k] = (hi ? a4[k + 2] : a4[k]) + __shfl_xor(hi ? a4[k] : a4[k + 2], 16, 64);
+        }
+        double a1;
+        {
+            const bool hi = lane & 8;
+            a1 = (hi ? a2[1] : a2[0]) + __shfl_xor(hi ? a2[0] : a2[1], 8, 64);
+        }
+        a1 += __shfl_xor(a1, 4, 64);
+        a1 += __shfl_xor(a1, 2, 64);
+        a1 += __shfl_xor(a1, 1, 64);
+        if ((lane & 7) == 0) red[m][t >> 6][((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = a1;
+    }
+    __syncthreads();
+    if (t < 3 * GT_COLS) {
+        const int m = t / GT_COLS, c = t % GT_COLS;
+        if (j0 + c < tot)
+            part[(size_t(m) * tot + size_t(j0 + c)) * nrb + rbk] =
+                (red[m][0][c] + red[m][1][c]) + (red[m][2][c] + red[m][3][c]);
+    }
+}
+
 // The canonical order of a column sum over the projection partials: 8 lanes
 // per column, lane l summing blocks l, l+8, l+16, ... in order, then a fixed
 // xor tree over the 8 lanes (every lane of the group gets the sum).  Used by
@@ -297,6 +388,89 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
         const double s = block_sum256(x.x * x.x + x.y * x.y, lds4);
         if (threadIdx.x == 0) npart[blockIdx.x] = s;
     }
+}
+
+// The sharded step's update (after the one all-reduce of k_gemvt3's column
+// sums, hall = [V^T w | V^T v_i | V^T v_{i-1}], tot values each):
+//   alpha = (V^T w)_i, beta = ||f_{i-1}|| (or the injected override, 0 at i = 0),
+//   h = V^T w - alpha V^T v_i - beta V^T v_{i-1}   (the projection of f'),
+//   dst = f' - V h - u0 h_u0,  f' = w - alpha v_i - beta v_{i-1},
+// with ||dst||^2 partials -> npart, and block 0 publishes the projected
+// matrix entries alpha[i] = alpha + h[i], offd[i] = beta + h[i-1] (Spectra's
+// H += V^T f correction, as k_finalize_step's three-term form).  f' is formed
+// with k_three_term's operation order; the subtractions of V h keep
+// k_update's order.
+__global__ __launch_bounds__(256) void k_update_mr(int ldv, const double* __restrict__ V, int ncols, int has_u0,
+                                                   double u0val, int nreal, const double* __restrict__ hall,
+                                                   const double* __restrict__ w, const double* __restrict__ vi,
+                                                   const double* __restrict__ vim1, const double* __restrict__ fn2_i,
+                                                   const double* __restrict__ bov_i, double* __restrict__ dst,
+                                                   double* __restrict__ npart, double* __restrict__ alpha,
+                                                   double* __restrict__ offd) {
+    constexpr int UB = EK_UPD_UB;
+    __shared__ double hc[MAX_NCV + 2 * UB];
+    __shared__ double hu0;
+    __shared__ double lds4[4];
+    const int tot = ncols + has_u0, i = ncols - 1;
+    const int jmax = ncols > 0 ? ncols - 1 : 0;
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    auto load_batch = [&](double2* vb, int j0) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u) vb[u] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + u, jmax)) * ldv + r);
+    };
+    double2 ba[UB], bb[UB];
+    const double2 xw = *reinterpret_cast<const double2*>(w + r);
+    const double2 xv = *reinterpret_cast<const double2*>(vi + r);
+    const double2 xu = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
+    load_batch(ba, 0);
+    load_batch(bb, UB);
+    const double a = hall[i];
+    const double braw = i > 0 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
+    const double b = vim1 ? braw : 0.0;
+    for (int j = threadIdx.x; j < tot; j += 256) {
+        const double hj = (hall[j] - a * hall[tot + j]) - b * hall[2 * tot + j];
+        if (j < ncols) hc[j] = hj;
+        else hu0 = hj;
+    }
+    for (int j = ncols + int(threadIdx.x); j < ncols + 2 * UB; j += 256) hc[j] = 0.0;
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        alpha[i] = a + hc[i];
+        if (i > 0) offd[i] = braw + hc[i - 1];
+    }
+    double2 x = xw;
+    x.x -= a * xv.x;
+    x.y -= a * xv.y;
+    if (vim1) {
+        x.x -= b * xu.x;
+        x.y -= b * xu.y;
+    }
+    auto consume = [&](const double2* vb, int j0) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            const double hj = hc[j0 + u];
+            x.x -= vb[u].x * hj;
+            x.y -= vb[u].y * hj;
+        }
+    };
+    for (int j0 = 0; j0 < ncols; j0 += 2 * UB) {
+        consume(ba, j0);
+        __builtin_amdgcn_sched_barrier(0);
+        load_batch(ba, j0 + 2 * UB);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(bb, j0 + UB);
+        __builtin_amdgcn_sched_barrier(0);
+        load_batch(bb, j0 + 3 * UB);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (has_u0) {
+        const double c = u0val * hu0;
+        if (r < size_t(nreal)) x.x -= c;
+        if (r + 1 < size_t(nreal)) x.y -= c;
+    }
+    *reinterpret_cast<double2*>(dst + r) = x;
+    const double s = block_sum256(x.x * x.x + x.y * x.y, lds4);
+    if (threadIdx.x == 0) npart[blockIdx.x] = s;
 }
 
 // fn2_out = sum(npart); H(step,step) / H(step-1,step) from the projections:
@@ -454,6 +628,21 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
                        has_u0, u0val, nreal, w, part);
 }
 
+
+void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
+            const double* w, const double* va, const double* vb, double* part) {
+    const int cols = ncols + has_u0;
+    if (cols <= 0) return;
+    hipLaunchKernelGGL(k_gemvt3, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V, ncols,
+                       has_u0, u0val, nreal, w, va, vb, part);
+}
+
+void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
+               const double* hall, const double* w, const double* vi, const double* vim1, const double* fn2_i,
+               const double* bov_i, double* dst, double* npart, double* alpha, double* offd) {
+    hipLaunchKernelGGL(k_update_mr, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal, hall,
+                       w, vi, vim1, fn2_i, bov_i, dst, npart, alpha, offd);
+}
 
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h) {
     if (ncols_total <= 0) return;

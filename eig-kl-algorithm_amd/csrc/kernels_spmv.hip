@@ -44,12 +44,13 @@ __device__ __forceinline__ void finalize_publish(const StepFin& f, double n2) {
 
 // thread-strided partial of sum(x[0:n)): x[t] + x[t+256] + ... in order (the
 // order of k_finalize_step), loads batched so they are in flight together
-__device__ __forceinline__ double strided_sum(const double* __restrict__ x, int n) {
+__device__ __forceinline__ double strided_sum(const double* __restrict__ x, int n, int stride) {
     double s = 0.0;
     for (int i0 = threadIdx.x; i0 < n; i0 += 4 * SPMV_THREADS) {
         double v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = i0 + u * SPMV_THREADS < n ? x[i0 + u * SPMV_THREADS] : 0.0;
+        for (int u = 0; u < 4; ++u)
+            v[u] = i0 + u * SPMV_THREADS < n ? x[size_t(i0 + u * SPMV_THREADS) * size_t(stride)] : 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (i0 + u * SPMV_THREADS < n) s += v[u];
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     // the solve: loading them in the segment's round trip, 13.1 us, or every
     // wave reducing all of them without barriers, 15.3 us, were both slower
     // than this form, 12.7 us.)
-    const double npart_t = fin.npart ? strided_sum(fin.npart, fin.nb) : 0.0;
+    const double npart_t = fin.npart ? strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
             const double n2 = block_sum_all(npart_t, wsum);

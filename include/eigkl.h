@@ -97,6 +97,15 @@ void ek_csr_free(ek_csr* c);
 /* 1-D row-block partition for the sharded Lanczos: rank r owns
  * rows [row0, row0+nrows) with nrows <= nloc (equal padded blocks). */
 int ek_shard_rows(int64_t n, int nranks, int rank, int64_t* row0, int64_t* nrows, int64_t* nloc);
+/* The nnz-balanced partition (SURVEY §8e "1-D row block partition balanced
+ * by nnz"), the one ek_spmv_setup_pins uses: rank r owns rows
+ * [row_offsets[r], row_offsets[r+1]) (nranks + 1 offsets), cut where the
+ * prefix of the Laplacian rows' entries (1 + sum over the row's nets of
+ * |e| - 1: initializeMatrix's triplets, cEIG.cpp:86-133) reaches r/nranks of
+ * the total.  Deterministic: every rank computes the same map.  No reference
+ * counterpart (the reference has no multi-GPU path). */
+int ek_shard_map(int64_t n, int64_t nets, const int64_t* net_ptr, const int32_t* pins, int nranks,
+                 int64_t* row_offsets);
 
 /* ------------------------------------------------------------------ */
 /* GPU context                                                          */
@@ -134,13 +143,15 @@ int ek_comm_init_host(ek_ctx* ctx, int nranks, int rank, ek_allgather_fn allgath
 /* ------------------------------------------------------------------ */
 /* Upload the Laplacian rows this context owns.  n = global size; rowptr has
  * nrows+1 entries starting at 0; col holds global column ids.  Host arrays
- * are copied; the caller keeps ownership. */
+ * are copied; the caller keeps ownership.  Sharded contexts: every rank
+ * calls it; the ranks' [row0, row0+nrows) must tile [0, n) in rank order
+ * (learned with one all-gather; ek_shard_map or ek_shard_rows). */
 int ek_spmv_setup(ek_ctx* ctx, int64_t n, int64_t row0, int64_t nrows, const int32_t* rowptr,
                   const int32_t* col, const double* val);
 /* The same rows built on the GPU straight from the hypergraph's pins (net e
  * owns pins[net_ptr[e] .. net_ptr[e+1]), 0-based): the clique Laplacian of
  * initializeMatrix (cEIG.cpp:86-133) assembled by device kernels into the
- * SpMV's coded form, the rows of this context's shard only (ek_shard_rows).
+ * SpMV's coded form, the rows of this context's shard only (ek_shard_map).
  * The values and the row blocks are the host build's (ek_laplacian_build),
  * so every SpMV and Lanczos result is bit-identical to ek_spmv_setup on
  * those rows.  Falls back to the host build for a row too long for the
@@ -205,6 +216,8 @@ typedef struct {
     double spmv_ms;       /* sum of SpMV launch durations (time_spmv=1) */
     int32_t spmv_timed;   /* SpMV launches timed */
     double comm_ms;       /* time inside RCCL calls (host-observed, sharded) */
+    int32_t allgathers;   /* collectives issued by this rank during the solve (sharded; */
+    int32_t allreduces;   /* one of each per Lanczos step, plus restarts/injections/end) */
 } ek_lanczos_stats;
 
 void ek_lanczos_default_opts(ek_lanczos_opts* o);

@@ -1,10 +1,20 @@
 """The N>1 data path on CPU (gloo, world_size 2): the row-sharded Lanczos
-exchange pattern the HIP path runs over RCCL (ctx.cpp Lanczos):
-rows split by ek_shard_rows, x replicated by an all-gather of the rank-major
-padded slices, every dot product / norm all-reduced.  Each rank runs the
-product's host pieces (generator, Laplacian, shard map) and a numpy restatement
-of the per-rank arithmetic; the sharded recurrence must reproduce the
-single-process one."""
+exchange the HIP path runs over RCCL (ctx.cpp
+Lanczos::factorize_mr), restated in numpy on each rank with the product's host
+pieces (generator, Laplacian rows, the nnz-balanced shard map):
+
+* rank r owns rows [off[r], off[r+1]) of ek_shard_map (unequal slices);
+* ONE all-gather per step: every rank's f slice padded to a slot of S
+  doubles, with the rank's ||f||^2 partial in the slot's tail, so the matrix
+  reads x through columns remapped to r*S + (c - off[r]) and every rank sums
+  the ranks' partials in rank order (the same bits everywhere);
+* ONE all-reduce per step: [V^T w | V^T v_i | V^T v_{i-1}], from which
+  alpha = (V^T w)_i and the projection of f' = w - alpha v_i - beta v_{i-1}
+  come by linearity.
+
+The sharded recurrence must reproduce the single-process three-term + CGS one
+(the single-GPU step) within fp64 round-off, with exactly two collectives per
+step."""
 import os
 import socket
 
@@ -33,22 +43,22 @@ def _local_spmv(rp, col, val, x):
     return y
 
 
-def _lanczos_steps(matvec, dot, n_local, mask, n, x0, steps):
-    """Deflated three-term Lanczos + one CGS pass (the default reorth=1 path)."""
-    u0 = mask / np.sqrt(n)
-    f = x0 - dot(u0, x0) * u0
+def _lanczos_single(matvec, n, x0, steps):
+    """Deflated three-term Lanczos + one CGS pass of f' (the single-GPU reorth=1 step)."""
+    u0 = np.ones(n) / np.sqrt(n)
+    f = x0 - (u0 @ x0) * u0
     V, alpha, beta = [], [], []
-    b = np.sqrt(dot(f, f))
+    b = np.sqrt(f @ f)
     for i in range(steps):
         v = f / b
         V.append(v)
         w = matvec(v)
-        a = dot(v, w)
+        a = v @ w
         f = w - a * v - (beta[-1] * V[-2] if i > 0 else 0.0)
-        h = np.array([dot(q, f) for q in V] + [dot(u0, f)])
+        h = np.array([q @ f for q in V] + [u0 @ f])
         f = f - sum(hj * q for hj, q in zip(h[:-1], V)) - h[-1] * u0
         alpha.append(a + h[i])
-        b = np.sqrt(dot(f, f))
+        b = np.sqrt(f @ f)
         beta.append(b)
     return np.array(alpha), np.array(beta)
 
@@ -61,57 +71,101 @@ def _worker(rank, port, out):
         h = ek.Hypergraph.generate(0.05, 3)
         n = h.nodes
         L = h.laplacian()
-        row0, nrows, nloc = ek.shard_rows(n, WORLD, rank)
-        rp = L.rowptr[row0: row0 + nrows + 1].astype(np.int64)
-        lrp, lcol, lval = rp - rp[0], L.col[rp[0]: rp[-1]], L.val[rp[0]: rp[-1]]
-        mask = np.zeros(nloc)
-        mask[:nrows] = 1.0
+        off = ek.shard_map(h, WORLD)
+        row0, nrows = int(off[rank]), int(off[rank + 1] - off[rank])
+        M = int(np.diff(off).max())
+        ldv = -(-M // 1024) * 1024
+        S = ldv + 64  # the library's slot: Lanczos rows + 64, ||f||^2 partial at [ldv]
+        S_rows = h.laplacian_rows(row0, row0 + nrows)
+        owner = np.searchsorted(off[1:-1], S_rows.col, side="right")
+        colx = owner * S + (S_rows.col - off[owner])  # k_remap_cols
+        real = np.zeros(ldv)
+        real[:nrows] = 1.0
+        u0 = real / np.sqrt(n)
+        calls = {"allgather": 0, "allreduce": 0}
 
-        def allgather(xloc):
-            parts = [torch.zeros(nloc, dtype=torch.float64) for _ in range(WORLD)]
-            dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(xloc)))
-            return torch.cat(parts).numpy()[:n]
+        def allgather(slot):
+            calls["allgather"] += 1
+            parts = [torch.zeros(S, dtype=torch.float64) for _ in range(WORLD)]
+            dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(slot)))
+            return torch.cat(parts).numpy()
 
-        def matvec(xloc):
-            y = np.zeros(nloc)
-            y[:nrows] = _local_spmv(lrp, lcol, lval, allgather(xloc))
-            return y
-
-        def dot(a, b):
-            t = torch.tensor([float(a @ b)], dtype=torch.float64)
+        def allreduce(buf):
+            calls["allreduce"] += 1
+            t = torch.from_numpy(buf)
             dist.all_reduce(t)
-            return float(t.item())
+            return t.numpy()
 
+        # start vector (deflated), distributed; its setup collectives are not steps
         x0 = np.random.default_rng(1).uniform(-0.5, 0.5, n)
-        xl = np.zeros(nloc)
-        xl[:nrows] = x0[row0: row0 + nrows]
-        # sharded SpMV == full SpMV
-        y_full = allgather(matvec(xl))
-        y_ref = _local_spmv(L.rowptr.astype(np.int64), L.col, L.val, x0)
-        spmv_err = float(np.abs(y_full - y_ref).max())
-        a_sh, b_sh = _lanczos_steps(matvec, dot, nloc, mask, n, xl, STEPS)
-        a_1, b_1 = _lanczos_steps(lambda v: _local_spmv(L.rowptr.astype(np.int64), L.col, L.val, v),
-                                  lambda a, b: float(a @ b), n, np.ones(n), n, x0, STEPS)
-        out[rank] = (spmv_err, float(np.abs(a_sh - a_1).max()), float(np.abs(b_sh - b_1).max()))
+        f = np.zeros(ldv)
+        f[:nrows] = x0[row0: row0 + nrows]
+        f -= (allreduce(np.array([u0 @ f]))[0]) * u0
+        V, alpha, beta = [], [], []
+        base = dict(calls)
+        for i in range(STEPS):
+            slot = np.zeros(S)
+            slot[:ldv] = f
+            slot[ldv] = f @ f                          # this rank's ||f||^2 partial
+            x = allgather(slot)                        # collective 1
+            fn2 = sum(x[r * S + ldv] for r in range(WORLD))  # rank order: same bits on every rank
+            b_prev = np.sqrt(fn2)
+            v = f / b_prev
+            w = np.zeros(ldv)
+            w[:nrows] = _local_spmv(S_rows.rowptr.astype(np.int64), colx, S_rows.val, x) / b_prev
+            V.append(v)
+            if i > 0:
+                beta.append(b_prev)
+            vim1 = V[-2] if i > 0 else v
+            P = np.concatenate([[q @ y for q in V] + [u0 @ y] for y in (w, v, vim1)])
+            P = allreduce(P)                           # collective 2
+            tot = i + 2
+            Pw, Pv, Pm = P[:tot], P[tot:2 * tot], P[2 * tot:]
+            a = Pw[i]
+            bb = b_prev if i > 0 else 0.0
+            hcoef = Pw - a * Pv - bb * Pm
+            fp = w - a * v - (bb * vim1 if i > 0 else 0.0)
+            f = fp - sum(hj * q for hj, q in zip(hcoef[:-1], V)) - hcoef[-1] * u0
+            alpha.append(a + hcoef[i])
+        steps_calls = {k: calls[k] - base[k] for k in calls}
+        fn2_last = allreduce(np.array([f @ f]))[0]
+        beta.append(np.sqrt(fn2_last))
+        a1, b1 = _lanczos_single(lambda y: _local_spmv(L.rowptr.astype(np.int64), L.col, L.val, y), n, x0, STEPS)
+        # the sharded SpMV through the padded layout == the full SpMV's rows
+        xs = np.zeros(WORLD * S)
+        for r in range(WORLD):
+            xs[r * S: r * S + off[r + 1] - off[r]] = x0[off[r]: off[r + 1]]
+        y_sh = _local_spmv(S_rows.rowptr.astype(np.int64), colx, S_rows.val, xs)
+        y_ref = _local_spmv(L.rowptr.astype(np.int64), L.col, L.val, x0)[row0: row0 + nrows]
+        out[rank] = {"spmv_err": float(np.abs(y_sh - y_ref).max()), "da": float(np.abs(np.array(alpha) - a1).max()),
+                     "db": float(np.abs(np.array(beta) - b1).max()), "calls": steps_calls, "nrows": nrows,
+                     "alpha": np.array(alpha).tobytes()}
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_sharded_lanczos_matches_single_process():
+def test_sharded_lanczos_two_collectives_per_step():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(_free_port(), out), nprocs=WORLD, join=True)
     for r in range(WORLD):
-        spmv_err, da, db = out[r]
-        assert spmv_err <= 1e-13
-        assert da <= 1e-10 and db <= 1e-10, (da, db)
+        o = out[r]
+        assert o["spmv_err"] <= 1e-13
+        assert o["da"] <= 1e-10 and o["db"] <= 1e-10, (o["da"], o["db"])
+        assert o["calls"] == {"allgather": STEPS, "allreduce": STEPS}  # one of each per step
+    assert out[0]["alpha"] == out[1]["alpha"]  # the same projected matrix on every rank
+    assert out[0]["nrows"] != out[1]["nrows"]  # nnz-balanced slices are unequal
 
 
 def test_shard_map_is_what_the_library_enforces():
     ek = load_package()
-    n = 201920
+    h = ek.Hypergraph.generate(0.25, 3)
     for world in (2, 4, 8):
+        off = ek.shard_map(h, world)
+        assert off[0] == 0 and off[-1] == h.nodes and np.all(np.diff(off) > 0)
+    n = 201920
+    for world in (2, 4, 8):  # the equal map stays available (ek_spmv_setup accepts any tiling)
         slices = [ek.shard_rows(n, world, r) for r in range(world)]
         nloc = slices[0][2]
         assert all(s[2] == nloc for s in slices)

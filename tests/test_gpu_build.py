@@ -97,10 +97,12 @@ def test_device_build_shard_rows(ek, ctxs, ranks):
         raise AssertionError("no collective expected")
 
     try:
+        off = ek.shard_map(h, ranks)  # the nnz-balanced map the device build uses
         for r in range(ranks):
             dev_ctx.comm_init_host(ranks, r, never, never)
             assert dev_ctx.spmv_setup_pins(h) is True
-            row0, nrows, _ = ek.shard_rows(n, ranks, r)
+            row0, nrows = int(off[r]), int(off[r + 1] - off[r])
+            assert dev_ctx.spmv_dims() == (n, row0, nrows)
             y = dev_ctx.spmv_host(x)
             S = h.laplacian_rows(row0, row0 + nrows)
             absrow = np.add.reduceat(np.abs(S.val * x[S.col]), S.rowptr[:-1])

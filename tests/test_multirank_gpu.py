@@ -1,19 +1,22 @@
 """The library's own sharded Lanczos with 2 ranks, on one GPU.
 
 Two processes each open a context on GPU 0 and join a 2-rank exchange through
-ek_comm_init_host: every collective of the sharded path (the all-gather of f
-before each SpMV, the all-reduces of alpha, of the Gram-Schmidt coefficients
-and of ||f||^2, the final all-gather and the residual) goes through the
+ek_comm_init_host: every collective of the sharded path goes through the
 library's comm seam, staged through host memory and carried by
-torch.distributed gloo.  RCCL, the production backend, refuses two ranks on
-one device; the device code, the shard map (row0 > 0, padded slices), the
-unfused step sequence and the global-index restart vectors are the same.
+torch.distributed gloo.  Per Lanczos step that is ONE all-gather (every
+rank's padded f slice with its ||f||^2 partial) and ONE all-reduce (the
+projections of w, v_i, v_{i-1}); the callbacks count them.  RCCL, the
+production backend, refuses two ranks on one device; the device code, the
+nnz-balanced shard map (unequal slices, remapped columns), the step sequence
+and the global-index restart vectors are the same.
 
 Checks: the 2-rank Fiedler pair against the reference's pre_saved_EIG files
 (ibm01, industry2; the SURVEY §8c tolerances), the 2-rank SpMV against the
 1-rank one per row, the sharded solve_file (parse -> results file) against the
-reference cKL results, and a disconnected synthetic whose solve goes through
-breakdowns and injected restart vectors on both ranks."""
+reference cKL results, a disconnected synthetic whose solve goes through
+breakdowns and injected restart vectors on both ranks, and configs[4] — the
+10x synthetic (2,019,200 nodes), rows built on the device per shard — against
+the 1-rank solve."""
 import os
 import socket
 
@@ -41,6 +44,23 @@ def _fiedler_ok(ek, name, lam, v):
             "bits_equal": bool(np.array_equal(bits[mask], bits_ref[mask]))}
 
 
+def _comm(ctx, rank, counts):
+    import torch
+    import torch.distributed as dist
+
+    def allgather(x):
+        counts["allgather"] += 1
+        parts = [torch.empty(len(x), dtype=torch.float64) for _ in range(WORLD)]
+        dist.all_gather(parts, torch.from_numpy(x))
+        return torch.cat(parts).numpy()
+
+    def allreduce(x):
+        counts["allreduce"] += 1
+        dist.all_reduce(torch.from_numpy(x))  # in place (shared memory)
+
+    ctx.comm_init_host(WORLD, rank, allgather, allreduce)
+
+
 def _worker(rank, port, tmp, out):
     import datetime
     import faulthandler
@@ -55,27 +75,23 @@ def _worker(rank, port, tmp, out):
     res = {}
     try:
         ctx = ek.Context(0)
-
-        def allgather(x):
-            parts = [torch.empty(len(x), dtype=torch.float64) for _ in range(WORLD)]
-            dist.all_gather(parts, torch.from_numpy(x))
-            return torch.cat(parts).numpy()
-
-        def allreduce(x):
-            dist.all_reduce(torch.from_numpy(x))  # in place (shared memory)
-
-        ctx.comm_init_host(WORLD, rank, allgather, allreduce)
+        counts = {"allgather": 0, "allreduce": 0}
+        _comm(ctx, rank, counts)
         one = ek.Context(0)  # an unsharded context for the 1-rank comparison
         for name in ("ibm01", "industry2"):
             h = ek.Hypergraph.read(circuit_path(name))
             n = h.nodes
-            row0, nrows, nloc = ek.shard_rows(n, WORLD, rank)
+            off = ek.shard_map(h, WORLD)
+            row0, nrows = int(off[rank]), int(off[rank + 1] - off[rank])
             S = h.laplacian_rows(row0, row0 + nrows)
             ctx.spmv_setup(n, row0, S.rowptr, S.col, S.val)
+            c0 = dict(counts)
             lam, v, st = ctx.lanczos_fiedler()
             r = _fiedler_ok(ek, name, lam, v)
             r.update(converged=bool(st["converged"]), residual=st["residual"], matvecs=st["matvecs"],
-                     row0=row0, nrows=nrows, comm_ms=st["comm_ms"])
+                     restarts=st["restarts"], row0=row0, nrows=nrows, comm_ms=st["comm_ms"],
+                     allgathers=counts["allgather"] - c0["allgather"], allreduces=counts["allreduce"] - c0["allreduce"],
+                     stat_ag=st["allgathers"], stat_ar=st["allreduces"], v_bytes=v.tobytes(), lam=lam)
             # SpMV: this rank's rows vs the same rows of a 1-rank SpMV
             x = np.random.default_rng(7).standard_normal(n)
             y = ctx.spmv_host(x)
@@ -92,7 +108,7 @@ def _worker(rank, port, tmp, out):
         # disconnected synthetic: breakdowns, injected vectors over global indices on both ranks
         h = ek.Hypergraph.generate(0.25, 3)
         n = h.nodes
-        row0, nrows, _ = ek.shard_rows(n, WORLD, rank)
+        row0, nrows, _ = ek.shard_rows(n, WORLD, rank)  # (any tiling is accepted: here equal blocks)
         S = h.laplacian_rows(row0, row0 + nrows)
         ctx.spmv_setup(n, row0, S.rowptr, S.col, S.val)
         lam, v, st = ctx.lanczos_fiedler()
@@ -121,13 +137,21 @@ def test_two_rank_sharded_lanczos_through_comm_seam(tmp_path):
     assert not errors, errors
     for r in (r0, r1):
         for name in ("ibm01", "industry2"):
-            x = r[name]
+            x = {k: v for k, v in r[name].items() if k != "v_bytes"}
             assert x["converged"] and x["residual"] < 1e-9, x
             assert x["dlam"] <= 1e-10 and x["dv"] <= 1e-8 and x["bits_equal"], x
             assert x["spmv_rows_ok"], x
+            # ONE all-gather and ONE all-reduce per Lanczos step (+ the final
+            # vector's all-gather; + the start vector's two norms, one per
+            # restart and cycle end, and the residual's all-reduce)
+            assert x["allgathers"] == x["stat_ag"] == x["matvecs"] + 1, x
+            assert x["allreduces"] == x["stat_ar"], x
+            assert x["matvecs"] <= x["allreduces"] <= x["matvecs"] + 3 + 2 * (x["restarts"] + 1), x
     assert r1["ibm01"]["row0"] > 0 and r0["ibm01"]["nrows"] + r1["ibm01"]["nrows"] == 12752
+    assert r0["industry2"]["nrows"] != r1["industry2"]["nrows"]  # nnz-balanced: unequal slices
     # every rank holds the same full vector: identical Ritz pairs
-    assert r0["ibm01"]["dv"] == r1["ibm01"]["dv"]
+    for name in ("ibm01", "industry2"):
+        assert r0[name]["lam"] == r1[name]["lam"] and r0[name]["v_bytes"] == r1[name]["v_bytes"]
     s0, s1 = r0["syn0.25"], r1["syn0.25"]
     for s in (s0, s1):
         assert s["converged"] and s["finite"] and abs(s["norm"] - 1) < 1e-10 and s["residual"] < 1e-8, s
@@ -137,3 +161,79 @@ def test_two_rank_sharded_lanczos_through_comm_seam(tmp_path):
     res = tmp_path / "r0" / "results" / "ibm01.hgr_KL_CutSize_EIG_output.txt"
     compare_results_text(res.read_text(), open(ref_results_path("ibm01")).read())
     assert r0["solve_file"]["net_cut_best"] == 367
+
+
+def _worker10(rank, port, out):
+    import datetime
+    import faulthandler
+    import sys
+    import torch.distributed as dist
+    faulthandler.enable()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD, timeout=datetime.timedelta(seconds=240))
+    from conftest import load_package
+    ek = load_package()
+    res = {}
+    try:
+        h = ek.Hypergraph.generate(10.0, 10)  # configs[4]: 2,019,200 nodes
+        n = h.nodes
+        ctx = ek.Context(0)
+        counts = {"allgather": 0, "allreduce": 0}
+        _comm(ctx, rank, counts)
+        assert ctx.spmv_setup_pins(h) is True  # this rank's rows built on the device
+        _, row0, nrows = ctx.spmv_dims()
+        c0 = dict(counts)
+        lam, v, st = ctx.lanczos_fiedler()
+        res.update(lam=lam, v_sha=__import__("hashlib").sha1(v.tobytes()).hexdigest(), residual=st["residual"],
+                   converged=bool(st["converged"]), matvecs=st["matvecs"], restarts=st["restarts"], row0=row0,
+                   nrows=nrows, allgathers=counts["allgather"] - c0["allgather"],
+                   allreduces=counts["allreduce"] - c0["allreduce"], norm=float(np.linalg.norm(v)),
+                   finite=bool(np.all(np.isfinite(v))))
+        # this rank's SpMV rows vs the 1-rank SpMV
+        x = np.random.default_rng(11).standard_normal(n)
+        y = ctx.spmv_host(x)
+        ctx.close()
+        one = ek.Context(0)
+        assert one.spmv_setup_pins(h) is True
+        y1 = one.spmv_host(x)[row0: row0 + nrows]
+        S = h.laplacian_rows(row0, row0 + nrows)
+        absrow = np.add.reduceat(np.abs(S.val * x[S.col]), S.rowptr[:-1])
+        res["spmv_rows_ok"] = bool(np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300))
+        res["spmv_max_abs_diff"] = float(np.abs(y - y1).max())
+        if rank == 0:  # the 1-rank solve of the same problem
+            lam1, v1, st1 = one.lanczos_fiedler()
+            res.update(lam1=lam1, residual1=st1["residual"], matvecs1=st1["matvecs"])
+        one.close()
+    except Exception:
+        import traceback
+        res["error"] = traceback.format_exc()
+        print(f"[rank {rank}] {res['error']}", file=sys.stderr, flush=True)
+    finally:
+        out[rank] = res
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_sharded_lanczos_syn10_config4():
+    """configs[4]: the 10x synthetic, Lanczos rows
+    sharded over 2 ranks (nnz-balanced map, rows built on the device per
+    shard).  Converged residual, the same pair on both ranks, each rank's SpMV
+    rows equal to the 1-rank SpMV's, lambda equal to the 1-rank solve's, and
+    2 collectives per step.  (The synthetic is disconnected, so lambda1 = 0 and
+    the null vector returned is not unique: v is compared across ranks, not
+    with the 1-rank run.)"""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker10, args=(_free_port(), out), nprocs=WORLD, join=True)
+    r0, r1 = out[0], out[1]
+    errors = {k: out[k]["error"] for k in (0, 1) if "error" in out[k]}
+    assert not errors, errors
+    for r in (r0, r1):
+        assert r["converged"] and r["residual"] < 1e-8 and r["finite"] and abs(r["norm"] - 1) < 1e-10, r
+        assert r["spmv_rows_ok"], r
+        assert r["allgathers"] == r["matvecs"] + 1, r
+        assert r["matvecs"] <= r["allreduces"] <= r["matvecs"] + 3 + 2 * (r["restarts"] + 1) + 3 * 64, r
+    assert r0["nrows"] + r1["nrows"] == 2019200 and r1["row0"] == r0["nrows"]
+    assert r0["lam"] == r1["lam"] and r0["v_sha"] == r1["v_sha"]
+    assert abs(r0["lam"] - r0["lam1"]) <= 1e-10 and r0["residual1"] < 1e-8
