@@ -63,30 +63,46 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def pmc_traffic(mult, seed, work):
-    """FETCH_SIZE / WRITE_SIZE of the Lanczos SpMV, one rocprofv3 pass each over
-    tools/spmv_probe.py (a resident solve), run BEFORE this process touches the
-    GPU.  Per dispatch, kB -> bytes.  Returns a dict or None."""
+def rocprof_pass(what, probe_args, work, tag):
+    """One rocprofv3 pass over tools/spmv_probe.py (a child process started
+    BEFORE this process touches the GPU).  what = "trace": --kernel-trace
+    --stats, returns {kernel name: (calls, average ns)}; otherwise a PMC
+    counter (FETCH_SIZE / WRITE_SIZE), returns the SpMV dispatches' average in
+    bytes (kB -> bytes) and their count.  None on failure."""
     if not shutil.which("rocprofv3"):
         return None
-    out = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(work, f"pmc_{ctr}")
-        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o",
-               "p", "--", sys.executable, os.path.join(REPO, "tools", "spmv_probe.py"), str(mult), str(seed)]
-        env = dict(os.environ, TMPDIR="/tmp")
-        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
-        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        if r.returncode != 0 or not files:
-            log(f"rocprofv3 {ctr} pass failed (rc {r.returncode}): {r.stderr[-300:]}")
-            return None
-        vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(files[0]))
-                if "k_spmv_adaptive" in row["Kernel_Name"]]
-        if not vals:
-            return None
-        out[ctr] = sum(vals) / len(vals) * 1024.0
-        out[ctr + "_dispatches"] = len(vals)
-    return out
+    d = os.path.join(work, f"rp_{tag}_{what}")
+    mode = ["--kernel-trace", "--stats"] if what == "trace" else ["--pmc", what]
+    cmd = (["timeout", "-s", "KILL", "150", "rocprofv3"] + mode + ["--output-format", "csv", "-d", d, "-o", "p", "--",
+           sys.executable, os.path.join(REPO, "tools", "spmv_probe.py")] + [str(a) for a in probe_args])
+    env = dict(os.environ, TMPDIR="/tmp")
+    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)
+    pat = "*kernel_stats.csv" if what == "trace" else "*counter_collection.csv"
+    files = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    if r.returncode != 0 or not files:
+        log(f"rocprofv3 {what} pass ({tag}) failed (rc {r.returncode}): {r.stderr[-300:]}")
+        return None
+    if what == "trace":
+        return {row["Name"]: (int(row["Calls"]), float(row["AverageNs"])) for row in csv.DictReader(open(files[0]))}
+    vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(files[0]))
+            if "k_spmv_adaptive" in row["Kernel_Name"]]
+    if not vals:
+        return None
+    return {"bytes": sum(vals) / len(vals) * 1024.0, "dispatches": len(vals)}
+
+
+def kernel_avg_us(stats, needle):
+    """(calls, average us) of the kernels whose name holds `needle` (calls-weighted)."""
+    rows = [v for k, v in (stats or {}).items() if needle in k]
+    calls = sum(c for c, _ in rows)
+    return (calls, sum(c * a for c, a in rows) / calls / 1e3) if calls else (0, None)
+
+
+def traffic_of(fetch, write):
+    if not fetch or not write:
+        return None
+    return {"traffic": round(2 * fetch["bytes"] + write["bytes"]), "fetch_raw_bytes": round(fetch["bytes"]),
+            "write_bytes": round(write["bytes"]), "dispatches": fetch["dispatches"]}
 
 
 def cpu_baseline(hgr, split_npz, threads, max_matvec):
@@ -129,12 +145,23 @@ def main():
     work = tempfile.mkdtemp(prefix=f"ekbench_r{rank}_")
     extras = not args.no_extras and world == 1
 
-    # PMC passes first: child processes, before this process touches the GPU
-    pmc = None
+    # rocprofv3 passes first: child processes, before this process touches the GPU
+    #  * kernel trace of the bench's own step (1 untimed + 3 solve_file steps):
+    #    the SpMV's average duration the line's roofline is computed from;
+    #  * PMC FETCH_SIZE / WRITE_SIZE of the SpMV over a resident solve (1x, 10x);
+    #  * kernel trace of the 10x resident solve (syn10's roofline).
+    prof = {}
     if extras and not args.no_pmc:
         t = time.time()
-        pmc = pmc_traffic(args.mult, args.seed, work)
-        log(f"PMC passes {time.time() - t:.1f} s: {pmc}")
+        prof["trace"] = rocprof_pass("trace", ["file", args.mult, args.seed, 1, 3], work, "1x")
+        prof["fetch"] = rocprof_pass("FETCH_SIZE", ["resident", args.mult, args.seed], work, "1x")
+        prof["write"] = rocprof_pass("WRITE_SIZE", ["resident", args.mult, args.seed], work, "1x")
+        prof["trace10"] = rocprof_pass("trace", ["resident", 10.0, 10], work, "10x")
+        prof["fetch10"] = rocprof_pass("FETCH_SIZE", ["resident", 10.0, 10], work, "10x")
+        prof["write10"] = rocprof_pass("WRITE_SIZE", ["resident", 10.0, 10], work, "10x")
+        log(f"rocprofv3 passes {time.time() - t:.1f} s: " + json.dumps(
+            {k: (v if not k.startswith("trace") else {n[:40]: c for n, c in list((v or {}).items())[:6]})
+             for k, v in prof.items()}))
 
     import torch.distributed as dist
     if world > 1:
@@ -284,7 +311,18 @@ def main():
                  "spmv_GBps_per_gpu": round(b10 / us10_max / 1e3, 1),
                  "spmv_frac_per_gpu": round(b10 / us10_max / 1e3 / HBM_PEAK_GBS, 4),
                  "spmv_GBps_aggregate": round(world * b10 / us10_max / 1e3, 1),
+                 "spmv_timing": "HIP kernel start/end events of every 4th SpMV (this process)",
+                 "collectives_per_solve": {"allgather": st10["allgathers"], "allreduce": st10["allreduces"]},
                  "comm_ms_per_solve": round(max_over_ranks(st10["comm_ms"]), 3), "comm": comm if world > 1 else None}
+        calls10, us10_rp = kernel_avg_us(prof.get("trace10"), "k_spmv")
+        if us10_rp:  # 1 rank: the rocprofv3 kernel trace of the same solve (a child pass before this process)
+            syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,
+                                "achieved_GBps": round(b10 / us10_rp / 1e3, 1),
+                                "frac": round(b10 / us10_rp / 1e3 / HBM_PEAK_GBS, 4)}
+        t10 = traffic_of(prof.get("fetch10"), prof.get("write10"))
+        if t10:
+            t10["per_algorithmic_byte"] = round(t10["traffic"] / b10, 3)
+            syn10["traffic"] = t10
         del h10
 
     if rank != 0:
@@ -295,6 +333,7 @@ def main():
 
     # ---------------- sub-configs (N = 1): the file path on other inputs
     subs = {}
+    lcc_path = lcc_bits = lcc_log = None
     if extras:
         hl, _ = h.largest_component()
         inputs = [("ibm01", os.path.join(GOLD, "ibm01.hgr"), "configs[1] ibm01.hgr (shipped)"),
@@ -306,11 +345,21 @@ def main():
                 p = os.path.join(work, f"{name}.hgr")
                 (hl if name == "syn1_lcc" else ek.Hypergraph.generate(2.0, 2)).write(p)
             walls, rr = [], None
-            for i in range(3):
+            # the connected ibm18-scale problem gets the headline's treatment:
+            # 2 untimed + 10 timed steps; the others a median of 2 warm runs
+            nrun, nwarm = (12, 2) if name == "syn1_lcc" else (3, 1)
+            for i in range(nrun):
                 t = time.time()
                 rr, _ = ctx.solve_file(p, eig=1, out_dir=out_dir)
                 walls.append(time.time() - t)
-            subs[name] = {"what": what, "nodes": rr["nodes"], "wall_s": round(float(np.median(walls[1:])), 4),
+            if name == "syn1_lcc":  # its split and swap log for the CPU baseline's KL comparison
+                lcc_path = p
+                _, lcc_log = ctx.solve_file(p, eig=1, out_dir=out_dir, log_cap=rr["nodes"] // 2)
+                ctx.kl_n = rr["nodes"]
+                lcc_bits = ctx.kl_sides(0)
+            subs[name] = {"what": what, "nodes": rr["nodes"], "wall_s": round(float(np.median(walls[nwarm:])), 4),
+                          "ms_per_step": round(1e3 * float(np.mean(walls[nwarm:])), 3),
+                          "steps_timed": nrun - nwarm,
                           "lambda1": rr["lambda"], "matvecs": rr["lanczos"]["matvecs"],
                           "restarts": rr["lanczos"]["restarts"], "lanczos_s": round(rr["t_lanczos"], 4),
                           "kl_iterations": rr["kl"]["iterations"], "kl_s": round(rr["t_kl"], 4),
@@ -332,83 +381,114 @@ def main():
                           "GB/s": round(b2 / us / 1e3, 1), "frac": round(b2 / us / 1e3 / HBM_PEAK_GBS, 4)})
             c2.close()
 
-    # ---------------- fresh-process wall of the drop-in tool (HIP start-up included)
-    fresh = None
+    # ---------------- fresh-process wall of the drop-in tool (HIP start-up included),
+    # split by the library's EK_COLD_TRACE stamps (tools/cold_probe.py)
+    fresh = fresh_breakdown = None
     if extras:
-        tool = os.path.join(REPO, "eig-kl-algorithm_amd", "build", "bin", "gKL2")
-        walls = []
-        for _ in range(5):
-            t = time.time()
-            r = subprocess.run([tool, path, "-EIG", "--quiet"], cwd=out_dir, capture_output=True, timeout=300)
-            walls.append(time.time() - t)
-            if r.returncode != 0:
-                walls = [f"failed rc {r.returncode}: {r.stderr[-200:]!r}"]
-                break
-        fresh = round(float(np.median(walls)), 4) if isinstance(walls[0], float) else walls[0]
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import cold_probe
+        fb = cold_probe.probe(path, 5, cwd=out_dir)
+        if "error" in fb:
+            fresh = fb["error"]
+        else:
+            fresh = fb["exit"]
+            fresh_breakdown = {"offsets_s": fb, "what": (
+                "median offsets from the spawn of `gKL2 <1x .hgr> -EIG --quiet` (5 runs): lib_loaded = exec + "
+                "dynamic loading; hip_first_call..hip_streams = ek_init on its thread (beside the parse); "
+                "laplacian/lanczos/kl = the solve's phases incl. first-launch costs; exit = the child reaped "
+                "(the executables leave the context to the process exit: EK_CLI_NO_TEARDOWN)")}
 
-    # ---------------- CPU baseline: oracle restatement on this host, 1 core and all cores
+    # ---------------- CPU baseline: oracle restatement on this host's cores
+    #  * the headline workload (all cores): its Lanczos is capped at 3x the
+    #    GPU's matvecs (the synthetic is disconnected: lambda1 = 0 has a large
+    #    eigenspace the thick-restart restatement does not settle within the cap);
+    #  * its largest connected component (a bounded, non-degenerate sample of the
+    #    same workload): to convergence, all cores and 1 core.  This is `value`,
+    #    timed beside the GPU's configs.syn1_lcc steps.
     cpu = None
     if extras and not args.no_cpu_baseline:
-        # the resident leg's split and swap log (bit-identical to the timed steps': checked below)
-        bits = res_bits
         split_npz = os.path.join(work, "split.npz")
-        np.savez(split_npz, bits=bits, log=res_log)
+        np.savez(split_npz, bits=res_bits, log=res_log)
         ncpu = len(os.sched_getaffinity(0))
         all_cores = min(16, ncpu)  # the GPU box grants each job a 16-CPU share
-        legs = {}
         gmv = last["lanczos"]["matvecs"]
-        for t in sorted({1, all_cores}, reverse=True):
-            tt = time.time()
-            # all cores: to convergence, capped at 3x the GPU's matvecs; one core: the GPU's matvecs (bounded sample)
-            legs[t] = cpu_baseline(path, split_npz, t, 3 * gmv if t == all_cores else gmv)
-            log(f"cpu baseline {t} thread(s): {time.time() - tt:.1f} s: {legs[t]}")
-        best = legs[all_cores]
+        legs = {}
+        t = time.time()
+        legs["syn"] = cpu_baseline(path, split_npz, all_cores, 3 * gmv)
+        log(f"cpu baseline headline workload, {all_cores} threads: {time.time() - t:.1f} s: {legs['syn']}")
+        if lcc_bits is not None:
+            lcc_npz = os.path.join(work, "split_lcc.npz")
+            np.savez(lcc_npz, bits=lcc_bits, log=lcc_log)
+            for key, th in (("lcc", all_cores), ("lcc_1", 1)):
+                t = time.time()
+                legs[key] = cpu_baseline(lcc_path, lcc_npz, th, 0)
+                log(f"cpu baseline LCC, {th} thread(s): {time.time() - t:.1f} s: {legs[key]}")
+        best = legs.get("lcc", legs["syn"])
         if "error" not in best:
+            is_lcc = "lcc" in legs
+            gpu_same = subs["syn1_lcc"]["ms_per_step"] / 1e3 if is_lcc else sec_per_step
             cpu = {"value": round(best["total_s"], 3), "unit": "s", "cores": best["threads"], "kind": "port",
-                   "sample": ("whole solve on the oracle restatement of cEIG+cKL (oracle/eko_eig.cpp, eko_kl.cpp), "
+                   "sample": ((f"the largest connected component of the headline workload ({subs['syn1_lcc']['nodes']:,}"
+                               f" of {n:,} nodes; the non-degenerate Fiedler problem), " if is_lcc else
+                               "the headline workload, ")
+                              + "whole solve on the oracle restatement of cEIG+cKL (oracle/eko_eig.cpp, eko_kl.cpp), "
                               f"OpenMP on {best['threads']} pinned host cores: parse, Laplacian + Lanczos "
                               + (f"to convergence ({best['lanczos_matvecs']} matvecs)" if best["lanczos_converged"]
-                                 else f"capped at {best['lanczos_matvecs']} matvecs = 3x the GPU's, not converged "
-                                      "(a lower bound)")
+                                 else f"capped at {best['lanczos_matvecs']} matvecs, not converged (a lower bound)")
                               + f", KL() from the GPU run's split ({best['kl_iterations']} swaps, swap log "
                                 "compared with the GPU's)"),
+                   "gpu_same_sample_s": round(gpu_same, 4),
+                   "gpu_speedup_same_sample": round(best["total_s"] / gpu_same, 1),
                    "lanczos_converged": best["lanczos_converged"], "lanczos_matvecs": best["lanczos_matvecs"],
                    "parse_s": best["parse_s"], "lanczos_s": best["lanczos_s"], "kl_s": best["kl_s"],
                    "swap_log_match": best["swap_log_match"], "first_mismatch": best["first_mismatch"],
-                   "net_cut_match": best["net_cut_best"] == last["kl"]["net_cut_best"] and
-                   best["net_cut_final"] == last["kl"]["net_cut_final"],
-                   "one_core": legs[1] if all_cores != 1 else None,
+                   "one_core": legs.get("lcc_1"),
+                   "headline_workload_capped": legs["syn"],
                    "reference_cKL_note": "real cKL (oracle/_ref, built from /root/reference) is O(n^2) in setup and "
-                                         "per swap (cKL.cpp:53-72, 225-251): see BASELINE.md for its measured times"}
+                                         "per swap (cKL.cpp:53-72, 225-251): see BASELINE.md for its measured times "
+                                         "(2,440 s on this LCC)"}
         else:
             cpu = {"error": best["error"]}
 
+    # the roofline's duration: the rocprofv3 kernel trace of the bench's own step
+    # (a child pass before this process touched the GPU; profiles/ holds the
+    # same summary from the round's runs); the event-timed figure of the timed
+    # steps is kept beside it
+    calls_rp, us_rp = kernel_avg_us(prof.get("trace"), "k_spmv")
+    us_line = us_rp if us_rp else spmv_us
     roof = {"bound": "hbm", "kernel": f"k_spmv_adaptive<512,{str(packed).lower()}> (Lanczos CSR SpMV, fp64)",
-            "achieved": round(alg_bytes / spmv_us / 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(alg_bytes / spmv_us / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
+            "achieved": round(alg_bytes / us_line / 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg_bytes / us_line / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
             "bytes_per_launch": int(alg_bytes),
             "bytes_rule": "SURVEY §8d: 12 nnz + 4 (n+1) + 8 n (x) + 8 n (y)",
-            "avg_launch_us": round(spmv_us, 3), "launches_timed": spmv_timed,
-            "timing": "HIP kernel start/end timestamps (hipExtLaunchKernelGGL events on the context stream) of every "
-                      "4th SpMV of each Lanczos cycle, inside the timed steps. The start event is a marker ahead of "
-                      "the dispatch, so this duration also holds the ~1.5 us kernel boundary before the SpMV: "
-                      "rocprofv3 --kernel-trace of the same command gives 11.8 us against 13.4 us here "
-                      "(profiles/r02/r02s_kernel_stats.csv); achieved and frac are therefore lower bounds",
+            "avg_launch_us": round(us_line, 3),
+            "timing": ("rocprofv3 --kernel-trace --stats over tools/spmv_probe.py file (1 untimed + 3 solve_file "
+                       f"steps of this workload, {calls_rp} SpMV dispatches), run by this bench before it touched the "
+                       "GPU: achieved = bytes_per_launch / its AverageNs" if us_rp else
+                       "HIP kernel start/end events (no rocprofv3 on this host)"),
+            "events": {"avg_launch_us": round(spmv_us, 3), "launches_timed": spmv_timed,
+                       "frac": round(alg_bytes / spmv_us / 1e3 / HBM_PEAK_GBS, 4),
+                       "what": "HIP kernel start/end timestamps of every 4th SpMV of each Lanczos cycle inside the "
+                               "timed steps; the start marker precedes the dispatch, so this also holds the ~1.5 us "
+                               "kernel boundary"},
             "fused_bytes_per_launch": int(fused_bytes),
-            "fused_frac": round(fused_bytes / spmv_us / 1e3 / HBM_PEAK_GBS, 4),
+            "fused_frac": round(fused_bytes / us_line / 1e3 / HBM_PEAK_GBS, 4),
             "stored_bytes_per_launch": int(stored),
             "storage": ("dictionary-coded CSR: 32-bit (code<<colbits | col) words + exact fp64 value table"
                         if packed else "CSR: int32 col + fp64 val"),
             "sweep_back_to_back": sweep}
-    if pmc:
-        f_raw, w_raw = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
-        roof["traffic"] = round(2 * f_raw + w_raw)
-        roof["traffic_detail"] = {
-            "fetch_raw_bytes": round(f_raw), "write_bytes": round(w_raw), "dispatches": pmc["FETCH_SIZE_dispatches"],
-            "correction": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide reads, "
-                          "MI355X_MICROARCH.md HBM; this kernel's widths: see profiles/r02/pmc_calib.txt); "
-                          "L2 memory-side requests, Infinity-Cache hits included",
-            "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over tools/spmv_probe.py in this run"}
+    if us_rp:
+        roof["kernel_trace_top"] = {
+            name.split("(")[0].replace("void ", "")[:60]: {"calls": c, "avg_us": round(a / 1e3, 3)}
+            for name, (c, a) in sorted(prof["trace"].items(), key=lambda kv: -kv[1][0] * kv[1][1])[:8]}
+    t1 = traffic_of(prof.get("fetch"), prof.get("write"))
+    if t1:
+        roof["traffic"] = t1.pop("traffic")
+        roof["traffic_detail"] = dict(t1, per_algorithmic_byte=round(roof["traffic"] / alg_bytes, 3),
+            correction="traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide reads, "
+                       "MI355X_MICROARCH.md HBM; this kernel's widths: profiles/r02/pmc_calib_*); L2 memory-side "
+                       "requests, Infinity-Cache hits included",
+            source="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over tools/spmv_probe.py resident in this run")
 
     out = {
         "metric": "wall-clock to final cut (s) + cut size, ibm18.hgr; SpMV GB/s vs HBM peak",
@@ -439,6 +519,7 @@ def main():
                    "comm_ms_per_step": round(comm_ms, 3), "spmv_us_max_rank": round(spmv_us_max, 3),
                    "resident_solve": resident},
         "e2e_fresh_process_s": fresh,
+        "e2e_fresh_breakdown": fresh_breakdown,
         "configs": subs,
         "syn10_sharded_lanczos": syn10,
     }

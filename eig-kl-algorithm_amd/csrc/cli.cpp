@@ -36,7 +36,7 @@ namespace {
 
 struct Opts {
     std::string tool, input;
-    bool eig = false, quiet = false, have_seed = false, deflate = true;
+    bool eig = false, quiet = false, have_seed = false, deflate = true, teardown = true;
     int device = 0, ncv = 0;
     double tol = 0.0;
     uint64_t seed = 0;
@@ -68,9 +68,12 @@ struct CtxInit {
     ek_ctx* ctx = nullptr;
     int rc = EK_OK;
     std::string err;
-    explicit CtxInit(int device) {
+    bool teardown = true;  // false: the context is left to the process exit (EK_CLI_NO_TEARDOWN)
+    explicit CtxInit(int device, bool td = true) : teardown(td) {
         th = std::thread([this, device] {
+            ek::cold_stamp("ctx_init_start");
             rc = ek_init(device, &ctx);
+            ek::cold_stamp("ctx_init_done");
             if (rc != EK_OK) err = ek_last_error();
         });
     }
@@ -81,7 +84,9 @@ struct CtxInit {
     }
     ~CtxInit() {
         if (th.joinable()) th.join();
-        if (ctx) ek_destroy(ctx);
+        ek::cold_stamp("ctx_destroy_start");
+        if (ctx && teardown) ek_destroy(ctx);
+        ek::cold_stamp("ctx_destroy_done");
     }
 };
 
@@ -112,7 +117,7 @@ ek_solve_opts solve_opts(const Opts& o) {
 
 int run_eig(const Opts& o) {
     const auto t0 = clk::now();
-    CtxInit ci(o.device);
+    CtxInit ci(o.device, o.teardown);
     Phases ph;
     const std::string outfile = "pre_saved_EIG/" + base_name(o.input) + "_out.txt";
     if (!o.quiet) {
@@ -158,13 +163,14 @@ int run_eig(const Opts& o) {
 
 int run_kl(const Opts& o) {
     const auto t0 = clk::now();
-    CtxInit ci(o.device);
+    CtxInit ci(o.device, o.teardown);
     const std::string base = base_name(o.input);
     if (!o.quiet) std::printf("\n============= Reading Input File ==============\n");
     ek_hgr* h = nullptr;
     check(ek_hgr_read(o.input.c_str(), &h), "Error opening file");
     std::unique_ptr<ek_hgr, void (*)(ek_hgr*)> hg(h, ek_hgr_free);
     const double t_read = secs(t0);
+    ek::cold_stamp("read_done");
     int64_t nets = 0, nodes = 0;
     ek_hgr_dims(h, &nets, &nodes, nullptr);
     if (!o.quiet)
@@ -177,6 +183,7 @@ int run_kl(const Opts& o) {
     ek_solve_result r{};
     try {
         ek::solve([&ci] { return ci.get(); }, 0, 1, *h, base, so, nullptr, 0, r);
+        ek::cold_stamp("solve_done");
     } catch (const ek::Error& e) {
         if (e.code == EK_ENOCONV) throw Fail{"Eigenvalue computation failed"};
         const std::string msg = ek_last_error();
@@ -205,8 +212,14 @@ int run_kl(const Opts& o) {
 }  // namespace
 
 extern "C" int ek_cli_main(const char* tool_c, int argc, char** argv) {
+    return ek_cli_main_ex(tool_c, argc, argv, 0);
+}
+
+extern "C" int ek_cli_main_ex(const char* tool_c, int argc, char** argv, int flags) {
+    ek::cold_stamp("main");
     Opts o;
     o.tool = tool_c ? tool_c : "cKL";
+    o.teardown = !(flags & EK_CLI_NO_TEARDOWN);
     std::vector<std::string> pos;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];

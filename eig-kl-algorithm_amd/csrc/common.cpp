@@ -71,6 +71,24 @@ void PhaseTimer::mark(const char* what) {
     t0 = t;
 }
 
+// EK_COLD_TRACE=1: "[cold] <event> <epoch s>" lines on stderr (CLOCK_REALTIME,
+// the clock the caller's launch time is read from), so a fresh process's
+// wall can be split: library load, HIP init, context, solve phases, exit.
+static const bool g_cold = std::getenv("EK_COLD_TRACE") != nullptr;
+void cold_stamp(const char* what) {
+    if (!g_cold) return;
+    const double t = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "[cold] %s %.6f\n", what, t);
+}
+namespace {
+struct ColdLoad {  // runs when the dynamic loader has mapped libeigkl_hip.so and its dependencies
+    ColdLoad() {
+        cold_stamp("lib_loaded");
+        if (g_cold) std::atexit([] { cold_stamp("atexit"); });
+    }
+} g_cold_load;
+}  // namespace
+
 int host_threads() {
     static const int cached = [] {
         for (const char* var : {"EK_THREADS", "OMP_NUM_THREADS"}) {

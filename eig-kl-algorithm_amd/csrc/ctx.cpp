@@ -292,7 +292,9 @@ int ek_init(int device, ek_ctx** out) {
     EK_TRY
     if (!out) ek::fail(EK_EINVAL, "ek_init: null out");
     int cnt = 0;
+    ek::cold_stamp("hip_first_call");
     if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) ek::fail(EK_EHIP, "no HIP device available (no CPU fallback)");
+    ek::cold_stamp("hip_device_count");
     if (device < 0 || device >= cnt) ek::fail(EK_EINVAL, "device %d out of range [0,%d)", device, cnt);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -303,6 +305,7 @@ int ek_init(int device, ek_ctx** out) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
+    ek::cold_stamp("hip_streams");
     *out = c.release();
     return EK_OK;
     EK_CATCH
@@ -1141,8 +1144,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     c->apart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
     c->Qd.ensure(size_t(m) * size_t(m + 1) * 8);
     c->scal.ensure(64);
-    HIPCHK(hipMemsetAsync(c->V.p, 0, c->V.bytes, s));  // padded rows must stay exactly 0
-    HIPCHK(hipMemsetAsync(c->Vn.p, 0, c->Vn.bytes, s));
+    // padded rows must be exactly 0 (only those: every kernel writes real
+    // rows before it reads them, and no kernel writes a padded row nonzero)
+    ek::dev::zero_pad_rows(s, c->V.as<double>(), L.ldv, L.nreal, m + 1);
+    ek::dev::zero_pad_rows(s, c->Vn.as<double>(), L.ldv, L.nreal, m + 1);
     HIPCHK(hipMemsetAsync(c->w.p, 0, c->w.bytes, s));
     HIPCHK(hipMemsetAsync(c->f.p, 0, c->f.bytes, s));
     if (c->nranks > 1) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));

@@ -40,6 +40,7 @@ struct PhaseTimer {
     double t0;
     bool on;
 };
+void cold_stamp(const char* what);  // EK_COLD_TRACE: epoch-time stamp of a start-up event
 template <class F>
 void parallel_for(int64_t n, F&& fn);  // fn(begin, end)
 template <class F>
@@ -281,6 +282,8 @@ void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double*
 // out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device)
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out);
 void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long nrows, unsigned long long st0);
+// zero the padded rows [nreal, ldv) of the first ncols columns of V
+void zero_pad_rows(hipStream_t s, double* V, int ldv, int nreal, int ncols);
 // device median split of the Fiedler vector (kernels_kl.hip)
 size_t split_tmp_bytes(int n);
 void fiedler_scale(hipStream_t s, const double* x, double sgn, int n, double* out);

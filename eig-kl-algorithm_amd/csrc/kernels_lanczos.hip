@@ -696,6 +696,22 @@ __global__ __launch_bounds__(256) void k_inject(double* __restrict__ f, int ldv,
     f[i] = double(st) / 2147483647.0 - 0.5;
 }
 
+// V[r, j] = 0 for the padded rows r in [nreal, ldv) of the first ncols columns:
+// what the basis needs at a solve's start (no kernel writes a padded row
+// with anything but 0 afterwards), instead of clearing the whole buffers
+__global__ __launch_bounds__(256) void k_zero_pad(double* __restrict__ V, int ldv, int nreal, int ncols) {
+    const int pad = ldv - nreal;
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)pad * ncols) return;
+    const int j = int(i / pad), r = nreal + int(i % pad);
+    V[size_t(j) * ldv + r] = 0.0;
+}
+
+void zero_pad_rows(hipStream_t s, double* V, int ldv, int nreal, int ncols) {
+    const long long tot = (long long)(ldv - nreal) * ncols;
+    if (tot > 0) hipLaunchKernelGGL(k_zero_pad, dim3(unsigned((tot + 255) / 256)), dim3(256), 0, s, V, ldv, nreal, ncols);
+}
+
 void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long nrows, unsigned long long st0) {
     hipLaunchKernelGGL(k_inject, dim3((ldv + 255) / 256), dim3(256), 0, s, f, ldv, row0, nrows, st0);
 }

@@ -95,13 +95,16 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
     if (after_laplacian) after_laplacian();
     // this rank's rows, assembled on the GPU from the pins into the SpMV's
     // coded form (the host build only as ek_spmv_setup_pins' fallback)
+    cold_stamp("laplacian_start");
     chk(ek_spmv_setup_pins(ctx, n, h.nets, h.net_ptr.data(), h.pins.data(), nullptr));
+    cold_stamp("laplacian_done");
     if (t_laplacian) *t_laplacian = since(t);
     if (t_spmv_setup) *t_spmv_setup = 0.0;
     t = clk::now();
     // (host_v false: the vector stays on the device for ek_kl_set_partition_fiedler)
     if (host_v) v.assign(size_t(n), 0.0);
     chk(ek_lanczos_fiedler(ctx, &o.lanczos, &lambda, host_v ? v.data() : nullptr, &st));
+    cold_stamp("lanczos_done");
     if (host_v && o.sign_ref && o.sign_ref[0]) {
         std::vector<double> ref(static_cast<size_t>(n));
         chk(ek_eig_read(o.sign_ref, n, nullptr, nullptr, nullptr, ref.data(), nullptr, nullptr, nullptr, nullptr));
@@ -218,7 +221,9 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
         own.resize(size_t(std::max<int64_t>(lcap, 1)));
         log_buf = own.data();
     }
+    cold_stamp("kl_start");
     chk(ek_kl_run(ctx, o.limit, log_buf, lcap, &r.kl));
+    cold_stamp("kl_done");
     r.t_kl = since(t);
     const int64_t iters = std::min<int64_t>(r.kl.iterations, lcap);
     if (log_out && log_buf != log_out && cap > 0) std::copy(log_buf, log_buf + std::min(iters, cap), log_out);

@@ -334,6 +334,12 @@ int ek_solve_file(ek_ctx* ctx, const char* path, const ek_solve_opts* o, ek_swap
 /* tool = "cEIG" | "cKL" | "gKL" | "gKL2".  Returns the process exit code. */
 /* ------------------------------------------------------------------ */
 int ek_cli_main(const char* tool, int argc, char** argv);
+/* As ek_cli_main.  flags & EK_CLI_NO_TEARDOWN: the GPU context is not
+ * destroyed on return (every output is written and every stream drained
+ * first); for an executable that then ends with _exit, leaving the context
+ * to the process exit instead of the runtime's orderly teardown. */
+#define EK_CLI_NO_TEARDOWN 1
+int ek_cli_main_ex(const char* tool, int argc, char** argv, int flags);
 
 #ifdef __cplusplus
 }

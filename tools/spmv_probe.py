@@ -1,29 +1,51 @@
 #!/usr/bin/env python3
-"""One resident Lanczos solve of a bench workload, for rocprofv3 counter passes
-(bench.py runs it under `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` as a
-child process before it touches the GPU itself).  The SpMV dispatches then sit
-exactly where they sit in the timed solve: between the basis passes.
+"""Child workload for bench.py's rocprofv3 passes (run BEFORE bench.py touches
+the GPU itself, each pass a process of its own):
 
-usage: python tools/spmv_probe.py MULT SEED
+  resident MULT SEED       one resident Lanczos solve (rows built on the
+                           device): the PMC FETCH_SIZE / WRITE_SIZE passes and
+                           the 10x kernel trace.  The SpMV dispatches sit
+                           where they sit in the timed solve, between the
+                           basis passes.
+  file MULT SEED W K       W untimed + K ek_solve_file steps on the generated
+                           .hgr: the bench's timed step, for the kernel-trace
+                           pass whose average SpMV duration the line's
+                           roofline uses.
+
+usage: python tools/spmv_probe.py MODE MULT SEED [W K]
+       python tools/spmv_probe.py MULT SEED          (= resident)
 """
 import importlib.util
 import os
+import shutil
 import sys
+import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
-    mult, seed = float(sys.argv[1]), int(sys.argv[2])
+    args = sys.argv[1:]
+    mode = args.pop(0) if args and args[0] in ("resident", "file") else "resident"
+    mult, seed = float(args[0]), int(args[1])
     spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
     ek = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ek)
     h = ek.Hypergraph.generate(mult, seed)
-    L = h.laplacian()
     ctx = ek.Context(0)
-    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
-    lam, _, st = ctx.lanczos_fiedler()
-    print(f"probe: {h.nodes} nodes, {st['matvecs']} matvecs, lambda1 {lam:.3e}", flush=True)
+    if mode == "resident":
+        ctx.spmv_setup_pins(h)
+        lam, _, st = ctx.lanczos_fiedler()
+        print(f"probe: {h.nodes} nodes, {st['matvecs']} matvecs, lambda1 {lam:.3e}", flush=True)
+    else:
+        warm, steps = int(args[2]), int(args[3])
+        work = tempfile.mkdtemp(prefix="ekprobe_")
+        path = os.path.join(work, "w.hgr")
+        h.write(path)
+        for i in range(warm + steps):
+            r, _ = ctx.solve_file(path, eig=1, out_dir=work)
+        print(f"probe: {steps} timed file steps, last {r['t_total'] * 1e3:.1f} ms", flush=True)
+        shutil.rmtree(work, ignore_errors=True)
     ctx.close()
 
 
