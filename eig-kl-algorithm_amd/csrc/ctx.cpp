@@ -116,12 +116,16 @@ struct ek_ctx {
     std::vector<int64_t> shard_off;
     int64_t slot = 0;
     DBuf off_d, xexp;
+    // the column-panel form of the SpMV (pn_G > 0; kernels_panel.hip)
+    int pn_G = 0, pn_P = 0, pn_pb = 0, pn_max_rows = 0;
+    DBuf pn_wrow, pn_start, pn_word, pn_rid;
     int block_nnz = 1024, nrb_spmv = 0;
     DBuf rb, rowptr, col, val, pk, rel, dict;
     int colbits = 0;  // > 0: the dictionary-coded matrix (pk, dict) is the one the SpMV reads
     int64_t mat_bytes = 0;  // bytes of the matrix arrays one SpMV reads, as stored
     // Lanczos workspace
     DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, apart, Qd, scal, bov;
+    DBuf actr;  // the SpMV's last-block counter (alpha hand-off), zero between launches
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
@@ -185,6 +189,18 @@ ek_ctx* check_ctx(ek_ctx* c) {
 ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
     ek::dev::SpmvMat m;
     m.nblocks = c->nrb_spmv;
+    if (c->pn_G > 0) {
+        m.panel.G = c->pn_G;
+        m.panel.P = c->pn_P;
+        m.panel.pb = c->pn_pb;
+        m.panel.max_rows = c->pn_max_rows;
+        m.panel.wrow = c->pn_wrow.as<int32_t>();
+        m.panel.start = c->pn_start.as<long long>();
+        m.panel.word = c->pn_word.as<uint32_t>();
+        m.panel.rid = c->pn_rid.as<uint16_t>();
+        m.dict = c->dict.as<double>();
+        return m;
+    }
     m.block_nnz = c->block_nnz;
     m.desc = c->rb.as<int32_t>();
     m.rowptr = c->rowptr.as<int32_t>();
@@ -424,6 +440,52 @@ void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
 // The column space the SpMV reads: global ids, or the padded all-gather layout
 int64_t x_extent(const ek_ctx* c) { return c->nranks > 1 ? c->slot * c->nranks : c->n; }
 
+// The column-panel form when x outgrows an XCD's L2 share (EK_SPMV_PANEL=0/1
+// forces it off/on; default: x > 3 MB, i.e. the 2x and 10x synthetics, not
+// the 1x one whose 1.6 MB x every L2 keeps)
+bool want_panels(const ek_ctx* c) {
+    if (const char* e = std::getenv("EK_SPMV_PANEL"); e && e[0]) return e[0] != '0';
+    return x_extent(c) * 8 > (int64_t(3) << 20);
+}
+
+// Build the panel layout from this rank's coded CSR on the device (rowptr_d,
+// pk_d: (code << colbits) | col words); rowptr_h is the host copy.  False
+// when the codes do not fit beside the panel column bits.
+bool build_panels(ek_ctx* c, hipStream_t s, const int32_t* rowptr_h, const int32_t* rowptr_d, const uint32_t* pk_d,
+                  int colbits, int64_t ncodes) {
+    const int64_t X = x_extent(c);
+    int pb = 17;  // 1 MB of x per panel
+    while (((X + (int64_t(1) << pb) - 1) >> pb) > ek::dev::MAX_PANELS) ++pb;
+    if (pb >= 32 || ncodes > (int64_t(1) << (32 - pb))) return false;
+    const int P = int((X + (int64_t(1) << pb) - 1) >> pb);
+    const int64_t nnz = rowptr_h[c->nrows];
+    // ~12 K entries per workgroup (10x: 1,063 workgroups, 4 per CU)
+    auto wr = ek::dev::panel_row_ranges(rowptr_h, c->nrows, int(std::max<int64_t>(256, nnz / 12288)));
+    const int G = int(wr.size()) - 1;
+    int max_rows = 1;
+    for (int w = 0; w < G; ++w) max_rows = std::max(max_rows, wr[size_t(w) + 1] - wr[size_t(w)]);
+    upload(c->pn_wrow, wr.data(), wr.size(), s);
+    DBuf cnt, tiles;
+    cnt.ensure(size_t(G) * P * 4 + 4);
+    tiles.ensure((size_t(G) * P / 1024 + 4) * 8);
+    c->pn_start.ensure((size_t(G) * P + 1) * 8);
+    c->pn_word.ensure(size_t(std::max<int64_t>(nnz, 1)) * 4);
+    c->pn_rid.ensure(size_t(std::max<int64_t>(nnz, 1)) * 2);
+    ek::dev::panel_count(s, G, rowptr_d, pk_d, colbits, c->pn_wrow.as<int32_t>(), pb, P, cnt.as<int>());
+    ek::dev::exclusive_scan(s, cnt.as<int>(), (long long)G * P, c->pn_start.as<long long>(), tiles.as<long long>());
+    ek::dev::panel_fill(s, G, rowptr_d, pk_d, colbits, c->pn_wrow.as<int32_t>(), pb, P, c->pn_start.as<long long>(),
+                        c->pn_word.as<uint32_t>(), c->pn_rid.as<uint16_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));  // the temporaries and the host row ranges go out of scope
+    c->pn_G = G;
+    c->pn_P = P;
+    c->pn_pb = pb;
+    c->pn_max_rows = max_rows;
+    c->nrb_spmv = G;  // the alpha partials: one per workgroup
+    c->mat_bytes = nnz * 6 + int64_t(G) * P * 8 + int64_t(wr.size()) * 4 + ncodes * 8;
+    return true;
+}
+
 // Global column -> the all-gather layout (host copy of k_remap_cols)
 void remap_cols_host(const ek_ctx* c, const int32_t* col, int64_t nnz, std::vector<int32_t>& out) {
     out.resize(size_t(nnz));
@@ -468,6 +530,24 @@ void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, cons
     pt.mark("pack");
     // 512-nnz blocks (tools/spmv_lab.hip for plain CSR; for the coded form,
     // 1024-nnz segments measured 14.3 against 12.7 us inside the solve)
+    c->pn_G = 0;
+    if (packed && want_panels(c)) {
+        DBuf rp_d, pk_d;
+        upload(c->dict, dictv.data(), dictv.size(), c->stream);
+        upload(rp_d, rowptr, size_t(nrows) + 1, c->stream);
+        upload(pk_d, pkv.data(), pkv.size(), c->stream);
+        if (build_panels(c, c->stream, rowptr, rp_d.as<int32_t>(), pk_d.as<uint32_t>(), colbits, int64_t(dictv.size()))) {
+            c->colbits = colbits;
+            c->pk.reset();
+            c->rel.reset();
+            c->col.reset();
+            c->val.reset();
+            c->rowptr.reset();
+            c->rb.reset();
+            pt.mark("panels");
+            return;
+        }
+    }
     c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
     auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
     c->nrb_spmv = int(rbv.size() / 4);
@@ -693,6 +773,22 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         HIPCHK(hipStreamSynchronize(s));
         ncodes = nd;
         packed = cnt_h[1] == 0 && nd <= TSIZE / 2 && nd <= (int64_t(1) << (32 - colbits));
+    }
+    c->pn_G = 0;
+    if (packed && want_panels(c)) {
+        DBuf pk_d;
+        c->dict.ensure(size_t(std::max<int64_t>(ncodes, 1)) * 8);
+        ek::dev::dict_values(s, c->lb_table.as<unsigned long long>(), TSIZE, c->lb_codes.as<long long>(),
+                             c->dict.as<double>());
+        pk_d.ensure(size_t(std::max<int64_t>(nnz, 1)) * 4);
+        ek::dev::encode_words(s, nnz, c->col.as<int>(), c->val.as<double>(), c->lb_table.as<unsigned long long>(), TSIZE,
+                              c->lb_codes.as<long long>(), colbits, pk_d.as<uint32_t>());
+        if (build_panels(c, s, rowptr.data(), c->rowptr.as<int32_t>(), pk_d.as<uint32_t>(), colbits, ncodes)) {
+            c->colbits = colbits;
+            pt.mark("panels");
+            if (on_device) *on_device = 1;
+            return EK_OK;
+        }
     }
     c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
     auto rbv = ek::dev::spmv_row_blocks(rowptr.data(), nrows, c->block_nnz);
@@ -1001,6 +1097,11 @@ struct Lanczos {
     // i - 1 in its SpMV, also across chunks; the last step of the cycle is
     // finalized by its own launch.
     void factorize_fused(int k, int kend) {
+        // EK_LANCZOS_TT=0: the separate three-term launch (A/B; the same bits)
+        static const bool tt_fused = [] {
+            const char* e = std::getenv("EK_LANCZOS_TT");
+            return !(e && e[0] == '0');
+        }();
         double* fn2 = c->fn2.as<double>();
         double* a3 = c->scal.as<double>() + 2;
         const double* bov = c->bov.as<double>();
@@ -1019,14 +1120,21 @@ struct Lanczos {
                 fin.bov_i = bov + i - 1;
             }
             const bool timed = spmv_timed_step(i);
+            // the SpMV's last block also reduces alpha into a3 (k_three_term's bits)
             ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
                           c->apart.as<double>(), i > seg0 ? &fin : nullptr,
-                          timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
+                          timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr,
+                          tt_fused ? a3 : nullptr, c->actr.as<unsigned>());
             ++matvecs;
             const int nc = i + 1;
-            ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
-                                i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>());
-            ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
+            if (tt_fused) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
+                ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
+                                  i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>());
+            } else {
+                ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
+                                    i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>());
+                ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
+            }
             ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
                               c->f.as<double>(), c->f.as<double>(), c->npart.as<double>());
         }
@@ -1144,6 +1252,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     c->apart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
     c->Qd.ensure(size_t(m) * size_t(m + 1) * 8);
     c->scal.ensure(64);
+    if (!c->actr.p) {
+        c->actr.ensure(64);
+        HIPCHK(hipMemsetAsync(c->actr.p, 0, 64, s));
+    }
     // padded rows must be exactly 0 (only those: every kernel writes real
     // rows before it reads them, and no kernel writes a padded row nonzero)
     ek::dev::zero_pad_rows(s, c->V.as<double>(), L.ldv, L.nreal, m + 1);

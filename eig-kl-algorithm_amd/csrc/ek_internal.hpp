@@ -168,6 +168,33 @@ std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int b
 // fin: the previous step's finalize folded in (then ||f||^2 comes from it, not *fn2).
 // ev_start/ev_stop: kernel start/end timestamps (hipExtLaunchKernelGGL), optional.
 //
+// Column-panel form (kernels_panel.hip) for an x larger than an XCD's L2
+// share: G persistent workgroups over equal-nnz row ranges (<= PANEL_MAX_ROWS
+// rows each), the entries bucketed by (workgroup, panel of 2^pb columns):
+// bucket (w, p) = [start[w*P + p], start[w*P + p + 1]), each entry a word
+// (code << pb) | column-in-panel and a row index relative to wrow[w].
+constexpr int MAX_PANELS = 64;
+constexpr int PANEL_MAX_ROWS = 8192;
+struct SpmvPanel {
+    int G = 0, P = 0, pb = 0, max_rows = 0;
+    const int32_t* wrow = nullptr;   // G + 1
+    const long long* start = nullptr;  // G * P + 1
+    const uint32_t* word = nullptr;
+    const uint16_t* rid = nullptr;
+};
+size_t panel_lds_bytes(int max_rows);
+void panel_count(hipStream_t s, int G, const int32_t* rowptr, const uint32_t* pk, int colbits, const int32_t* wrow,
+                 int pb, int P, int* cnt);
+void panel_fill(hipStream_t s, int G, const int32_t* rowptr, const uint32_t* pk, int colbits, const int32_t* wrow,
+                int pb, int P, const long long* start, uint32_t* word, uint16_t* rid);
+void spmv_panel(hipStream_t s, const SpmvPanel& m, const double* dict, const double* x, double* y, const double* fn2,
+                const double* f, double* vcol, double* apart, const StepFin* fin, hipEvent_t ev_start,
+                hipEvent_t ev_stop, double* alpha_out, unsigned* actr);
+// host: the workgroup row ranges (equal nnz, <= PANEL_MAX_ROWS rows each)
+std::vector<int32_t> panel_row_ranges(const int32_t* rowptr, int64_t nrows, int target_groups);
+// pk[e] = (code << colbits) | col[e] from the device build's value table
+void encode_words(hipStream_t s, long long nnz, const int* col, const double* val, const unsigned long long* table,
+                  int tsize, const long long* code_of_slot, int colbits, uint32_t* pk);
 // Matrix storage: plain CSR (col int32 + val fp64, 12 B per entry) or the
 // value-dictionary form (pk != null): one 32-bit word per entry,
 // (code << colbits) | col, with val = dict[code].  A clique Laplacian holds few
@@ -184,6 +211,7 @@ struct SpmvMat {
     const uint32_t* pk = nullptr;  // per-block segments of the coded words (spmv_segment)
     const uint16_t* rel = nullptr;  // row starts inside each segment
     const double* dict = nullptr;
+    SpmvPanel panel;  // panel.G > 0: the column-panel form (pk/rel/col/val unused)
 };
 constexpr int SPMV_SEG_NNZ = 512;     // default block_nnz (segment size) of the coded form
 constexpr int SPMV_REL_STRIDE = 258;  // rel entries per block (nrows + 1 <= 257, padded)
@@ -194,9 +222,12 @@ bool spmv_pack(int64_t n, int64_t nnz, const int32_t* col, const double* val, st
 // desc (from spmv_row_blocks with SPMV_SEG_NNZ) is updated for long rows.
 void spmv_segment(std::vector<int32_t>& desc, const int32_t* rowptr, const std::vector<uint32_t>& pk, int seg_nnz,
                   std::vector<uint32_t>& seg, std::vector<uint16_t>& rel);
+// alpha_out (with apart): the last block to finish also reduces every block's
+// alpha partial (k_three_term's order and bits) into *alpha_out; actr: a
+// device counter, zero before the first such launch (re-armed by each)
 void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
           double* vcol, double* apart, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
-          hipEvent_t ev_stop = nullptr);
+          hipEvent_t ev_stop = nullptr, double* alpha_out = nullptr, unsigned* actr = nullptr);
 
 // kernels_build.hip — the Laplacian rows built on the device from the pins
 struct LapBuild {
@@ -257,6 +288,11 @@ void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has
 void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
                const double* hall, const double* w, const double* vi, const double* vim1, const double* fn2_i,
                const double* bov_i, double* dst, double* npart, double* alpha, double* offd);
+// gemvt of the three-term residual f' = w - *alpha vi - beta_i vim1 (vim1 may
+// be null; beta_i as three_term), formed per row; f' is also stored to fp
+void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
+              const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
+              const double* bov_i, double* fp, double* part);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 

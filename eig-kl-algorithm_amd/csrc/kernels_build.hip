@@ -383,7 +383,23 @@ __global__ __launch_bounds__(BT) void k_encode(const int4* __restrict__ desc, co
     for (int t = threadIdx.x; t < SPMV_REL_STRIDE; t += BT) rl[t] = uint16_t(t <= nr ? rowptr[r0 + t] - p0 : cnt);
 }
 
+__global__ __launch_bounds__(BT) void k_encode_words(long long nnz, const int* __restrict__ col,
+                                                     const double* __restrict__ val,
+                                                     const unsigned long long* __restrict__ table, unsigned mask,
+                                                     const long long* __restrict__ code_of_slot, int colbits,
+                                                     uint32_t* __restrict__ pk) {
+    const long long e = (long long)blockIdx.x * BT + threadIdx.x;
+    if (e < nnz) pk[e] = (code_of(val[e], table, mask, code_of_slot) << colbits) | uint32_t(col[e]);
+}
+
 }  // namespace
+
+void encode_words(hipStream_t s, long long nnz, const int* col, const double* val, const unsigned long long* table,
+                  int tsize, const long long* code_of_slot, int colbits, uint32_t* pk) {
+    if (nnz > 0)
+        hipLaunchKernelGGL(k_encode_words, dim3(grid_of(nnz)), dim3(BT), 0, s, nnz, col, val, table, unsigned(tsize - 1),
+                           code_of_slot, colbits, pk);
+}
 
 void exclusive_scan(hipStream_t s, const int* in, long long n, long long* out, long long* tiles) {
     const int ntiles = int((n + SCAN_TILE - 1) / SCAN_TILE);

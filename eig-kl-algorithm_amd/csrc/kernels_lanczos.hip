@@ -71,9 +71,19 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 // blocks with all their column groups (the guide's bijective XCD remap), so
 // a row block's slice of w is fetched into one XCD's L2 and re-read from
 // there by its other column groups.  Same partials, same bits.
+// TT: the right-hand side is the three-term residual f' = w - alpha v_i -
+// beta_i v_{i-1}, formed per row with k_three_term's operations (alpha from
+// the SpMV's last block, beta_i from ||f_i||^2 or the injected override),
+// and the column-group-0 block of each row block stores it to fp for the
+// update: the three-term launch and its per-block re-reduction of the alpha
+// partials are gone, the bits are the same.
+template <bool TT>
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
-                                               double* __restrict__ part) {
+                                               double* __restrict__ part, const double* __restrict__ alpha,
+                                               const double* __restrict__ vi, const double* __restrict__ vim1,
+                                               const double* __restrict__ fn2_i, const double* __restrict__ bov_i,
+                                               double* __restrict__ fp) {
     __shared__ double red[4][GT_COLS];
     const int t = threadIdx.x;
     const int ncg = (ncols + has_u0 + GT_COLS - 1) / GT_COLS;
@@ -90,14 +100,35 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     // are unchanged
     constexpr int KR = GT_ROWS / 512;
     const int jmax = ncols > 0 ? ncols - 1 : 0;
-    double2 xs[KR], vs[KR][GT_COLS];
+    double2 xs[KR], vs[KR][GT_COLS], tv[KR], tu[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
         const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
         xs[k] = *reinterpret_cast<const double2*>(w + r);
+        if constexpr (TT) {
+            tv[k] = *reinterpret_cast<const double2*>(vi + r);
+            tu[k] = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
+        }
 #pragma unroll
         for (int jj = 0; jj < GT_COLS; ++jj)
             vs[k][jj] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+    }
+    if constexpr (TT) {  // k_three_term's f' (same operations, same order)
+        const double a = *alpha;
+        const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            double2 y = xs[k];
+            y.x -= a * tv[k].x;
+            y.y -= a * tv[k].y;
+            if (vim1) {
+                y.x -= b * tu[k].x;
+                y.y -= b * tu[k].y;
+            }
+            xs[k] = y;
+            if (j0 == 0)
+                *reinterpret_cast<double2*>(fp + size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t)) = y;
+        }
     }
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -624,8 +655,16 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
            const double* w, double* part) {
     const int cols = ncols + has_u0;
     if (cols <= 0) return;
-    hipLaunchKernelGGL(k_gemvt, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V, ncols,
-                       has_u0, u0val, nreal, w, part);
+    hipLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
+                       ncols, has_u0, u0val, nreal, w, part, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
+              const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
+              const double* bov_i, double* fp, double* part) {
+    const int cols = ncols + has_u0;
+    hipLaunchKernelGGL(k_gemvt<true>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
+                       ncols, has_u0, u0val, nreal, w, part, alpha, vi, vim1, fn2_i, bov_i, fp);
 }
 
 

@@ -71,6 +71,41 @@ __device__ __forceinline__ double block_sum_all(double s, double* wsum) {
     return r;
 }
 
+// The three-term recurrence's alpha = sum of every block's partial, reduced by
+// the LAST block to finish (no separate launch; k_three_term's order: each
+// thread sums the partials t, t + 256, ... in turn, then the fixed tree, so
+// alpha has the bits k_three_term computes).  Hand-off (MI355X_MICROARCH.md,
+// inter-workgroup visibility, the sc1 row): each block's partial is stored
+// sc1 by thread 0, which waits for it (vmcnt 0) before its agent-scope add to
+// the counter; the block whose add returns gridDim - 1 reads every partial
+// with sc1 loads after a barrier, publishes alpha and re-arms the counter
+// (visible to the next launch at the kernel boundary).
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+    return __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+__device__ __forceinline__ void alpha_handoff(const double* apart, double* alpha_out, unsigned* ctr, double* wsum,
+                                              int* s_last) {
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = old == gridDim.x - 1u ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    double s = 0.0;
+    for (int i = int(threadIdx.x); i < int(gridDim.x); i += SPMV_THREADS) s += load_sc1(apart + i);
+    s = block_sum_all(s, wsum);
+    if (threadIdx.x == 0) {
+        *alpha_out = s;
+        *ctr = 0u;
+    }
+}
+
 // PK: entries are dictionary-coded 32-bit words in per-block segments
 // (SpmvMat::seg, spmv_segment); `col` then holds the segments, `val` the
 // dictionary and `rel` the row starts inside each segment.  Block b's entries
@@ -87,12 +122,14 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
                                                                 const double* __restrict__ fn2,
                                                                 const double* __restrict__ f,
                                                                 double* __restrict__ vcol, double* __restrict__ apart,
-                                                                StepFin fin) {
+                                                                StepFin fin, double* __restrict__ alpha_out,
+                                                                unsigned* __restrict__ actr) {
     constexpr int PER = BLOCK_NNZ / SPMV_THREADS;
     __shared__ double prod[BLOCK_NNZ];
     __shared__ int rbeg[SPMV_THREADS + 1];
     __shared__ double yrow[SPMV_THREADS];
     __shared__ double wsum[SPMV_THREADS / 64];
+    __shared__ int s_last;
     const int t = threadIdx.x;
     uint32_t wd[PER];
     int rb0 = 0, rb1 = 0;
@@ -147,9 +184,10 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
             if (vcol) {
                 const double v = f[r0] * scale;
                 vcol[r0] = v;
-                if (apart) apart[blockIdx.x] = v * (a * scale);
+                if (apart) store_sc1(apart + blockIdx.x, v * (a * scale));
             }
         }
+        if (alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
         return;
     }
     // stream mode: every global load of the block is issued before the first
@@ -215,13 +253,19 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
             for (int o = 32; o > 0; o >>= 1) av += __shfl_xor(av, o, 64);
             if ((t & 63) == 0) wsum[t >> 6] = av;
             __syncthreads();
-            if (t == 0) apart[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+            if (t == 0) store_sc1(apart + blockIdx.x, (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]));
         }
     }
+    if (alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
 }
 
 void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
-          double* vcol, double* apart, const StepFin* fin, hipEvent_t ev_start, hipEvent_t ev_stop) {
+          double* vcol, double* apart, const StepFin* fin, hipEvent_t ev_start, hipEvent_t ev_stop, double* alpha_out,
+          unsigned* actr) {
+    if (m.panel.G > 0) {
+        spmv_panel(s, m.panel, m.dict, x, y, fn2, f, vcol, apart, fin, ev_start, ev_stop, alpha_out, actr);
+        return;
+    }
     if (m.nblocks <= 0) return;
     const int4* d = reinterpret_cast<const int4*>(m.desc);
     const StepFin fv = fin ? *fin : StepFin{};
@@ -231,7 +275,7 @@ void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const dou
     // rocprofv3 reports), not event packets around it
 #define EK_SPMV_LAUNCH(BN, PK)                                                                                 \
     hipExtLaunchKernelGGL(k_spmv_adaptive<BN, PK>, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, ev_start, ev_stop, 0, \
-                          d, m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv)
+                          d, m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv, alpha_out, actr)
     if (m.pk) {
         EK_SPMV_LAUNCH(SPMV_SEG_NNZ, true);
     } else {

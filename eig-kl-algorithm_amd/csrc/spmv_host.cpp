@@ -180,5 +180,22 @@ void spmv_segment(std::vector<int32_t>& desc, const int32_t* rowptr, const std::
     });
 }
 
+
+// Workgroup row ranges of the column-panel form: contiguous, an equal share
+// of the entries each, at most PANEL_MAX_ROWS rows (the LDS accumulators).
+std::vector<int32_t> panel_row_ranges(const int32_t* rowptr, int64_t nrows, int target_groups) {
+    const int64_t nnz = rowptr[nrows];
+    const int64_t want = std::max<int64_t>(1, (nnz + target_groups - 1) / std::max(1, target_groups));
+    std::vector<int32_t> w{0};
+    int64_t r = 0;
+    while (r < nrows) {
+        const int64_t r_nnz = std::upper_bound(rowptr + r, rowptr + nrows + 1, int64_t(rowptr[r]) + want - 1) - rowptr;
+        int64_t r1 = std::min<int64_t>({nrows, std::max<int64_t>(r + 1, r_nnz), r + PANEL_MAX_ROWS});
+        w.push_back(int32_t(r1));
+        r = r1;
+    }
+    return w;
+}
+
 }  // namespace dev
 }  // namespace ek

@@ -80,6 +80,49 @@ def test_spmv_dictionary_form_bit_identical(ek, ctx, monkeypatch, which):
     assert np.array_equal(out[False][2], out[True][2])
 
 
+def _sequential_rows(L, x):
+    """y[r] = (((0 + v0 x0) + v1 x1) + ...) over the row in ascending column
+    order: every product rounded, then added left to right (no FMA)."""
+    rp = L.rowptr.astype(np.int64)
+    ln = np.diff(rp)
+    y = np.zeros(len(ln))
+    for k in range(int(ln.max())):
+        live = ln > k
+        e = rp[:-1][live] + k
+        y[live] = y[live] + L.val[e] * x[L.col[e]]
+    return y
+
+
+@pytest.mark.parametrize("which", ["ibm01", "industry2", "syn0.25"])
+@pytest.mark.parametrize("path", ["host_csr", "pins"])
+def test_spmv_panel_form_is_the_sequential_row_sum(ek, ctx, monkeypatch, which, path):
+    """The column-panel SpMV (kernels_panel.hip; chosen by default once x
+    outgrows an XCD's L2, forced here on small graphs): each row summed
+    strictly left to right in column order, bit for bit, through both setup
+    paths (host CSR, device build from the pins)."""
+    h = ek.Hypergraph.generate(0.25, 3) if which == "syn0.25" else ek.Hypergraph.read(circuit_path(which))
+    L = h.laplacian()
+    monkeypatch.setenv("EK_SPMV_PANEL", "1")
+    if path == "pins":
+        assert ctx.spmv_setup_pins(h) is True
+    else:
+        ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    x = np.random.default_rng(3).standard_normal(h.nodes)
+    y = ctx.spmv_host(x)
+    assert np.array_equal(y.view(np.uint64), _sequential_rows(L, x).view(np.uint64))
+
+
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
+def test_spmv_panel_form_lanczos_golden(ek, ctx, monkeypatch, name):
+    monkeypatch.setenv("EK_SPMV_PANEL", "1")
+    h = ek.Hypergraph.read(circuit_path(name))
+    assert ctx.spmv_setup_pins(h) is True
+    lam, v, st = ctx.lanczos_fiedler()
+    assert st["converged"] and st["residual"] < 1e-9
+    lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
+    _fiedler_parity(name, lam, v, lam_ref, med_ref, bits_ref, v_ref, ek)
+
+
 def test_spmv_dictionary_overflow_falls_back(ek, ctx):
     """More distinct values than the code bits hold -> plain CSR, same result."""
     n = 1 << 20  # colbits 20 -> 4096 codes; 6000 distinct values do not fit
@@ -249,6 +292,32 @@ def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
     if name != "ibm10":
         lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
         _fiedler_parity(name, lam_b, v_b, lam_ref, med_ref, bits_ref, v_ref, ek)
+
+
+@pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
+def test_lanczos_three_term_fused_bit_identical(ek, tmp_path, which):
+    """The single-GPU step without the three-term launch (alpha reduced by the
+    SpMV's last block, f' formed inside the projection) gives the bits of the
+    step with it (EK_LANCZOS_TT=0): the same reductions in the same order.
+    syn0.25 goes through breakdowns (injected vectors, beta = 0), syn2 through
+    the column-panel SpMV."""
+    import subprocess
+    import sys
+    gen = {"ibm01": "ek.Hypergraph.read(circuit_path('ibm01'))", "syn0.25": "ek.Hypergraph.generate(0.25, 3)",
+           "syn2": "ek.Hypergraph.generate(2.0, 2)"}[which]
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); from conftest import load_package, circuit_path; "
+        "ek = load_package(); h = %s; c = ek.Context(0); c.spmv_setup_pins(h); lam, v, st = c.lanczos_fiedler(); "
+        "np.save(sys.argv[1], np.concatenate([[lam, st['matvecs'], st['residual']], v]))"
+    ) % (os.path.dirname(os.path.abspath(__file__)), gen)
+    env = dict(os.environ)
+    a, b = str(tmp_path / "tt.npy"), str(tmp_path / "sep.npy")
+    subprocess.run([sys.executable, "-c", code, a], check=True, timeout=180, env=env)
+    env["EK_LANCZOS_TT"] = "0"
+    subprocess.run([sys.executable, "-c", code, b], check=True, timeout=180, env=env)
+    x, y = np.load(a), np.load(b)
+    assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
+    assert x[2] < 1e-8
 
 
 @pytest.mark.parametrize("name", ["ibm01", "industry2", "fract"])

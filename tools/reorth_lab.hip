@@ -158,8 +158,9 @@ int main(int argc, char** argv) {
             std::printf("J=%3d %-34s %8.2f us  %7.1f GB/s\n", J, name, us, bytes / us / 1e3);
         };
         rep("gemvt (prod, 1024x8 tiles)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL(k_gemvt, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a, b, 0,
-                                      ldv, nrb, V, J, 1, u0val, n, w, part);
+                hipExtLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
+                                      b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr);
             }),
             vbytes + 8.0 * n);
         rep("update<true> (prod, RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
