@@ -88,6 +88,7 @@ inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::d
 
 struct ek_ctx {
     int device = 0;
+    int num_cu = 256;  // compute units (the panel SpMV's resident workgroups)
     hipStream_t stream = nullptr;
     // the KL graph's setup (ek_kl_graph_setup / ek_kl_nets_setup) runs on its
     // own stream: ek_solve_file calls it from its host thread while the
@@ -117,7 +118,7 @@ struct ek_ctx {
     int64_t slot = 0;
     DBuf off_d, xexp;
     // the column-panel form of the SpMV (pn_G > 0; kernels_panel.hip)
-    int pn_G = 0, pn_P = 0, pn_pb = 0, pn_max_rows = 0;
+    int pn_G = 0, pn_P = 0, pn_pb = 0, pn_max_rows = 0, pn_ndict = 0;
     DBuf pn_wrow, pn_start, pn_word, pn_rid;
     int block_nnz = 1024, nrb_spmv = 0;
     DBuf rb, rowptr, col, val, pk, rel, dict;
@@ -194,6 +195,7 @@ ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
         m.panel.P = c->pn_P;
         m.panel.pb = c->pn_pb;
         m.panel.max_rows = c->pn_max_rows;
+        m.panel.ndict = c->pn_ndict;
         m.panel.wrow = c->pn_wrow.as<int32_t>();
         m.panel.start = c->pn_start.as<long long>();
         m.panel.word = c->pn_word.as<uint32_t>();
@@ -318,6 +320,7 @@ int ek_init(int device, ek_ctx** out) {
         ek::fail(EK_EHIP, "device %d is %s; this build targets gfx950 (MI355X)", device, prop.gcnArchName);
     auto c = std::make_unique<ek_ctx>();
     c->device = device;
+    c->num_cu = std::max(1, prop.multiProcessorCount);
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
@@ -440,12 +443,13 @@ void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
 // The column space the SpMV reads: global ids, or the padded all-gather layout
 int64_t x_extent(const ek_ctx* c) { return c->nranks > 1 ? c->slot * c->nranks : c->n; }
 
-// The column-panel form when x outgrows an XCD's L2 share (EK_SPMV_PANEL=0/1
-// forces it off/on; default: x > 3 MB, i.e. the 2x and 10x synthetics, not
-// the 1x one whose 1.6 MB x every L2 keeps)
+// The column-panel form when x outgrows an XCD's L2 (EK_SPMV_PANEL=0/1 forces
+// it off/on; default: x > 8 MB, the 10x synthetic.  At 2x (3.2 MB) the two
+// forms took the same time inside the solve, 29 vs 30 us, and the 1x x
+// stays in every L2: tools/panel_lab.py)
 bool want_panels(const ek_ctx* c) {
     if (const char* e = std::getenv("EK_SPMV_PANEL"); e && e[0]) return e[0] != '0';
-    return x_extent(c) * 8 > (int64_t(3) << 20);
+    return x_extent(c) * 8 > (int64_t(8) << 20);
 }
 
 // Build the panel layout from this rank's coded CSR on the device (rowptr_d,
@@ -454,16 +458,25 @@ bool want_panels(const ek_ctx* c) {
 bool build_panels(ek_ctx* c, hipStream_t s, const int32_t* rowptr_h, const int32_t* rowptr_d, const uint32_t* pk_d,
                   int colbits, int64_t ncodes) {
     const int64_t X = x_extent(c);
-    int pb = 17;  // 1 MB of x per panel
+    int pb = 17;  // 1 MB of x per panel (EK_PANEL_PB: lab override)
+    if (const char* e = std::getenv("EK_PANEL_PB"); e && std::atoi(e) >= 10 && std::atoi(e) <= 24) pb = std::atoi(e);
     while (((X + (int64_t(1) << pb) - 1) >> pb) > ek::dev::MAX_PANELS) ++pb;
     if (pb >= 32 || ncodes > (int64_t(1) << (32 - pb))) return false;
     const int P = int((X + (int64_t(1) << pb) - 1) >> pb);
     const int64_t nnz = rowptr_h[c->nrows];
-    // ~12 K entries per workgroup (10x: 1,063 workgroups, 4 per CU)
-    auto wr = ek::dev::panel_row_ranges(rowptr_h, c->nrows, int(std::max<int64_t>(256, nnz / 12288)));
-    const int G = int(wr.size()) - 1;
-    int max_rows = 1;
-    for (int w = 0; w < G; ++w) max_rows = std::max(max_rows, wr[size_t(w) + 1] - wr[size_t(w)]);
+    // The most workgroups (<= 8 per CU) that are all resident at once, so they
+    // walk the panels together (a straggling second round of workgroups
+    // measured 90 -> 124 us at 10x): each holds its rows' accumulators in LDS.
+    std::vector<int32_t> wr;
+    int G = 0, max_rows = 1;
+    for (int per_cu = 8; per_cu >= 1; --per_cu) {
+        wr = ek::dev::panel_row_ranges(rowptr_h, c->nrows, per_cu * c->num_cu);
+        G = int(wr.size()) - 1;
+        max_rows = 1;
+        for (int w = 0; w < G; ++w) max_rows = std::max(max_rows, wr[size_t(w) + 1] - wr[size_t(w)]);
+        const int fit = int(std::min<size_t>(8, (160 * 1024) / (ek::dev::panel_lds_bytes(max_rows, int(ncodes)) + 1024)));
+        if (G <= fit * c->num_cu) break;
+    }
     upload(c->pn_wrow, wr.data(), wr.size(), s);
     DBuf cnt, tiles;
     cnt.ensure(size_t(G) * P * 4 + 4);
@@ -481,6 +494,7 @@ bool build_panels(ek_ctx* c, hipStream_t s, const int32_t* rowptr_h, const int32
     c->pn_P = P;
     c->pn_pb = pb;
     c->pn_max_rows = max_rows;
+    c->pn_ndict = int(ncodes);
     c->nrb_spmv = G;  // the alpha partials: one per workgroup
     c->mat_bytes = nnz * 6 + int64_t(G) * P * 8 + int64_t(wr.size()) * 4 + ncodes * 8;
     return true;
@@ -1253,8 +1267,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     c->Qd.ensure(size_t(m) * size_t(m + 1) * 8);
     c->scal.ensure(64);
     if (!c->actr.p) {
-        c->actr.ensure(64);
-        HIPCHK(hipMemsetAsync(c->actr.p, 0, 64, s));
+        c->actr.ensure((ek::dev::ALPHA_SUB + 1) * 256);
+        HIPCHK(hipMemsetAsync(c->actr.p, 0, c->actr.bytes, s));
     }
     // padded rows must be exactly 0 (only those: every kernel writes real
     // rows before it reads them, and no kernel writes a padded row nonzero)

@@ -175,14 +175,15 @@ std::vector<int32_t> spmv_row_blocks(const int32_t* rowptr, int64_t nrows, int b
 // (code << pb) | column-in-panel and a row index relative to wrow[w].
 constexpr int MAX_PANELS = 64;
 constexpr int PANEL_MAX_ROWS = 8192;
+constexpr int PANEL_LDS_DICT = 2048;  // value-table entries the panel SpMV keeps in LDS
 struct SpmvPanel {
-    int G = 0, P = 0, pb = 0, max_rows = 0;
+    int G = 0, P = 0, pb = 0, max_rows = 0, ndict = 0;
     const int32_t* wrow = nullptr;   // G + 1
     const long long* start = nullptr;  // G * P + 1
     const uint32_t* word = nullptr;
     const uint16_t* rid = nullptr;
 };
-size_t panel_lds_bytes(int max_rows);
+size_t panel_lds_bytes(int max_rows, int ndict);
 void panel_count(hipStream_t s, int G, const int32_t* rowptr, const uint32_t* pk, int colbits, const int32_t* wrow,
                  int pb, int P, int* cnt);
 void panel_fill(hipStream_t s, int G, const int32_t* rowptr, const uint32_t* pk, int colbits, const int32_t* wrow,
@@ -222,6 +223,7 @@ bool spmv_pack(int64_t n, int64_t nnz, const int32_t* col, const double* val, st
 // desc (from spmv_row_blocks with SPMV_SEG_NNZ) is updated for long rows.
 void spmv_segment(std::vector<int32_t>& desc, const int32_t* rowptr, const std::vector<uint32_t>& pk, int seg_nnz,
                   std::vector<uint32_t>& seg, std::vector<uint16_t>& rel);
+constexpr int ALPHA_SUB = 32;  // first-level counters of the SpMV's last-block hand-off (64 uints apart)
 // alpha_out (with apart): the last block to finish also reduces every block's
 // alpha partial (k_three_term's order and bits) into *alpha_out; actr: a
 // device counter, zero before the first such launch (re-armed by each)

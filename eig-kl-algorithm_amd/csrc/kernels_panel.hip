@@ -38,7 +38,14 @@ namespace dev {
 namespace {
 
 constexpr int PT = 256;       // threads per workgroup
-constexpr int PCH = 4 * PT;   // entries per chunk (4 per thread)
+#ifndef EK_PANEL_DEPTH
+#define EK_PANEL_DEPTH 2  // chunks in flight: 2 = chunk k+1's gathers issued before chunk k's LDS phase
+#endif
+#ifndef EK_PANEL_PER
+#define EK_PANEL_PER 2
+#endif
+constexpr int PER = EK_PANEL_PER;  // entries per thread per chunk
+constexpr int PCH = PER * PT;  // entries per chunk
 
 // thread-strided partial of npart (the adaptive kernel's strided_sum order)
 __device__ __forceinline__ double panel_strided_sum(const double* __restrict__ x, int n, int stride) {
@@ -145,20 +152,26 @@ __global__ __launch_bounds__(PT) void k_panel_fill(const int32_t* __restrict__ r
     }
 }
 
+template <bool LDICT>
 __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __restrict__ dict,
                                                    const double* __restrict__ x, double* __restrict__ y,
                                                    const double* __restrict__ fn2, const double* __restrict__ f,
                                                    double* __restrict__ vcol, double* __restrict__ apart, StepFin fin,
                                                    double* __restrict__ alpha_out, unsigned* __restrict__ actr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* prod = reinterpret_cast<double*>(smem);      // [PCH]
-    double* acc = prod + PCH;                            // [max_rows]
-    uint16_t* rl = reinterpret_cast<uint16_t*>(acc + m.max_rows);  // [PCH]
+    double* prod = reinterpret_cast<double*>(smem);  // [2][PCH] (double-buffered chunks)
+    double* acc = prod + 2 * PCH;                    // [max_rows]
+    uint16_t* rl = reinterpret_cast<uint16_t*>(acc + m.max_rows);  // [2][PCH]
     __shared__ double wsum[PT / 64];
     __shared__ long long bst[MAX_PANELS + 1];
     __shared__ int s_last;
     const int w = blockIdx.x, t = threadIdx.x;
     const int r0 = m.wrow[w], nr = m.wrow[w + 1] - r0;
+    // the value table in LDS when it fits (PANEL_LDS_DICT entries): the
+    // per-entry lookup is then an LDS read instead of a second global gather
+    double* sdict = reinterpret_cast<double*>(rl + 2 * PCH);
+    if constexpr (LDICT)
+        for (int i = t; i < m.ndict; i += PT) sdict[i] = dict[i];
     const int P = m.P, pb = m.pb;
     const uint32_t pmask = (1u << pb) - 1u;
     for (int p = t; p <= P; p += PT) bst[p] = m.start[size_t(w) * P + p];
@@ -166,49 +179,129 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     // ||f||^2 of the previous step (its partials' loads go out first)
     const double npart_t = fin.npart ? panel_strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
     __syncthreads();
-    for (int p = 0; p < P; ++p) {
-        const long long b1 = bst[p + 1];
-        const double* xp = x + (size_t(p) << pb);
-        for (long long c0 = bst[p]; c0 < b1; c0 += PCH) {
-            const int cnt = int(min((long long)PCH, b1 - c0));
-            uint32_t wd[4];
-            uint16_t rr[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = t + u * PT;
-                wd[u] = i < cnt ? m.word[c0 + i] : 0u;
-                rr[u] = i < cnt ? m.rid[c0 + i] : uint16_t(0);
-            }
-            double xv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) xv[u] = xp[wd[u] & pmask];  // word 0 past cnt: a valid address
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = t + u * PT;
-                if (i < cnt) {
-                    prod[i] = dict[wd[u] >> pb] * xv[u];
-                    rl[i] = rr[u];
-                }
-            }
-            __syncthreads();
-            // the first entry of each row's run adds the run in order
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = t + u * PT;
-                if (i < cnt && (i == 0 || rl[i - 1] != rr[u])) {
-                    const int r = rr[u];
-                    double s = acc[r];
-                    int j = i;
-                    do {
-                        s += prod[j];
-                        ++j;
-                    } while (j < cnt && rl[j] == rr[u]);
-                    acc[r] = s;
-                }
-            }
-            __syncthreads();
+    // The workgroup's chunks, panel by panel (every workgroup walks the panels
+    // in the same order).  The next chunk's words and row indices are loaded
+    // while this chunk's gathers are in flight; the LDS staging alternates
+    // between two buffers, so one barrier per chunk orders both the staging
+    // and the accumulators (a row's runs in consecutive chunks are added
+    // after that barrier, in chunk order).
+    // Software pipeline, two chunks deep: chunk k+1's gathers of x and of the
+    // value table go out before chunk k's products are staged, and chunk
+    // k+2's words and row indices before those, so a chunk's dependent
+    // gathers overlap the previous chunk's LDS phase.
+    auto advance = [&](int& pp, long long& cc) {  // to the next non-empty chunk (pp == P: done)
+        while (pp < P && cc >= bst[pp + 1]) {
+            ++pp;
+            if (pp < P) cc = bst[pp];
         }
+    };
+    auto chunk_cnt = [&](int pp, long long cc) { return pp < P ? int(min((long long)PCH, bst[pp + 1] - cc)) : 0; };
+    auto load_words = [&](int pp, long long cc, uint32_t* wd, uint16_t* rr) {
+        const int cnt = chunk_cnt(pp, cc);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = t + u * PT;
+            wd[u] = i < cnt ? m.word[cc + i] : 0u;
+            rr[u] = i < cnt ? m.rid[cc + i] : uint16_t(0xffff);  // 0xffff: no entry
+        }
+    };
+    auto gather = [&](int pp, const uint32_t* wd, double* xv, double* dv) {
+        const double* xp = x + (size_t(pp < P ? pp : 0) << pb);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            xv[u] = xp[wd[u] & pmask];  // word 0 past cnt: a valid address
+            dv[u] = LDICT ? sdict[wd[u] >> pb] : dict[wd[u] >> pb];
+        }
+    };
+    // chunk k (p, c0), k+1 (p1, c1), k+2 (p2, c2)
+    int p = 0;
+    long long c0 = bst[0];
+    advance(p, c0);
+    int p1 = p;
+    long long c1 = c0 + PCH;
+    advance(p1, c1);
+    uint32_t wd0[PER], wd1[PER], wd2[PER];
+    uint16_t rr0[PER], rr1[PER], rr2[PER];
+    double xv0[PER], dv0[PER], xv1[PER], dv1[PER];
+    load_words(p, c0, wd0, rr0);
+    load_words(p1, c1, wd1, rr1);
+    gather(p, wd0, xv0, dv0);
+    int buf = 0;
+    while (p < P) {
+        const int cnt = chunk_cnt(p, c0);
+        int p2 = p1;
+        long long c2 = c1 + PCH;
+        advance(p2, c2);
+#if EK_PANEL_DEPTH == 2
+        gather(p1, wd1, xv1, dv1);     // chunk k+1's gathers
+#endif
+        load_words(p2, c2, wd2, rr2);  // chunk k+2's words
+        double* pr = prod + buf * PCH;
+        uint16_t* rb = rl + buf * PCH;
+        double my[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = t + u * PT;
+            my[u] = dv0[u] * xv0[u];
+            if (i < cnt) {
+                pr[i] = my[u];
+                rb[i] = rr0[u];
+            }
+        }
+        __syncthreads();
+        // The first entry of each row's run adds the run in order.  A thread's
+        // entries are 256 apart, so its heads are distinct rows: every LDS read
+        // they need (the previous and next entries' rows, the accumulators) is
+        // issued at once, and a run of one entry (most of them: ~1.2 entries
+        // per row and panel at 10x) needs no further read.
+        int prv[PER], nxt[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = t + u * PT;
+            prv[u] = rb[max(i - 1, 0)];
+            nxt[u] = rb[min(i + 1, PCH - 1)];
+        }
+        bool hd[PER];
+        double a0[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = t + u * PT;
+            hd[u] = i < cnt && (i == 0 || prv[u] != int(rr0[u]));
+            a0[u] = acc[hd[u] ? int(rr0[u]) : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            if (!hd[u]) continue;
+            const int i = t + u * PT;
+            double sum = a0[u] + my[u];
+            if (i + 1 < cnt && nxt[u] == int(rr0[u])) {
+                int j = i + 1;
+                do {
+                    sum += pr[j];
+                    ++j;
+                } while (j < cnt && rb[j] == rr0[u]);
+            }
+            acc[rr0[u]] = sum;
+        }
+#if EK_PANEL_DEPTH != 2
+        gather(p1, wd1, xv1, dv1);  // chunk k+1's gathers, after this chunk's LDS phase
+#endif
+        // rotate
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            wd1[u] = wd2[u];
+            rr0[u] = rr1[u];
+            rr1[u] = rr2[u];
+            xv0[u] = xv1[u];
+            dv0[u] = dv1[u];
+        }
+        p = p1;
+        c0 = c1;
+        p1 = p2;
+        c1 = c2;
+        buf ^= 1;
     }
+    __syncthreads();  // the last chunk's runs are in acc
     double n2 = fn2 ? *fn2 : 1.0;
     if (fin.npart) {
         n2 = panel_block_sum(npart_t, wsum);
@@ -238,26 +331,32 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     }
     if (alpha_out) {  // kernels_spmv.hip alpha_handoff: the last workgroup reduces alpha
         if (t == 0) {
+            const unsigned nb = gridDim.x, g = blockIdx.x % ALPHA_SUB;
+            const unsigned gsize = (nb - g + ALPHA_SUB - 1) / ALPHA_SUB, ngroups = nb < ALPHA_SUB ? nb : ALPHA_SUB;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned old = __hip_atomic_fetch_add(actr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = old == gridDim.x - 1u ? 1 : 0;
+            s_last = __hip_atomic_fetch_add(actr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u &&
+                             __hip_atomic_fetch_add(actr + ALPHA_SUB * 64, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1u
+                         ? 1
+                         : 0;
         }
         __syncthreads();
         if (s_last) {
             double s = 0.0;
             for (int i = t; i < int(gridDim.x); i += PT) s += panel_load_sc1(apart + i);
             s = panel_block_sum(s, wsum);
-            if (t == 0) {
-                *alpha_out = s;
-                *actr = 0u;
-            }
+            if (t < ALPHA_SUB + 1) actr[t * 64] = 0u;
+            if (t == 0) *alpha_out = s;
         }
     }
 }
 
 }  // namespace
 
-size_t panel_lds_bytes(int max_rows) { return size_t(PCH) * 8 + size_t(max_rows) * 8 + size_t(PCH) * 2; }
+size_t panel_lds_bytes(int max_rows, int ndict) {
+    return 2 * size_t(PCH) * 8 + size_t(max_rows) * 8 + 2 * size_t(PCH) * 2 +
+           (ndict <= PANEL_LDS_DICT ? size_t(ndict) * 8 : 0);
+}
 
 void panel_count(hipStream_t s, int G, const int32_t* rowptr, const uint32_t* pk, int colbits, const int32_t* wrow,
                  int pb, int P, int* cnt) {
@@ -273,8 +372,12 @@ void spmv_panel(hipStream_t s, const SpmvPanel& m, const double* dict, const dou
                 const double* f, double* vcol, double* apart, const StepFin* fin, hipEvent_t ev_start,
                 hipEvent_t ev_stop, double* alpha_out, unsigned* actr) {
     const StepFin fv = fin ? *fin : StepFin{};
-    hipExtLaunchKernelGGL(k_spmv_panel, dim3(m.G), dim3(PT), panel_lds_bytes(m.max_rows), s, ev_start, ev_stop, 0, m,
-                          dict, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);
+    if (m.ndict <= PANEL_LDS_DICT)
+        hipExtLaunchKernelGGL(k_spmv_panel<true>, dim3(m.G), dim3(PT), panel_lds_bytes(m.max_rows, m.ndict), s, ev_start,
+                              ev_stop, 0, m, dict, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);
+    else
+        hipExtLaunchKernelGGL(k_spmv_panel<false>, dim3(m.G), dim3(PT), panel_lds_bytes(m.max_rows, m.ndict), s,
+                              ev_start, ev_stop, 0, m, dict, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);
 }
 
 }  // namespace dev

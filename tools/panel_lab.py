@@ -21,6 +21,7 @@ for mult in mults:
         b = ctx.spmv_bytes(fused=False)
         us = ctx.spmv_bench(100, fused=False)
         usf = ctx.spmv_bench(100, fused=True)
+        ctx.lanczos_fiedler()  # warm (first-solve allocations)
         lam, _, st = ctx.lanczos_fiedler(time_spmv=True)
         us_in = 1e3 * st["spmv_ms"] / max(1, st["spmv_timed"])
         print(f"{mult:5.1f}x panel={panel}: b2b {us:8.2f} us ({b / us / 1e3 / 8000:.3f} of 8 TB/s), fused {usf:8.2f} us; "
