@@ -147,6 +147,8 @@ struct ek_ctx {
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
     double* chk_pin = nullptr;
     double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1))
+    ek::QRot* rot_pin = nullptr;  // ... and of its rotations (MAX_NCV x MAX_NCV)
+    DBuf rotd;
     // the last Fiedler vector as returned (normalised, sign fixed), kept on
     // the device for ek_kl_set_partition_fiedler, and that split's scratch
     DBuf fied, sp_sorted, sp_flag, sp_pos, sp_tmp;
@@ -349,6 +351,7 @@ void ek_destroy(ek_ctx* c) {
     (void)hipStreamDestroy(c->stream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
     if (c->q_pin) (void)hipHostFree(c->q_pin);
+    if (c->rot_pin) (void)hipHostFree(c->rot_pin);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->up) (void)hipHostFree(c->up);
@@ -1287,6 +1290,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                              hipHostMallocDefault));
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
                              size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) * 8, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->rot_pin),
+                             size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV) * sizeof(ek::QRot),
+                             hipHostMallocDefault));
     }
     if (L.time_spmv) {  // created once per context: ~200 creations per solve cost milliseconds
         while (c->spmv_ev.size() < size_t(2 * m)) {
@@ -1315,6 +1321,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
 
     std::vector<double> d(size_t(m), 0.0), e(size_t(m), 0.0), theta(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
     std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
+    std::vector<ek::QRot> rots;
+    static const bool host_q = std::getenv("EK_HOST_Q") != nullptr;
     int k = 0, restarts = 0, nconv = 0, injected = 0;
     double fn2_k = 1.0;  // ||f_k||^2 entering a cycle (after an implicit restart: the restart's residual)
     bool converged = false;
@@ -1469,20 +1477,38 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // its largest component, and some sizes lost 3-12x on one of them)
         const int knew = nev_adjusted(nev, m, nconv, zl);
         if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
-        double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
-        std::fill(Q, Q + size_t(m) * size_t(m), 0.0);
         std::vector<double> dd(d), ee(e);
-        for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
         const auto tq0 = std::chrono::steady_clock::now();
-        for (int i = knew; i < m; ++i)  // Q starts as the identity: lower bandwidth i - knew
-            ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q, i - knew);
+        double sigma = 0.0;               // Q(m-1, knew-1)
+        const double* sigma_dev = nullptr;  // ... or where the device left it
+        if (!host_q) {
+            // the shifts' rotations recorded on the host (O(m) each: the
+            // tridiagonal only), Q accumulated from them on the device
+            // (k_apply_rots, the host's operations: the same bits), which
+            // took ~0.2 ms of host time per restart with the GPU idle
+            rots.clear();
+            for (int i = knew; i < m; ++i)  // Q starts as the identity: lower bandwidth i - knew
+                ek::tridiag_qr_shift_rots(m, dd.data(), ee.data(), theta[size_t(i)], i - knew, rots);
+            const size_t rb = rots.size() * sizeof(ek::QRot);
+            std::memcpy(c->rot_pin, rots.data(), rb);  // pinned: the upload is a plain DMA
+            c->rotd.ensure(std::max<size_t>(rb, 64));
+            if (rb) HIPCHK(hipMemcpyAsync(c->rotd.p, c->rot_pin, rb, hipMemcpyHostToDevice, s));
+            ek::dev::apply_rots(s, m, c->rotd.as<ek::QRot>(), int(rots.size()), knew + 1, c->Qd.as<double>());
+            sigma_dev = c->Qd.as<double>() + size_t(knew - 1) * m + size_t(m - 1);
+        } else {  // EK_HOST_Q=1: accumulated on the host (A/B)
+            double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
+            std::fill(Q, Q + size_t(m) * size_t(m), 0.0);
+            for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
+            for (int i = knew; i < m; ++i)
+                ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q, i - knew);
+            sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];
+            HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
+        }
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
-        const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
-        const double hk = ee[size_t(knew - 1)];                         // H(knew, knew-1)
-        HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
+        const double hk = ee[size_t(knew - 1)];  // H(knew, knew-1)
         ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>());
         ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
-                            c->npart.as<double>());
+                            c->npart.as<double>(), sigma_dev);
         L.reduce_scalar(c->fn2.as<double>() + knew);
         HIPCHK(hipMemcpyAsync(&fn2_k, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
         std::swap(c->V.p, c->Vn.p);

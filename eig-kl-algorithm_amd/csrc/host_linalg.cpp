@@ -105,6 +105,16 @@ bool tridiag_eig(int m, const double* d_in, const double* e_in, double* evals, d
 // simply ran through a split would stop there and never shift the trailing
 // block, which is the one that carries the residual row (Q(m-1, :)).
 void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int band) {
+    tridiag_qr_shift_impl(m, d, e, mu, Q, band, nullptr);
+}
+
+// The same step with Q's rotations recorded instead of applied ({p, iend, c,
+// s} in order: Q <- Q G_p on rows < iend), for the device accumulation
+void tridiag_qr_shift_rots(int m, double* d, double* e, double mu, int band, std::vector<QRot>& rots) {
+    tridiag_qr_shift_impl(m, d, e, mu, nullptr, band, &rots);
+}
+
+void tridiag_qr_shift_impl(int m, double* d, double* e, double mu, double* Q, int band, std::vector<QRot>* rots) {
     if (m < 2) return;
     // band scratch: only |i-j| <= 2 is ever non-zero (the chase's bulge), so
     // row i keeps columns i-2 .. i+2 (5 entries; same operations, same order
@@ -144,11 +154,15 @@ void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int ban
             at(i, q) = -s * ap + c * aq;
         }
         if (!split[size_t(p)]) at(q, p - 1) = at(p - 1, q) = 0.0;  // bulge annihilated
-        double* qp = Q + size_t(p) * m;
-        double* qq = Q + size_t(q) * m;
         // Q has lower bandwidth `band` before this sweep, so columns p and q
         // are zero below row q + band: the rotation leaves those rows alone
         const int iend = band >= 0 ? std::min(m, q + band + 1) : m;
+        if (rots) {
+            rots->push_back(QRot{p, iend, c, s});
+            continue;
+        }
+        double* qp = Q + size_t(p) * m;
+        double* qq = Q + size_t(q) * m;
         for (int i = 0; i < iend; ++i) {
             const double a = qp[i], b = qq[i];
             qp[i] = c * a + s * b;

@@ -621,8 +621,9 @@ __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restri
 // f = f*sigma + x*hk, per-block sum of f^2
 __global__ __launch_bounds__(256) void k_axpby_norm(double* __restrict__ f, double sigma,
                                                     const double* __restrict__ x, double hk,
-                                                    double* __restrict__ npart) {
+                                                    double* __restrict__ npart, const double* __restrict__ sigma_dev) {
     __shared__ double lds4[4];
+    if (sigma_dev) sigma = *sigma_dev;
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
     double2 a = *reinterpret_cast<const double2*>(f + r);
     const double2 b = *reinterpret_cast<const double2*>(x + r);
@@ -759,8 +760,58 @@ void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, in
     hipLaunchKernelGGL(k_gemm_vq, dim3(ldv / UPD_ROWS, (kk + 7) / 8), dim3(256), 0, s, ldv, V, m, Q, kk, out);
 }
 
-void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart) {
-    hipLaunchKernelGGL(k_axpby_norm, dim3(ldv / UPD_ROWS), dim3(256), 0, s, f, sigma, x, hk, npart);
+void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart,
+                const double* sigma_dev) {
+    hipLaunchKernelGGL(k_axpby_norm, dim3(ldv / UPD_ROWS), dim3(256), 0, s, f, sigma, x, hk, npart, sigma_dev);
+}
+
+// The restart's Q on the device (ctx.cpp implicit restart): lane i owns row i
+// of Q (in LDS, odd stride) and applies every rotation in order, so no lane
+// ever reads another's data and no barrier is needed.  Within a sweep,
+// rotation p+1 takes column p+1 as rotation p left it: that value stays in a
+// register.  The host's rows-below-band skip is kept (a skipped row keeps its
+// exact zeros, as on the host), and the products and sums are separate
+// roundings (no contraction), so Q has the host's bits.
+__global__ __launch_bounds__(MAX_NCV) void k_apply_rots(int m, const QRot* __restrict__ rots, int nrot, int kk,
+                                                      double* __restrict__ Qout) {
+#pragma clang fp contract(off)
+    extern __shared__ double qs[];  // [MAX_NCV][m | 1]
+    const int i = threadIdx.x, ld = m | 1;
+    if (i < m)
+        for (int j = 0; j < m; ++j) qs[i * ld + j] = i == j ? 1.0 : 0.0;
+    // (no barrier: every lane touches its own row only)
+    if (i < m) {
+        double carry = 0.0;
+        int cq = -1;  // column whose current value is `carry` (-1: none)
+        for (int r = 0; r < nrot; ++r) {
+            const QRot g = rots[r];
+            const int p = g.p, q = p + 1;
+            if (i >= g.iend) {  // below the band: the host leaves this row alone
+                if (cq >= 0) qs[i * ld + cq] = carry;
+                cq = -1;
+                continue;
+            }
+            double a;
+            if (cq == p) a = carry;
+            else {
+                if (cq >= 0) qs[i * ld + cq] = carry;
+                a = qs[i * ld + p];
+            }
+            const double b = qs[i * ld + q];
+            const double t1 = g.c * a, t2 = g.s * b;
+            const double t3 = -g.s * a, t4 = g.c * b;
+            qs[i * ld + p] = t1 + t2;
+            carry = t3 + t4;
+            cq = q;
+        }
+        if (cq >= 0) qs[i * ld + cq] = carry;
+        for (int j = 0; j < kk; ++j) Qout[size_t(j) * m + i] = qs[i * ld + j];
+    }
+}
+
+void apply_rots(hipStream_t s, int m, const QRot* rots, int nrot, int kk, double* Qout) {
+    hipLaunchKernelGGL(k_apply_rots, dim3(1), dim3(MAX_NCV), size_t(MAX_NCV) * size_t(m | 1) * 8, s, m, rots, nrot, kk,
+                       Qout);
 }
 
 // Lanczos start vector: x[r] = st_{row0+r+1} / (2^31 - 1) - 0.5 for the

@@ -295,12 +295,15 @@ def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
 
 
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
-def test_lanczos_three_term_fused_bit_identical(ek, tmp_path, which):
-    """The single-GPU step without the three-term launch (alpha reduced by the
-    SpMV's last block, f' formed inside the projection) gives the bits of the
-    step with it (EK_LANCZOS_TT=0): the same reductions in the same order.
-    syn0.25 goes through breakdowns (injected vectors, beta = 0), syn2 through
-    the column-panel SpMV."""
+@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_HOST_Q=1"])
+def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
+    """Two device-side restructurings give the bits of the forms they replace:
+    * the single-GPU step without the three-term launch (alpha reduced by the
+      SpMV's last block, f' formed inside the projection) vs EK_LANCZOS_TT=0;
+    * the implicit restart's Q accumulated on the device from the host's
+      rotation list (k_apply_rots) vs EK_HOST_Q=1 (accumulated on the host).
+    syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
+    syn2 through restarts whose residual collapses."""
     import subprocess
     import sys
     gen = {"ibm01": "ek.Hypergraph.read(circuit_path('ibm01'))", "syn0.25": "ek.Hypergraph.generate(0.25, 3)",
@@ -311,9 +314,10 @@ def test_lanczos_three_term_fused_bit_identical(ek, tmp_path, which):
         "np.save(sys.argv[1], np.concatenate([[lam, st['matvecs'], st['residual']], v]))"
     ) % (os.path.dirname(os.path.abspath(__file__)), gen)
     env = dict(os.environ)
-    a, b = str(tmp_path / "tt.npy"), str(tmp_path / "sep.npy")
+    a, b = str(tmp_path / "new.npy"), str(tmp_path / "old.npy")
     subprocess.run([sys.executable, "-c", code, a], check=True, timeout=180, env=env)
-    env["EK_LANCZOS_TT"] = "0"
+    k, v = switch.split("=")
+    env[k] = v
     subprocess.run([sys.executable, "-c", code, b], check=True, timeout=180, env=env)
     x, y = np.load(a), np.load(b)
     assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
