@@ -1322,7 +1322,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     std::vector<double> d(size_t(m), 0.0), e(size_t(m), 0.0), theta(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
     std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
     std::vector<ek::QRot> rots;
-    static const bool host_q = std::getenv("EK_HOST_Q") != nullptr;
+    static const bool host_q = std::getenv("EK_DEVICE_Q") == nullptr;
     int k = 0, restarts = 0, nconv = 0, injected = 0;
     double fn2_k = 1.0;  // ||f_k||^2 entering a cycle (after an implicit restart: the restart's residual)
     bool converged = false;
@@ -1482,10 +1482,13 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         double sigma = 0.0;               // Q(m-1, knew-1)
         const double* sigma_dev = nullptr;  // ... or where the device left it
         if (!host_q) {
-            // the shifts' rotations recorded on the host (O(m) each: the
-            // tridiagonal only), Q accumulated from them on the device
-            // (k_apply_rots, the host's operations: the same bits), which
-            // took ~0.2 ms of host time per restart with the GPU idle
+            // EK_DEVICE_Q=1 (A/B): the shifts' rotations recorded on the host
+            // (O(m) each: the tridiagonal only), Q accumulated from them on
+            // the device (k_apply_rots, the host's operations: the same
+            // bits).  One workgroup walking ~9k dependent rotations is
+            // latency-bound: 1.36 ms per restart against ~0.02 ms of extra
+            // host time for accumulating Q beside the shifts, so the host
+            // form is the default
             rots.clear();
             for (int i = knew; i < m; ++i)  // Q starts as the identity: lower bandwidth i - knew
                 ek::tridiag_qr_shift_rots(m, dd.data(), ee.data(), theta[size_t(i)], i - knew, rots);
@@ -1495,7 +1498,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             if (rb) HIPCHK(hipMemcpyAsync(c->rotd.p, c->rot_pin, rb, hipMemcpyHostToDevice, s));
             ek::dev::apply_rots(s, m, c->rotd.as<ek::QRot>(), int(rots.size()), knew + 1, c->Qd.as<double>());
             sigma_dev = c->Qd.as<double>() + size_t(knew - 1) * m + size_t(m - 1);
-        } else {  // EK_HOST_Q=1: accumulated on the host (A/B)
+        } else {  // default: Q accumulated on the host beside the shifts
             double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
             std::fill(Q, Q + size_t(m) * size_t(m), 0.0);
             for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;

@@ -541,6 +541,31 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     for (;; ++it) {
         stamp(-1);
         if constexpr (PROF) w_top = __builtin_amdgcn_s_memtime();
+        if constexpr (EK_KL_PREFETCH) {
+            if (wv == W_PF) {
+                // P. touch the provisional pair's rows (one lane per row line:
+                // lanes 0-31 node1's, 32-63 node2's; clamped addresses): the
+                // W wave's weight lookup and the gain waves' segment and
+                // descriptor loads after the selection then hit L2 instead
+                // of the MALL
+                const int rp = __builtin_amdgcn_readlane(pf_inf.y, 0), ln = __builtin_amdgcn_readlane(pf_inf.z, 0);
+                const int rq = __builtin_amdgcn_readlane(pf_inf.y, 32), lq = __builtin_amdgcn_readlane(pf_inf.z, 32);
+                const int r0 = half ? rq : rp, l0 = half ? lq : ln;
+                if (l0 > 0) {
+                    const int last = r0 + l0 - 1;
+                    const int rs = min(r0 + hl, last);
+                    if constexpr (SEGC) {
+                        pf_seg = *reinterpret_cast<const int4*>(d.segc + size_t(rs) * KL_SEGC_PIECES);
+                    } else if (d.seg) {
+                        pf_seg = *reinterpret_cast<const int4*>(d.seg + size_t(rs) * KL_SEG_LANES);
+                        pf_seg2 = *reinterpret_cast<const int4*>(d.seg + size_t(rs) * KL_SEG_LANES + KL_SEG_LANES / 2);
+                    }
+                    pf_aux = *reinterpret_cast<const int4*>(d.aux + min(r0 + 8 * hl, last));
+                    pf_col = d.col[min(r0 + 32 * hl, last)];
+                    pf_w = d.w[min(r0 + 32 * hl, last)];
+                }
+            }
+        }
         // S. selection (cKL.cpp:341-355): lanes 0-31 reduce remain[0]'s keys,
         // 32-63 remain[1]'s; identical in every wave
         u64 k = 0ull;
@@ -941,9 +966,10 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             if (wv == W_PF) {
                 // P. provisional next pair (a prefetch hint, never a result):
                 // per list the best shadow key outside node1's / node2's chunk
-                // against that chunk's early rescan; its rows are touched
-                // before barrier 2 (the loads are consumed a swap later, so
-                // nothing waits for them at the barrier)
+                // against that chunk's early rescan.  Its descriptor is read
+                // now and used after barrier 2 (the bitmap flip runs in another
+                // wave: the wait the compiler puts ahead of its LDS reads would
+                // hold this one at barrier 2 for the load)
                 const u64* ckn = half ? ckn1 : ckn0;
                 const int nck = half ? d.nck1 : d.nck0, cS = half ? cB : cA;
                 u64 k = 0ull;
@@ -963,54 +989,9 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     k = v > k ? v : k;
                 }
                 k = half_max_u64(k);
-                // its row descriptor from LDS (a global load here would have to
-                // return before barrier 2): an early-rescan part's winner, a row
-                // whose key rose this swap (the item list), else the chunk's
-                // winner as kept.  A hint only: a stale pick just mispredicts.
-                const u64 hmask = half ? 0xffffffff00000000ull : 0x00000000ffffffffull;
-                int4 inf = make_int4(0, 0, 0, 0);
-                bool got = false;
-#pragma unroll
-                for (int q = 0; q < E_PARTS; ++q) {
-                    const bool e = !got && er_key[half * E_PARTS + q] == k;
-                    if (e) inf = *reinterpret_cast<const int4*>(er_info + half * E_PARTS + q);
-                    got |= e;
-                }
-                int4 cand = make_int4(0, 0, 0, 0);
-                bool mine = false;
-                for (int i = hl; i < tot && i < KL_ITEM_CAP; i += 32) {
-                    if (it_key[i] == k && it_cs[i] != -1) {
-                        cand = *reinterpret_cast<const int4*>(it_info + i);
-                        mine = true;
-                    }
-                }
-                const u64 mb = __ballot(mine) & hmask;
-                const int src = mb ? __ffsll((long long)mb) - 1 : lane;
-                const int4 ic = make_int4(__shfl(cand.x, src, 64), __shfl(cand.y, src, 64), __shfl(cand.z, src, 64),
-                                          __shfl(cand.w, src, 64));
-                if (!got && mb) inf = ic;
-                got |= mb != 0ull;
-                if (!got && k != 0ull)
-                    inf = *reinterpret_cast<const int4*>((half ? ci1 : ci0) + int(~uint32_t(k & 0xffffffffull)) / KL_CHUNK);
-                pf_inf = k != 0ull ? inf : make_int4(0, 0, 0, 0);
-                // touch its rows now, before barrier 2 (one lane per row line:
-                // lanes 0-31 list 0's, 32-63 list 1's; clamped addresses): the W
-                // wave's weight lookup and the gain waves' segment and
-                // descriptor loads after the next selection then hit L2
-                const int r0 = pf_inf.y, l0 = pf_inf.z;
-                if (l0 > 0) {
-                    const int last = r0 + l0 - 1;
-                    const int rs = min(r0 + hl, last);
-                    if constexpr (SEGC) {
-                        pf_seg = *reinterpret_cast<const int4*>(d.segc + size_t(rs) * KL_SEGC_PIECES);
-                    } else if (d.seg) {
-                        pf_seg = *reinterpret_cast<const int4*>(d.seg + size_t(rs) * KL_SEG_LANES);
-                        pf_seg2 = *reinterpret_cast<const int4*>(d.seg + size_t(rs) * KL_SEG_LANES + KL_SEG_LANES / 2);
-                    }
-                    pf_aux = *reinterpret_cast<const int4*>(d.aux + min(r0 + 8 * hl, last));
-                    pf_col = d.col[min(r0 + 32 * hl, last)];
-                    pf_w = d.w[min(r0 + 32 * hl, last)];
-                }
+                pf_inf = make_int4(0, 0, 0, 0);
+                if (k != 0ull && hl == 0)
+                    pf_inf = *reinterpret_cast<const int4*>((half ? d.pinfo1 : d.pinfo0) + int(~uint32_t(k & 0xffffffffull)));
             }
         }
         // G2b. publish merged keys of the other untagged chunks (every item of

@@ -295,13 +295,13 @@ def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
 
 
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
-@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_HOST_Q=1"])
+@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_DEVICE_Q=1"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Two device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
       SpMV's last block, f' formed inside the projection) vs EK_LANCZOS_TT=0;
     * the implicit restart's Q accumulated on the device from the host's
-      rotation list (k_apply_rots) vs EK_HOST_Q=1 (accumulated on the host).
+      rotation list (EK_DEVICE_Q=1, k_apply_rots) vs on the host (default).
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses."""
     import subprocess
