@@ -13,6 +13,10 @@
 
 #include "ek_internal.hpp"
 
+#ifndef EK_UPD_RED_MAX_NRB
+#define EK_UPD_RED_MAX_NRB 256  // row blocks up to which the update workgroups sum the partials themselves
+#endif
+
 #define HIPCHK(call)                                                                                 \
     do {                                                                                             \
         const hipError_t e_ = (call);                                                                \
@@ -1113,6 +1117,16 @@ struct Lanczos {
     // column tile re-reads w, v_i and v_{i-1}.  Step i > seg0 finalizes step
     // i - 1 in its SpMV, also across chunks; the last step of the cycle is
     // finalized by its own launch.
+    // Who sums the projection partials (nrb row blocks per column): every
+    // update workgroup itself (k_update<true>: no launch, but each of the
+    // ldv/512 workgroups reads all tot x nrb partials, quadratic in n) or one
+    // k_reduce_cols launch ahead of k_update<false> (same col_sum2 order, the
+    // same bits).  EK_UPD_RED=0/1 forces either (A/B).
+    static bool upd_reduces(int nrb) {
+        const char* e = std::getenv("EK_UPD_RED");
+        if (e && e[0]) return e[0] != '0';
+        return nrb <= EK_UPD_RED_MAX_NRB;
+    }
     void factorize_fused(int k, int kend) {
         // EK_LANCZOS_TT=0: the separate three-term launch (A/B; the same bits)
         static const bool tt_fused = [] {
@@ -1122,6 +1136,7 @@ struct Lanczos {
         double* fn2 = c->fn2.as<double>();
         double* a3 = c->scal.as<double>() + 2;
         const double* bov = c->bov.as<double>();
+        const bool upd_red = upd_reduces(nrb);
         for (int i = k; i < kend; ++i) {
             ek::dev::StepFin fin;
             if (i > seg0) {
@@ -1152,8 +1167,14 @@ struct Lanczos {
                                     i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>());
                 ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
             }
-            ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
-                              c->f.as<double>(), c->f.as<double>(), c->npart.as<double>());
+            if (upd_red) {
+                ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
+                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>());
+            } else {
+                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0, c->h2.as<double>());
+                ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
+                                c->f.as<double>(), c->npart.as<double>());
+            }
         }
         if (kend == m)
             ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + m, nullptr, c->h2.as<double>(), m - 1,

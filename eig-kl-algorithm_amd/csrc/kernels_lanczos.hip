@@ -306,18 +306,54 @@ __device__ __forceinline__ void col_sum2(const double* __restrict__ pa, const do
     *sb = b;
 }
 
-// h[j] = sum_b part[j*nrb + b] for j < ncols (col_sum2 order): 64 columns
-// per workgroup, 8 lanes each, two columns per lane group.
+// h[j] = sum_b part[j*nrb + b] for j < ncols, in col_sum2's order (lane l of
+// 8 sums blocks l, l+8, ... in turn, then the xor tree: the same bits as the
+// update's in-kernel sums).  The partials are staged in LDS by the whole
+// workgroup first, every load in flight at once, and the 8-lane chains then
+// run from LDS: with the chains reading memory themselves (8 lanes per column,
+// 32 loads in flight each) a column of 1,972 row blocks (10x) took 8 dependent
+// memory trips, 34.8 us per launch.  RC_COLS columns per workgroup; row-block
+// chunks of RC_CHUNK (chunk starts are multiples of 8: the chains carry on).
+constexpr int RC_COLS = 2, RC_CHUNK = 2048, RC_LD = RC_CHUNK + 8;  // +8: the two columns' chains on disjoint banks
 __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ part, int nrb, int ncols,
                                                      double* __restrict__ h) {
-    const int g = int(threadIdx.x) / CS_LANES, l = int(threadIdx.x) % CS_LANES;
-    const int ja = blockIdx.x * 64 + g, jb = ja + 32;
-    double sa, sb;
-    col_sum2(part + size_t(min(ja, ncols - 1)) * nrb, part + size_t(min(jb, ncols - 1)) * nrb, nrb, l, &sa, &sb);
-    if (l == 0) {
-        if (ja < ncols) h[ja] = sa;
-        if (jb < ncols) h[jb] = sb;
+    __shared__ double st[RC_COLS * RC_LD];
+    constexpr int PT = RC_CHUNK / 256;
+    const int t = int(threadIdx.x), j0 = int(blockIdx.x) * RC_COLS;
+    const int g = t / CS_LANES, l = t % CS_LANES;
+    double a = 0.0;
+    for (int c0 = 0; c0 < nrb; c0 += RC_CHUNK) {
+        const int cn = min(RC_CHUNK, nrb - c0);
+        double v[RC_COLS][PT];
+#pragma unroll
+        for (int q = 0; q < RC_COLS; ++q) {
+            const double* src = part + size_t(min(j0 + q, ncols - 1)) * nrb + c0;
+#pragma unroll
+            for (int u = 0; u < PT; ++u) v[q][u] = src[min(t + 256 * u, cn - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < RC_COLS; ++q)
+#pragma unroll
+            for (int u = 0; u < PT; ++u)
+                if (t + 256 * u < cn) st[q * RC_LD + t + 256 * u] = v[q][u];
+        __syncthreads();
+        if (g < RC_COLS) {
+            const double* col = st + g * RC_LD;
+            int i = l;
+            for (; i + 3 * CS_LANES < cn; i += 4 * CS_LANES) {  // four reads in flight, adds in order
+                const double x0 = col[i], x1 = col[i + CS_LANES], x2 = col[i + 2 * CS_LANES], x3 = col[i + 3 * CS_LANES];
+                a += x0;
+                a += x1;
+                a += x2;
+                a += x3;
+            }
+            for (; i < cn; i += CS_LANES) a += col[i];
+        }
+        __syncthreads();
     }
+#pragma unroll
+    for (int o = 1; o < CS_LANES; o <<= 1) a += __shfl_xor(a, o, 64);
+    if (g < RC_COLS && l == 0 && j0 + g < ncols) h[j0 + g] = a;
 }
 
 // dst = src - V[:, :ncols] h - u0 h[ncols]; 256 threads x 2 rows (double2).
@@ -579,18 +615,28 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
     }
 }
 
-// out[:, j] = sum_{i<m} V[:, i] Q[i, j], j < kk; grid (ldv/512, ceil(kk/8)).
+// out[:, j] = sum_{i<m} V[:, i] Q[i, j], j < kk; 1-D grid of (ldv/512) row
+// blocks x ceil(kk/8) column groups.  Every column group of a row block reads
+// the same m x 512 tile of V: with the blocks dealt round-robin over the 8
+// XCDs, the (row block, column group) map gives each XCD a contiguous run of
+// row blocks with all their column groups (k_gemvt's remap), so the tile is
+// fetched from memory once and re-read from that XCD's L2.  (A 2-D grid ran
+// every row block of column group 0 first: at 10x, V = 1.6 GB, the tile came
+// from HBM once per column group, 1.34 ms per restart.)
 __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restrict__ V, int m,
                                                  const double* __restrict__ Q, int kk, double* __restrict__ out) {
     constexpr int TJ = 8;
     __shared__ double qs[MAX_NCV][TJ];
-    const int j0 = blockIdx.y * TJ;
+    const int ncg = (kk + TJ - 1) / TJ;
+    const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q8 = nwg / 8, rr = nwg % 8;
+    const int vb = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
+    const int rbk = vb / ncg, j0 = (vb % ncg) * TJ;
     for (int i = threadIdx.x; i < m * TJ; i += 256) {
         const int row = i / TJ, jj = i % TJ;
         qs[row][jj] = (j0 + jj < kk) ? Q[size_t(j0 + jj) * m + row] : 0.0;
     }
     __syncthreads();
-    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    const size_t r = (size_t(rbk) * 256 + threadIdx.x) * 2;
     double2 acc[TJ];
 #pragma unroll
     for (int jj = 0; jj < TJ; ++jj) acc[jj] = make_double2(0.0, 0.0);
@@ -686,7 +732,8 @@ void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, d
 
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h) {
     if (ncols_total <= 0) return;
-    hipLaunchKernelGGL(k_reduce_cols, dim3((ncols_total + 63) / 64), dim3(256), 0, s, part, nrb, ncols_total, h);
+    hipLaunchKernelGGL(k_reduce_cols, dim3((ncols_total + RC_COLS - 1) / RC_COLS), dim3(256), 0, s, part, nrb,
+                       ncols_total, h);
 }
 
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
@@ -757,7 +804,7 @@ void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long 
 }
 
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out) {
-    hipLaunchKernelGGL(k_gemm_vq, dim3(ldv / UPD_ROWS, (kk + 7) / 8), dim3(256), 0, s, ldv, V, m, Q, kk, out);
+    hipLaunchKernelGGL(k_gemm_vq, dim3((ldv / UPD_ROWS) * ((kk + 7) / 8)), dim3(256), 0, s, ldv, V, m, Q, kk, out);
 }
 
 void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart,

@@ -105,8 +105,19 @@ __device__ __forceinline__ void alpha_handoff(const double* apart, double* alpha
     if (threadIdx.x == 0) *s_last = alpha_last_block(ctr) ? 1 : 0;
     __syncthreads();
     if (!*s_last) return;
+    // every partial's load in flight at once (16 per thread per trip, clamped
+    // index, 0.0 added past the end: s + 0.0 == s as s never becomes -0): one
+    // memory round trip instead of one per partial the thread sums
+    constexpr int AB = 16;
+    const int nb = int(gridDim.x);
     double s = 0.0;
-    for (int i = int(threadIdx.x); i < int(gridDim.x); i += SPMV_THREADS) s += load_sc1(apart + i);
+    for (int i0 = int(threadIdx.x); i0 < nb; i0 += AB * SPMV_THREADS) {
+        double v[AB];
+#pragma unroll
+        for (int u = 0; u < AB; ++u) v[u] = load_sc1(apart + min(i0 + u * SPMV_THREADS, nb - 1));
+#pragma unroll
+        for (int u = 0; u < AB; ++u) s += i0 + u * SPMV_THREADS < nb ? v[u] : 0.0;
+    }
     s = block_sum_all(s, wsum);
     if (threadIdx.x < ALPHA_SUB + 1) ctr[threadIdx.x * 64] = 0u;  // re-armed for the next launch
     if (threadIdx.x == 0) *alpha_out = s;

@@ -1,35 +1,37 @@
-"""Lab (not shipped): A/B of Lanczos kernel builds.  Runs the GPU Lanczos
-solve on the 1x seed-1 synthetic (and its largest connected component) a few
-times with the library named by EK_LIB_PATH (default: the in-tree build) and
-prints the device time per solve, the matvec count and a hash of the result
-bits, so builds that must be bit-identical can be compared run to run.
-Usage: EK_LIB_PATH=... python tools/lanczos_ab.py [reps] [check_every]"""
-import hashlib
+#!/usr/bin/env python3
+"""Lab (not shipped): resident Lanczos solves on the synthetic under
+environment variants, one line per (size, variant): solve time, matvecs and
+the first bits of lambda (variants that claim the same bits must agree).
+usage: python tools/lanczos_ab.py MULT[,MULT..] VAR=VAL[,VAR=VAL..] [...]
+       (each further argument is one variant; "-" = no overrides)"""
 import importlib.util
 import os
+import struct
 import sys
-import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
+spec = importlib.util.spec_from_file_location("ek", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
 ek = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(ek)
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-check_every = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-print(f"lib {ek.LIB_PATH}", flush=True)
-h1 = ek.Hypergraph.generate(1.0, 1)
-hl, _ = h1.largest_component()
+mults = [float(m) for m in sys.argv[1].split(",")]
+variants = sys.argv[2:] or ["-"]
 ctx = ek.Context(0)
-for name, h in (("syn1", h1), ("syn1_lcc", hl)):
-    L = h.laplacian()
-    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
-    ms = []
-    for i in range(reps):
-        t0 = time.time()
-        lam, v, st = ctx.lanczos_fiedler(check_every=check_every)
-        ms.append((time.time() - t0) * 1e3)
-    dig = hashlib.md5(v.tobytes()).hexdigest()[:12]
-    print(f"{name}: wall ms {' '.join(f'{x:.2f}' for x in ms)}; device {st['total_ms']:.2f} ms, "
-          f"{st['matvecs']} matvecs, {st['restarts']} restarts, us/step {1e3 * min(ms[1:]) / st['matvecs']:.1f}, "
-          f"lambda {lam.hex()}, v md5 {dig}", flush=True)
+for mult in mults:
+    h = ek.Hypergraph.generate(mult, {1.0: 1, 2.0: 2, 10.0: 10}.get(mult, 3))
+    ctx.spmv_setup_pins(h)
+    for rep in range(int(os.environ.get("REPS", "2"))):
+        for var in variants:
+            env = dict(kv.split("=", 1) for kv in var.split(",")) if var != "-" else {}
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            ctx.lanczos_fiedler()  # warm
+            lam, v, st = ctx.lanczos_fiedler()
+            for k, o in saved.items():
+                if o is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = o
+            bits = struct.pack("<d", lam).hex()
+            print(f"{mult:5.1f}x {var:28s} Lanczos {st['total_ms']:9.3f} ms  {st['matvecs']} matvecs  lambda {lam:.6e} "
+                  f"[{bits}] v[0:2] {v[0]:.17g} {v[1]:.17g}", flush=True)
 ctx.close()
