@@ -130,6 +130,8 @@ struct ek_ctx {
     int64_t mat_bytes = 0;  // bytes of the matrix arrays one SpMV reads, as stored
     // Lanczos workspace
     DBuf V, Vn, f, w, xfull, part, h1, h2, alpha, offd, fn2, npart, apart, Qd, scal, bov;
+    DBuf V32, Vn32;  // the basis's fp32 shadow (ek_lanczos_opts::basis32) and its restart buffer
+    DBuf fbk;        // launches whose fp32-shadow update fell back to V (a device counter)
     DBuf actr;  // the SpMV's last-block counter (alpha hand-off), zero between launches
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
@@ -966,6 +968,8 @@ void ek_lanczos_default_opts(ek_lanczos_opts* o) {
     o->time_spmv = 0;
     o->reorth = 1;
     o->check_every = 8;
+    o->basis32 = 1;
+    o->alpha_last = 0;
 }
 
 }  // extern "C"
@@ -1024,6 +1028,13 @@ struct Lanczos {
     // H(i,i) / H(i-1,i) take the projections as corrections (Spectra's
     // H += V^T f after its re-orthogonalisation).
     int reorth = 1;
+    // the update reads the fp32 shadow V32 (single-context fused step; k_update B32)
+    bool b32 = false;
+    // alpha reduced by the SpMV's last workgroup (else by every projection workgroup)
+    bool alpha_last = true;
+    int u32_steps = 0;
+    float* V32() { return b32 ? c->V32.as<float>() : nullptr; }
+    float* col32(int j) { return b32 ? c->V32.as<float>() + size_t(j) * ldv : nullptr; }
     int seg0 = 0;  // first step of the current run of steps (cycle start or injected vector)
     // steps [k, kend) of a run that started at seg0 (the driver enqueues a
     // cycle in chunks to check convergence between them)
@@ -1156,25 +1167,30 @@ struct Lanczos {
             ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
                           c->apart.as<double>(), i > seg0 ? &fin : nullptr,
                           timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr,
-                          tt_fused ? a3 : nullptr, c->actr.as<unsigned>());
+                          tt_fused && alpha_last ? a3 : nullptr, c->actr.as<unsigned>());
             ++matvecs;
             const int nc = i + 1;
             if (tt_fused) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
-                                  i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>());
+                                  i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
+                                  col32(i), alpha_last ? nullptr : c->apart.as<double>(), c->nrb_spmv);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
-                                    i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>());
-                ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>());
+                                    i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), col32(i));
+                ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>(),
+                               b32 ? 1 : 0);
             }
+            // (b32: ||f'||^2 rides along as one more column of the partials)
+            unsigned* fb = b32 ? c->fbk.as<unsigned>() : nullptr;
             if (upd_red) {
                 ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
-                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>());
+                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb);
             } else {
-                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0, c->h2.as<double>());
+                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0 + (b32 ? 1 : 0), c->h2.as<double>());
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>());
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb);
             }
+            if (b32) ++u32_steps;
         }
         if (kend == m)
             ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + m, nullptr, c->h2.as<double>(), m - 1,
@@ -1274,6 +1290,22 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);
     c->Vn.ensure(ldv * size_t(m + 1) * 8);
+    // the fp32 shadow: single-context three-term steps (the sharded and CGS2
+    // steps project w itself, where h is not small)
+    // (EK_BASIS32=0|1 / EK_ALPHA_LAST=0|1 override the options: A/B runs)
+    auto env_or = [](const char* k, bool dflt) {
+        const char* e = std::getenv(k);
+        return e && e[0] ? e[0] != '0' : dflt;
+    };
+    L.b32 = env_or("EK_BASIS32", o.basis32 != 0) && c->nranks == 1 && L.reorth == 1 &&
+            std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
+    L.alpha_last = env_or("EK_ALPHA_LAST", o.alpha_last != 0);
+    if (L.b32) {
+        c->V32.ensure(ldv * size_t(m + 1) * 4);
+        c->Vn32.ensure(ldv * size_t(m + 1) * 4);
+        c->fbk.ensure(64);
+        HIPCHK(hipMemsetAsync(c->fbk.p, 0, 4, c->stream));
+    }
     // f: + 64 (the sharded step's all-gather slot carries the rank's ||f||^2 at [ldv])
     if (c->nranks > 1 && c->slot != int64_t(ldv) + 64) ek::fail(EK_ESTATE, "shard slot %lld != ldv + 64", (long long)c->slot);
     c->f.ensure((ldv + 64) * 8);
@@ -1530,13 +1562,18 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         }
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
         const double hk = ee[size_t(knew - 1)];  // H(knew, knew-1)
-        ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>());
+        ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>(),
+                         L.b32 ? c->Vn32.as<float>() : nullptr);
         ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
                             c->npart.as<double>(), sigma_dev);
         L.reduce_scalar(c->fn2.as<double>() + knew);
         HIPCHK(hipMemcpyAsync(&fn2_k, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
         std::swap(c->V.p, c->Vn.p);
         std::swap(c->V.bytes, c->Vn.bytes);
+        if (L.b32) {
+            std::swap(c->V32.p, c->Vn32.p);
+            std::swap(c->V32.bytes, c->Vn32.bytes);
+        }
         HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read
         for (int i = 0; i < knew; ++i) d[size_t(i)] = dd[size_t(i)];
         for (int i = 0; i + 1 < knew; ++i) e[size_t(i)] = ee[size_t(i)];
@@ -1626,6 +1663,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         stats->comm_ms = c->comm_ms;
         stats->allgathers = int32_t(c->n_ag);
         stats->allreduces = int32_t(c->n_ar);
+        stats->update32_steps = L.u32_steps;
+        stats->update32_fallbacks = 0;
+        if (L.b32) {
+            unsigned fbn = 0;
+            HIPCHK(hipMemcpyAsync(&fbn, c->fbk.p, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            stats->update32_fallbacks = int32_t(fbn);
+        }
     }
     return EK_OK;
     EK_CATCH

@@ -285,8 +285,10 @@ constexpr int UPD_ROWS = 512;  // rows per update block
 constexpr int MAX_NCV = 128;
 // part[j*nrb + b] = sum_{rows of block b} V[row, j] * w[row]; column `ncols` is
 // the implicit deflation vector u0 (value u0val on rows < nreal) if has_u0.
+// nrm: part column ncols + has_u0 also gets ||w||^2 over each row block
+// (the fp32-shadow update's accuracy test, k_update B32)
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val,
-           int nreal, const double* w, double* part);
+           int nreal, const double* w, double* part, int nrm = 0);
 // the sharded step (ctx.cpp factorize_mr): part for three vectors w, va, vb at
 // once, part[(k*tot + j)*nrb + b], tot = ncols + has_u0
 void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
@@ -300,21 +302,31 @@ void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, d
                const double* hall, const double* w, const double* vi, const double* vim1, const double* fn2_i,
                const double* bov_i, double* dst, double* npart, double* alpha, double* offd);
 // gemvt of the three-term residual f' = w - *alpha vi - beta_i vim1 (vim1 may
-// be null; beta_i as three_term), formed per row; f' is also stored to fp
+// be null; beta_i as three_term), formed per row; f' is also stored to fp.
+// v32col != null: the fp32 basis shadow's column i = fl32(vi) is written and
+// ||f'||^2 partials go to part column ncols + has_u0 (as gemvt's nrm).
+// apart != null: alpha is not read from *alpha but reduced by every workgroup
+// from the SpMV's nparts partials (k_three_term's order), and *alpha written
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
-              const double* bov_i, double* fp, double* part);
+              const double* bov_i, double* fp, double* part, float* v32col = nullptr, const double* apart = nullptr,
+              int nparts = 0);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 
 // Fused single-GPU step (reorth 1):
 // update_r: h = column sums of part (every block, fixed order; block 0 writes
 // h_out), then dst = src - V h - u0 h[ncols] with ||dst||^2 partials -> npart
+// V32 != null: the basis is read from its fp32 shadow when sum|h| <= 2^-29
+// ||src|| (exact to fp64 rounding; ||src||^2 is the partials' / h's entry
+// after u0's), else from V (*fb += 1 when fb != null)
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
-              const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart);
+              const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart,
+              const float* V32 = nullptr, unsigned* fb = nullptr);
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
-            const double* h, const double* src, double* dst, double* npart);
+            const double* h, const double* src, double* dst, double* npart, const float* V32 = nullptr,
+            unsigned* fb = nullptr);
 // fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
 // alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
 // alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]
@@ -325,9 +337,11 @@ void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, 
 // *bov_i is not NaN (0 after an injected restart vector); alpha = sum(apart[0:nparts]) when
 // nparts > 0 (written to *alpha_io), else read from *alpha_io
 void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,
-                const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp);
-// out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device)
-void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out);
+                const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp,
+                float* v32col = nullptr);
+// out[:, j] = V[:, :m] Q[:, j] for j < kk (Q col-major m x kk, device); out32: also fl32 of it
+void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out,
+             float* out32 = nullptr);
 void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long nrows, unsigned long long st0);
 // zero the padded rows [nreal, ldv) of the first ncols columns of V
 void zero_pad_rows(hipStream_t s, double* V, int ldv, int nreal, int ncols);

@@ -77,14 +77,23 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 // and the column-group-0 block of each row block stores it to fp for the
 // update: the three-term launch and its per-block re-reduction of the alpha
 // partials are gone, the bits are the same.
+// B32 (the fp32 basis shadow, k_update<_, true>): the column-group-0 block of
+// each row block also writes ||rhs||^2 over its rows to part column
+// ncols + has_u0 (the update's accuracy test reads the sum), and with TT
+// the fp32 copy of v_i to v32col (vi rows are loaded here anyway).
 template <bool TT>
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part, const double* __restrict__ alpha,
                                                const double* __restrict__ vi, const double* __restrict__ vim1,
                                                const double* __restrict__ fn2_i, const double* __restrict__ bov_i,
-                                               double* __restrict__ fp) {
+                                               double* __restrict__ fp, int nrm, float* __restrict__ v32col,
+                                               const double* __restrict__ apart, int nparts,
+                                               double* __restrict__ alpha_pub) {
     __shared__ double red[4][GT_COLS];
+    __shared__ double nred[4];
+    __shared__ double lds4[4];
+    __shared__ double s_alpha;
     const int t = threadIdx.x;
     const int ncg = (ncols + has_u0 + GT_COLS - 1) / GT_COLS;
     const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
@@ -114,7 +123,20 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
             vs[k][jj] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
     }
     if constexpr (TT) {  // k_three_term's f' (same operations, same order)
-        const double a = *alpha;
+        // apart != null: alpha = sum of the SpMV's per-block partials, reduced
+        // by this workgroup in k_three_term's order (the same bits as the
+        // SpMV's last-block reduction), its loads behind the tile's; the
+        // first workgroup publishes it for the finalize
+        if (apart) {
+            double sa = strided_sum256(apart, nparts);
+            sa = block_sum256(sa, lds4);
+            if (t == 0) {
+                s_alpha = sa;
+                if (orig == 0) *alpha_pub = sa;
+            }
+            __syncthreads();
+        }
+        const double a = apart ? s_alpha : *alpha;
         const double b = vim1 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
 #pragma unroll
         for (int k = 0; k < KR; ++k) {
@@ -126,9 +148,19 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
                 y.y -= b * tu[k].y;
             }
             xs[k] = y;
-            if (j0 == 0)
-                *reinterpret_cast<double2*>(fp + size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t)) = y;
+            if (j0 == 0) {
+                const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+                *reinterpret_cast<double2*>(fp + r) = y;
+                if (v32col) *reinterpret_cast<float2*>(v32col + r) = make_float2(float(tv[k].x), float(tv[k].y));
+            }
         }
+    }
+    if (nrm && j0 == 0) {  // ||rhs||^2 over this row block: a fixed tree (the same in TT and plain forms)
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < KR; ++k) s += xs[k].x * xs[k].x + xs[k].y * xs[k].y;
+        s = wave_sum(s);
+        if ((t & 63) == 0) nred[t >> 6] = s;
     }
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -173,6 +205,8 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     __syncthreads();
     if (t < GT_COLS && j0 + t < ncols + has_u0)
         part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (nrm && j0 == 0 && t == 0)
+        part[size_t(ncols + has_u0) * nrb + rbk] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
 }
 
 // The sharded step's projection (ctx.cpp Lanczos::factorize_mr): the partial
@@ -360,19 +394,35 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
 // RED: h is first reduced from the projection partials (column j: two lanes
 // each summing every other block in order, then one add — the same in every
 // workgroup; workgroup 0 publishes h_out).
-template <bool RED>
+//
+// B32: the basis is read from its fp32 shadow V32 (half the bytes) when the
+// correction is small enough for that to be exact to fp64 rounding.  With
+// unit columns, |V - fl32(V)| <= 2^-24 |V| elementwise, so the shadow changes
+// V h by at most 2^-24 sum_j |h_j| in norm; the test sum_j |h_j| <= 2^-29
+// ||src|| bounds that by 2^-53 ||src||, below the rounding of the fp64
+// update itself.  In a reorthogonalised Lanczos step h is the loss of
+// orthogonality, O(eps ||w||), so the test holds by many orders of magnitude;
+// when it does not (an injected vector, a residual that cancelled to near
+// zero) every workgroup takes the same decision (the same h and norm, the
+// same sums) and runs the fp64 loop (*fb counts those launches).
+// ||src||^2 comes as one more column of the partials (k_gemvt's nrm) or h.
+template <bool RED, bool B32>
 __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restrict__ V, int ncols, int has_u0,
                                                 double u0val, int nreal, const double* __restrict__ h,
                                                 const double* __restrict__ src, double* __restrict__ dst,
                                                 double* __restrict__ npart, const double* __restrict__ part, int nrb,
-                                                double* __restrict__ h_out) {
+                                                double* __restrict__ h_out, const float* __restrict__ V32,
+                                                unsigned* __restrict__ fb) {
     constexpr int UB = EK_UPD_UB;
+    constexpr int UB32 = 2 * EK_UPD_UB;  // fp32 columns per batch: the same bytes in flight
+    constexpr int UBX = B32 ? UB32 : UB;
     // hc: the basis coefficients, zero past ncols (whole batches read it
-    // unconditionally); hu0: the deflation vector's
-    __shared__ double hc[MAX_NCV + 2 * UB];
-    __shared__ double hu0;
+    // unconditionally); hu0: the deflation vector's; snrm: ||src||^2 (B32)
+    __shared__ double hc[MAX_NCV + 2 * UBX];
+    __shared__ double hu0, snrm;
     __shared__ double lds4[4];
     const int tot = ncols + has_u0;
+    const int totr = tot + (B32 ? 1 : 0);  // values reduced / read: + ||src||^2
     // Basis columns in batches of UB, two batches in flight: batch b+1's
     // loads are issued before batch b is used, and batch 0's (with src)
     // before h is reduced, so the projection reduce and every batch overlap a
@@ -395,34 +445,7 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
 #pragma unroll
         for (int u = 0; u < UB; ++u) vb[u] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + u, jmax)) * ldv + r);
     };
-    double2 ba[UB], bb[UB];
     double2 x = *reinterpret_cast<const double2*>(src + r);
-    load_batch(ba, 0);
-    load_batch(bb, UB);
-    auto put = [&](int j, double v) {
-        if (j < ncols) hc[j] = v;
-        else hu0 = v;
-    };
-    if constexpr (RED) {
-        const int g = int(threadIdx.x) / CS_LANES, l = int(threadIdx.x) % CS_LANES;
-        for (int ja = g; ja < tot; ja += 64) {  // lane groups: uniform trip counts
-            const int jb = ja + 32;
-            double sa, sb;
-            col_sum2(part + size_t(ja) * nrb, part + size_t(min(jb, tot - 1)) * nrb, nrb, l, &sa, &sb);
-            if (l == 0) {
-                put(ja, sa);
-                if (blockIdx.x == 0) h_out[ja] = sa;
-                if (jb < tot) {
-                    put(jb, sb);
-                    if (blockIdx.x == 0) h_out[jb] = sb;
-                }
-            }
-        }
-    } else {
-        for (int j = threadIdx.x; j < tot; j += 256) put(j, h[j]);
-    }
-    for (int j = ncols + int(threadIdx.x); j < ncols + 2 * UB; j += 256) hc[j] = 0.0;
-    __syncthreads();
     auto consume = [&](const double2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
@@ -434,16 +457,94 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     // past the end: clamped re-reads of column jmax (cache hits), coefficient 0
     // (scheduling barriers keep each batch's loads ahead of the other's use:
     // left alone the scheduler sank them below it)
-    // (both first batches were issued before the coefficients were reduced)
-    for (int j0 = 0; j0 < ncols; j0 += 2 * UB) {
-        consume(ba, j0);
-        __builtin_amdgcn_sched_barrier(0);
-        load_batch(ba, j0 + 2 * UB);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(bb, j0 + UB);
-        __builtin_amdgcn_sched_barrier(0);
-        load_batch(bb, j0 + 3 * UB);
-        __builtin_amdgcn_sched_barrier(0);
+    auto run64 = [&](double2* ba, double2* bb) {
+        for (int j0 = 0; j0 < ncols; j0 += 2 * UB) {
+            consume(ba, j0);
+            __builtin_amdgcn_sched_barrier(0);
+            load_batch(ba, j0 + 2 * UB);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(bb, j0 + UB);
+            __builtin_amdgcn_sched_barrier(0);
+            load_batch(bb, j0 + 3 * UB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // the first two batches are issued before the coefficients are reduced
+    // (B32: the shadow's; the fp64 fallback issues its own afterwards)
+    double2 ba[UB], bb[UB];
+    float2 fa[UB32], fbb[UB32];
+    auto load32 = [&](float2* vb, int j0) {
+#pragma unroll
+        for (int u = 0; u < UB32; ++u)
+            vb[u] = *reinterpret_cast<const float2*>(V32 + size_t(min(j0 + u, jmax)) * ldv + r);
+    };
+    if constexpr (B32) {
+        load32(fa, 0);
+        load32(fbb, UB32);
+    } else {
+        load_batch(ba, 0);
+        load_batch(bb, UB);
+    }
+    auto put = [&](int j, double v) {
+        if (j < ncols) hc[j] = v;
+        else if (j < tot) hu0 = v;
+        else snrm = v;
+    };
+    if constexpr (RED) {
+        const int g = int(threadIdx.x) / CS_LANES, l = int(threadIdx.x) % CS_LANES;
+        for (int ja = g; ja < totr; ja += 64) {  // lane groups: uniform trip counts
+            const int jb = ja + 32;
+            double sa, sb;
+            col_sum2(part + size_t(ja) * nrb, part + size_t(min(jb, totr - 1)) * nrb, nrb, l, &sa, &sb);
+            if (l == 0) {
+                put(ja, sa);
+                if (blockIdx.x == 0) h_out[ja] = sa;
+                if (jb < totr) {
+                    put(jb, sb);
+                    if (blockIdx.x == 0) h_out[jb] = sb;
+                }
+            }
+        }
+    } else {
+        for (int j = threadIdx.x; j < totr; j += 256) put(j, h[j]);
+    }
+    for (int j = ncols + int(threadIdx.x); j < ncols + 2 * UBX; j += 256) hc[j] = 0.0;
+    __syncthreads();
+    if constexpr (B32) {
+        // sum |h_j| per wave, the same order in every wave and workgroup
+        // (MAX_NCV <= 128: two values a lane)
+        static_assert(MAX_NCV <= 128, "two coefficients per lane");
+        const int lane = int(threadIdx.x) & 63;
+        double a = (lane < ncols ? fabs(hc[lane]) : 0.0) + (lane + 64 < ncols ? fabs(hc[lane + 64]) : 0.0);
+        a = wave_sum(a);
+        const bool ok = a <= 0x1p-29 * sqrt(snrm);  // false for NaN
+        if (ok) {
+            auto consume32 = [&](const float2* vb, int j0) {
+#pragma unroll
+                for (int u = 0; u < UB32; ++u) {
+                    const double hj = hc[j0 + u];
+                    x.x -= double(vb[u].x) * hj;
+                    x.y -= double(vb[u].y) * hj;
+                }
+            };
+            for (int j0 = 0; j0 < ncols; j0 += 2 * UB32) {
+                consume32(fa, j0);
+                __builtin_amdgcn_sched_barrier(0);
+                load32(fa, j0 + 2 * UB32);
+                __builtin_amdgcn_sched_barrier(0);
+                consume32(fbb, j0 + UB32);
+                __builtin_amdgcn_sched_barrier(0);
+                load32(fbb, j0 + 3 * UB32);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+            if (fb && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(fb, 1u);
+            load_batch(ba, 0);
+            load_batch(bb, UB);
+            run64(ba, bb);
+        }
+    } else {
+        run64(ba, bb);
     }
     if (has_u0) {
         const double c = u0val * hu0;
@@ -572,7 +673,7 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
                                                     double* __restrict__ alpha_io, const double* __restrict__ w,
                                                     const double* __restrict__ vi, const double* __restrict__ vim1,
                                                     const double* __restrict__ fn2_i, const double* __restrict__ bov_i,
-                                                    double* __restrict__ fp) {
+                                                    double* __restrict__ fp, float* __restrict__ v32col) {
     __shared__ double lds4[4];
     __shared__ double s_alpha;
     // TT_ROWS rows per block (2 double2 per thread): fewer blocks re-reduce the
@@ -612,6 +713,7 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
             y.y -= b * u[k].y;
         }
         *reinterpret_cast<double2*>(fp + r) = y;
+        if (v32col) *reinterpret_cast<float2*>(v32col + r) = make_float2(float(v[k].x), float(v[k].y));
     }
 }
 
@@ -624,7 +726,8 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
 // every row block of column group 0 first: at 10x, V = 1.6 GB, the tile came
 // from HBM once per column group, 1.34 ms per restart.)
 __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restrict__ V, int m,
-                                                 const double* __restrict__ Q, int kk, double* __restrict__ out) {
+                                                 const double* __restrict__ Q, int kk, double* __restrict__ out,
+                                                 float* __restrict__ out32) {
     constexpr int TJ = 8;
     __shared__ double qs[MAX_NCV][TJ];
     const int ncg = (kk + TJ - 1) / TJ;
@@ -661,7 +764,12 @@ __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restri
     }
 #pragma unroll
     for (int jj = 0; jj < TJ; ++jj)
-        if (j0 + jj < kk) *reinterpret_cast<double2*>(out + size_t(j0 + jj) * ldv + r) = acc[jj];
+        if (j0 + jj < kk) {
+            *reinterpret_cast<double2*>(out + size_t(j0 + jj) * ldv + r) = acc[jj];
+            if (out32)
+                *reinterpret_cast<float2*>(out32 + size_t(j0 + jj) * ldv + r) =
+                    make_float2(float(acc[jj].x), float(acc[jj].y));
+        }
 }
 
 // f = f*sigma + x*hk, per-block sum of f^2
@@ -699,19 +807,21 @@ __global__ __launch_bounds__(256) void k_sub_mean(double* __restrict__ x, int nr
 }
 
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
-           const double* w, double* part) {
+           const double* w, double* part, int nrm) {
     const int cols = ncols + has_u0;
     if (cols <= 0) return;
     hipLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
-                       ncols, has_u0, u0val, nreal, w, part, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       ncols, has_u0, u0val, nreal, w, part, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm,
+                       nullptr, nullptr, 0, nullptr);
 }
 
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
-              const double* bov_i, double* fp, double* part) {
+              const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts) {
     const int cols = ncols + has_u0;
     hipLaunchKernelGGL(k_gemvt<true>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
-                       ncols, has_u0, u0val, nreal, w, part, alpha, vi, vim1, fn2_i, bov_i, fp);
+                       ncols, has_u0, u0val, nreal, w, part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp,
+                       v32col ? 1 : 0, v32col, apart, nparts, apart ? const_cast<double*>(alpha) : nullptr);
 }
 
 
@@ -737,15 +847,24 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
 }
 
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
-            const double* h, const double* src, double* dst, double* npart) {
-    hipLaunchKernelGGL(k_update<false>, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal, h,
-                       src, dst, npart, nullptr, 0, nullptr);
+            const double* h, const double* src, double* dst, double* npart, const float* V32, unsigned* fb) {
+    if (V32)
+        hipLaunchKernelGGL((k_update<false, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
+                           nreal, h, src, dst, npart, nullptr, 0, nullptr, V32, fb);
+    else
+        hipLaunchKernelGGL((k_update<false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
+                           nreal, h, src, dst, npart, nullptr, 0, nullptr, nullptr, nullptr);
 }
 
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
-              const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart) {
-    hipLaunchKernelGGL(k_update<true>, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal,
-                       nullptr, src, dst, npart, part, nrb, h_out);
+              const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart,
+              const float* V32, unsigned* fb) {
+    if (V32)
+        hipLaunchKernelGGL((k_update<true, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
+                           nreal, nullptr, src, dst, npart, part, nrb, h_out, V32, fb);
+    else
+        hipLaunchKernelGGL((k_update<true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
+                           nreal, nullptr, src, dst, npart, part, nrb, h_out, nullptr, nullptr);
 }
 
 void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1, const double* h2,
@@ -755,9 +874,10 @@ void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, 
 }
 
 void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,
-                const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp) {
+                const double* vi, const double* vim1, const double* fn2_i, const double* bov_i, double* fp,
+                float* v32col) {
     hipLaunchKernelGGL(k_three_term, dim3(ldv / TT_ROWS), dim3(256), 0, s, apart, nparts, alpha_io, w, vi, vim1, fn2_i,
-                       bov_i, fp);
+                       bov_i, fp, v32col);
 }
 
 // The breakdown restart vector (ctx.cpp inject): element g of the global
@@ -803,8 +923,9 @@ void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long 
     hipLaunchKernelGGL(k_inject, dim3((ldv + 255) / 256), dim3(256), 0, s, f, ldv, row0, nrows, st0);
 }
 
-void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out) {
-    hipLaunchKernelGGL(k_gemm_vq, dim3((ldv / UPD_ROWS) * ((kk + 7) / 8)), dim3(256), 0, s, ldv, V, m, Q, kk, out);
+void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out, float* out32) {
+    hipLaunchKernelGGL(k_gemm_vq, dim3((ldv / UPD_ROWS) * ((kk + 7) / 8)), dim3(256), 0, s, ldv, V, m, Q, kk, out,
+                       out32);
 }
 
 void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart,

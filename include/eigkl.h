@@ -205,6 +205,13 @@ typedef struct {
                             criterion on the projected matrix every this many steps
                             (and stop there) instead of at cycle ends only; 0: cycle
                             ends only (Spectra's schedule).  Default 8. */
+    int32_t basis32;     /* 1 (default): the reorthogonalisation's update f = f' - V h reads
+                            an fp32 shadow of the basis when sum|h| <= 2^-29 ||f'|| (its
+                            effect then stays below fp64 rounding), else V;
+                            0: always the fp64 basis.  Single-context steps only. */
+    int32_t alpha_last;  /* 0 (default): every projection workgroup re-reduces the SpMV's
+                            alpha = v_i . w partials; 1: the SpMV's last workgroup does
+                            (a serial tail on the SpMV; the same bits) */
 } ek_lanczos_opts;
 
 typedef struct {
@@ -218,6 +225,8 @@ typedef struct {
     double comm_ms;       /* time inside RCCL calls (host-observed, sharded) */
     int32_t allgathers;   /* collectives issued by this rank during the solve (sharded; */
     int32_t allreduces;   /* one of each per Lanczos step, plus restarts/injections/end) */
+    int32_t update32_steps;     /* steps whose update was enqueued with the fp32 shadow */
+    int32_t update32_fallbacks; /* ... of which took the fp64 basis (the accuracy test failed) */
 } ek_lanczos_stats;
 
 void ek_lanczos_default_opts(ek_lanczos_opts* o);

@@ -294,12 +294,49 @@ def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
         _fiedler_parity(name, lam_b, v_b, lam_ref, med_ref, bits_ref, v_ref, ek)
 
 
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
+@pytest.mark.parametrize("deflate", [True, False])
+def test_lanczos_basis32_update_golden(ek, ctx, name, deflate):
+    """The update f = f' - V h reading the basis's fp32 shadow (basis32, the
+    default) only where sum|h| <= 2^-29 ||f'||, so the shadow's rounding stays
+    below the fp64 update's own: held to the reference's Fiedler tolerances
+    like the fp64-basis run, and every regular step took the shadow."""
+    h = ek.Hypergraph.read(circuit_path(name))
+    L = h.laplacian()
+    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    lam_a, v_a, st_a = ctx.lanczos_fiedler(deflate=deflate, basis32=True)
+    lam_b, v_b, st_b = ctx.lanczos_fiedler(deflate=deflate, basis32=False)
+    assert st_a["converged"] and st_a["residual"] < 1e-9 and st_b["residual"] < 1e-9
+    assert st_a["update32_steps"] == st_a["matvecs"] and st_b["update32_steps"] == 0
+    assert st_a["update32_fallbacks"] == 0, st_a
+    lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
+    for lam, v in ((lam_a, v_a), (lam_b, v_b)):
+        _fiedler_parity(name, lam, v * np.sign(v @ v_ref), lam_ref, med_ref, bits_ref, v_ref, ek)
+    assert abs(lam_a - lam_b) <= 1e-11 and abs(st_a["matvecs"] - st_b["matvecs"]) <= 8 + 0.05 * st_b["matvecs"]
+
+
+@pytest.mark.parametrize("which", ["syn0.25", "syn2", "syn1"])
+def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
+    """Disconnected synthetics (injected vectors, collapsed restart residuals):
+    the shadow update converges to a null vector with the fp64 run's residual
+    bar, and the accuracy test never had to fall back on a regular step."""
+    mult, seed = {"syn0.25": (0.25, 3), "syn2": (2.0, 2), "syn1": (1.0, 1)}[which]
+    h = ek.Hypergraph.generate(mult, seed)
+    ctx.spmv_setup_pins(h)
+    lam, v, st = ctx.lanczos_fiedler()
+    assert st["converged"] and st["residual"] < 1e-8 and abs(lam) < 1e-8
+    assert np.all(np.isfinite(v)) and abs(np.linalg.norm(v) - 1) < 1e-10
+    assert st["update32_steps"] == st["matvecs"] and st["update32_fallbacks"] == 0, st
+
+
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
-@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_DEVICE_Q=1"])
+@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_DEVICE_Q=1", "EK_ALPHA_LAST=1"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
-    """Two device-side restructurings give the bits of the forms they replace:
+    """Device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
       SpMV's last block, f' formed inside the projection) vs EK_LANCZOS_TT=0;
+    * alpha re-reduced by every projection workgroup (the default) vs by
+      the SpMV's last block (EK_ALPHA_LAST=1);
     * the implicit restart's Q accumulated on the device from the host's
       rotation list (EK_DEVICE_Q=1, k_apply_rots) vs on the host (default).
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,

@@ -32,6 +32,8 @@ for mult in mults:
                 else:
                     os.environ[k] = o
             bits = struct.pack("<d", lam).hex()
-            print(f"{mult:5.1f}x {var:28s} Lanczos {st['total_ms']:9.3f} ms  {st['matvecs']} matvecs  lambda {lam:.6e} "
+            print(f"{mult:5.1f}x {var:28s} Lanczos {st['total_ms']:9.3f} ms  {st['matvecs']} matvecs "
+                  f"({1000 * st['total_ms'] / st['matvecs']:.2f} us/matvec, u32 {st.get('update32_steps')}/"
+                  f"{st.get('update32_fallbacks')})  lambda {lam:.6e} "
                   f"[{bits}] v[0:2] {v[0]:.17g} {v[1]:.17g}", flush=True)
 ctx.close()

@@ -87,6 +87,26 @@ __global__ __launch_bounds__(T) void read_rows(int ldv, const double* __restrict
     if (x.x == 12345.0) out[blockIdx.x] = x.y;
 }
 
+// streaming read of the fp32 shadow V32[:, :ncols] (+ src), one float2 per thread per column
+template <int T, int UB>
+__global__ __launch_bounds__(T) void read_rows32(int ldv, const float* __restrict__ V, int ncols,
+                                                 const double* __restrict__ src, double* __restrict__ out) {
+    const int jmax = ncols - 1;
+    const size_t r = (size_t(blockIdx.x) * T + threadIdx.x) * 2;
+    double2 x = *reinterpret_cast<const double2*>(src + r);
+    for (int j0 = 0; j0 < ncols; j0 += UB) {
+        float2 vb[UB];
+#pragma unroll
+        for (int u = 0; u < UB; ++u) vb[u] = *reinterpret_cast<const float2*>(V + size_t(min(j0 + u, jmax)) * ldv + r);
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            x.x += vb[u].x;
+            x.y += vb[u].y;
+        }
+    }
+    if (x.x == 12345.0) out[blockIdx.x] = x.y;
+}
+
 // the same bytes as 2-D tiles (1024 rows x 8 columns per 256-thread block)
 __global__ __launch_bounds__(256) void read_tiles(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                   double* __restrict__ out) {
@@ -125,8 +145,19 @@ int main(int argc, char** argv) {
     for (int j = 0; j < NC; ++j)
         for (int i = 0; i < n; ++i) hV[size_t(j) * ldv + i] = rnd() * 0.01;
     for (int i = 0; i < n; ++i) hw[i] = rnd();
-    double *V, *w, *f1, *f2, *part, *h, *npart, *out;
+    double *V, *w, *f1, *f2, *part, *h, *npart, *out, *psm, *hsm;
+    float* V32;
+    unsigned* fb;
     CK(hipMalloc(&V, hV.size() * 8));
+    CK(hipMalloc(&V32, hV.size() * 4));
+    CK(hipMalloc(&fb, 64));
+    CK(hipMalloc(&psm, size_t(NC + 3) * nrb * 8));
+    CK(hipMalloc(&hsm, size_t(NC + 3) * 8));
+    {
+        std::vector<float> h32(hV.size());
+        for (size_t i = 0; i < hV.size(); ++i) h32[i] = float(hV[i]);
+        CK(hipMemcpy(V32, h32.data(), h32.size() * 4, hipMemcpyHostToDevice));
+    }
     CK(hipMalloc(&w, size_t(ldv) * 8));
     CK(hipMalloc(&f1, size_t(ldv) * 8));
     CK(hipMalloc(&f2, size_t(ldv) * 8));
@@ -160,19 +191,47 @@ int main(int argc, char** argv) {
         rep("gemvt (prod, 1024x8 tiles)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
                                       b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr);
+                                      nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr);
             }),
             vbytes + 8.0 * n);
         rep("update<true> (prod, RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL(k_update<true>, dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J, 1,
-                                      u0val, n, nullptr, w, f1, npart, part, nrb, h);
+                hipExtLaunchKernelGGL((k_update<true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
+                                      1, u0val, n, nullptr, w, f1, npart, part, nrb, h, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
         rep("update<false> (prod, h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL(k_update<false>, dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J, 1,
-                                      u0val, n, h, w, f2, npart, nullptr, 0, nullptr);
+                hipExtLaunchKernelGGL((k_update<false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
+                                      J, 1, u0val, n, h, w, f2, npart, nullptr, 0, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
+        {  // the fp32 shadow: tiny coefficients (the accuracy test passes), ||src||^2 = 1
+            std::vector<double> ps(size_t(J + 2) * nrb, 1e-22), hs(J + 3, 1e-22 * nrb);
+            for (int b = 0; b < nrb; ++b) ps[size_t(J + 1) * nrb + b] = 1.0 / nrb;
+            hs[J + 1] = 1.0;
+            CK(hipMemcpy(psm, ps.data(), ps.size() * 8, hipMemcpyHostToDevice));
+            CK(hipMemcpy(hsm, hs.data(), hs.size() * 8, hipMemcpyHostToDevice));
+            CK(hipMemset(fb, 0, 4));
+        }
+        rep("update<true,B32> (RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
+                hipExtLaunchKernelGGL((k_update<true, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
+                                      1, u0val, n, nullptr, w, f1, npart, psm, nrb, h, V32, fb);
+            }),
+            vbytes / 2 + 16.0 * n);
+        rep("update<false,B32> (h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
+                hipExtLaunchKernelGGL((k_update<false, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
+                                      J, 1, u0val, n, hsm, w, f2, npart, nullptr, 0, nullptr, V32, fb);
+            }),
+            vbytes / 2 + 16.0 * n);
+        {
+            unsigned nf = 0;
+            CK(hipMemcpy(&nf, fb, 4, hipMemcpyDeviceToHost));
+            if (nf) std::printf("  B32 fell back %u times\n", nf);
+        }
+        rep("read_rows32<256,16>", timeit([&](hipEvent_t a, hipEvent_t b) {
+                hipExtLaunchKernelGGL((read_rows32<256, 16>), dim3(ldv / 512), dim3(256), 0, s, a, b, 0, ldv, V32, J, w,
+                                      out);
+            }),
+            vbytes / 2 + 8.0 * n);
         {
             std::vector<double> a(ldv), b(ldv);
             CK(hipMemcpy(a.data(), f1, size_t(ldv) * 8, hipMemcpyDeviceToHost));
