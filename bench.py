@@ -9,10 +9,18 @@ while the GPU solves) -> GPU KL swap loop to termination (rank 0: the loop is a
 sequential dependency chain) -> results/<base>_KL_CutSize_EIG_output.txt.
 
 N = 1 workload: configs[2] "ibm18.hgr EIG+KL on 1 MI355X".  ibm18.hgr is not
-shipped, so the stand-in is the seeded ISPD98-shaped synthetic at 1.0x, seed 1
-(201,920 nodes), written to a file in the untimed setup.  `value` = seconds
-per step (lower is better), the GPU context staying up across steps like a
-service (a fresh process also pays HIP start-up: `e2e_fresh_process_s`).
+shipped.  Real ibm18 is ONE connected circuit of 210,613 cells; the seeded
+ISPD98-shaped generator leaves ~7 % of its nodes in no net, and on such a
+disconnected graph lambda1 = 0 has a large eigenspace, so the Lanczos length
+there is set by rounding noise (the 1.0x seed-1 synthetic took 503, 1071 and
+1085 matvecs in three builds differing in last bits).  The stand-in is
+therefore the largest connected component of the generator's 1.15x seed-1
+output: 211,813 nodes (>= ibm18's cells and >= the 1.0x synthetic's 201,920),
+240,591 nets, 597,707 pins, written to a file in the untimed setup
+(`--workload full --mult 1.0` gives the whole 1.0x synthetic, which is also
+timed as configs.syn1).  `value` = seconds per step (lower is better), the GPU
+context staying up across steps like a service (a fresh process also pays HIP
+start-up: `e2e_fresh_process_s`).
 N > 1: the same file; the Lanczos rows are sharded (strong scaling of the
 sharded phase), the KL loop stays on rank 0.  `--gpus N` without WORLD_SIZE
 starts the N ranks itself (torch.distributed.run, before any GPU call).
@@ -21,9 +29,10 @@ Also reported: `roofline` of the Lanczos SpMV (HIP kernel timestamps of the
 SpMVs of the timed steps; SURVEY §8d algorithmic bytes; PMC traffic from
 rocprofv3 passes over a resident solve run as child processes before the
 GPU is touched here), `cpu_baseline` (the oracle restatement on this host's
-cores, 1 core and all cores, whole solve, swap log compared), per-config
-sub-results (ibm01, ibm10, 2x, the 1x synthetic's largest connected
-component), the resident-input solve time and the syn10 sharded Lanczos phase.
+cores, 1 core and all cores, whole solve of the headline workload to
+convergence, swap log compared), per-config sub-results (ibm01, ibm10, the
+whole 1.0x and 2.0x synthetics), the resident-input solve time and the syn10
+sharded Lanczos phase.
 """
 import argparse
 import csv
@@ -122,8 +131,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mult", type=float, default=1.0)
+    ap.add_argument("--mult", type=float, default=1.15)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--workload", choices=["lcc", "full"], default="lcc",
+                    help="lcc: the synthetic's largest connected component (default); full: the whole synthetic")
     ap.add_argument("--comm", choices=["auto", "rccl", "host"], default="auto",
                     help="multi-rank exchange: RCCL over xGMI, or host-staged (several ranks per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -151,11 +162,13 @@ def main():
     #  * PMC FETCH_SIZE / WRITE_SIZE of the SpMV over a resident solve (1x, 10x);
     #  * kernel trace of the 10x resident solve (syn10's roofline).
     prof = {}
+    lcc = args.workload == "lcc"
+    wl = f"{args.mult:g}lcc" if lcc else f"{args.mult:g}"  # tools/spmv_probe.py's workload argument
     if extras and not args.no_pmc:
         t = time.time()
-        prof["trace"] = rocprof_pass("trace", ["file", args.mult, args.seed, 1, 3], work, "1x")
-        prof["fetch"] = rocprof_pass("FETCH_SIZE", ["resident", args.mult, args.seed], work, "1x")
-        prof["write"] = rocprof_pass("WRITE_SIZE", ["resident", args.mult, args.seed], work, "1x")
+        prof["trace"] = rocprof_pass("trace", ["file", wl, args.seed, 1, 3], work, "1x")
+        prof["fetch"] = rocprof_pass("FETCH_SIZE", ["resident", wl, args.seed], work, "1x")
+        prof["write"] = rocprof_pass("WRITE_SIZE", ["resident", wl, args.seed], work, "1x")
         prof["trace10"] = rocprof_pass("trace", ["resident", 10.0, 10], work, "10x")
         prof["fetch10"] = rocprof_pass("FETCH_SIZE", ["resident", 10.0, 10], work, "10x")
         prof["write10"] = rocprof_pass("WRITE_SIZE", ["resident", 10.0, 10], work, "10x")
@@ -206,8 +219,10 @@ def main():
 
     # ---------------- untimed setup: the workload file
     h = ek.Hypergraph.generate(args.mult, args.seed)
+    if lcc:
+        h, _ = h.largest_component()
     nets, n, npins = h.dims()
-    path = os.path.join(work, f"syn{args.mult:g}x_seed{args.seed}.hgr")
+    path = os.path.join(work, f"syn{args.mult:g}x_seed{args.seed}{'_lcc' if lcc else ''}.hgr")
     h.write(path)
     out_dir = os.path.join(work, "out")
     os.makedirs(out_dir, exist_ok=True)
@@ -333,30 +348,27 @@ def main():
 
     # ---------------- sub-configs (N = 1): the file path on other inputs
     subs = {}
-    lcc_path = lcc_bits = lcc_log = None
     if extras:
-        hl, _ = h.largest_component()
         inputs = [("ibm01", os.path.join(GOLD, "ibm01.hgr"), "configs[1] ibm01.hgr (shipped)"),
                   ("ibm10", os.path.join(GOLD, "ibm10.hgr"), "ibm10.hgr: the largest shipped ISPD98 circuit, connected"),
-                  ("syn1_lcc", None, "largest connected component of the 1x seed-1 synthetic (non-degenerate Fiedler)"),
-                  ("syn2", None, "configs[3] circuit_generator 2.0x shape, seed 2")]
+                  ("syn1", (1.0, 1), "the whole 1.0x seed-1 synthetic (SURVEY §8d's first stand-in; disconnected: "
+                                     "lambda1 = 0, its Lanczos length set by rounding noise)"),
+                  ("syn2", (2.0, 2), "configs[3] circuit_generator 2.0x shape, seed 2 (disconnected)")]
         for name, p, what in inputs:
-            if p is None:
+            if isinstance(p, tuple):
+                hp = ek.Hypergraph.generate(*p)
                 p = os.path.join(work, f"{name}.hgr")
-                (hl if name == "syn1_lcc" else ek.Hypergraph.generate(2.0, 2)).write(p)
+                hp.write(p)
+                del hp
             walls, rr = [], None
-            # the connected ibm18-scale problem gets the headline's treatment:
-            # 2 untimed + 10 timed steps; the others a median of 2 warm runs
-            nrun, nwarm = (12, 2) if name == "syn1_lcc" else (3, 1)
+            # the previous rounds' headline workload (syn1) keeps the
+            # headline's treatment: 2 untimed + 10 timed steps; the others a
+            # median of 2 warm runs
+            nrun, nwarm = (12, 2) if name == "syn1" else (3, 1)
             for i in range(nrun):
                 t = time.time()
                 rr, _ = ctx.solve_file(p, eig=1, out_dir=out_dir)
                 walls.append(time.time() - t)
-            if name == "syn1_lcc":  # its split and swap log for the CPU baseline's KL comparison
-                lcc_path = p
-                _, lcc_log = ctx.solve_file(p, eig=1, out_dir=out_dir, log_cap=rr["nodes"] // 2)
-                ctx.kl_n = rr["nodes"]
-                lcc_bits = ctx.kl_sides(0)
             subs[name] = {"what": what, "nodes": rr["nodes"], "wall_s": round(float(np.median(walls[nwarm:])), 4),
                           "ms_per_step": round(1e3 * float(np.mean(walls[nwarm:])), 3),
                           "steps_timed": nrun - nwarm,
@@ -398,55 +410,42 @@ def main():
                 "laplacian/lanczos/kl = the solve's phases incl. first-launch costs; exit = the child reaped "
                 "(the executables leave the context to the process exit: EK_CLI_NO_TEARDOWN)")}
 
-    # ---------------- CPU baseline: oracle restatement on this host's cores
-    #  * the headline workload (all cores): its Lanczos is capped at 3x the
-    #    GPU's matvecs (the synthetic is disconnected: lambda1 = 0 has a large
-    #    eigenspace the thick-restart restatement does not settle within the cap);
-    #  * its largest connected component (a bounded, non-degenerate sample of the
-    #    same workload): to convergence, all cores and 1 core.  This is `value`,
-    #    timed beside the GPU's configs.syn1_lcc steps.
+    # ---------------- CPU baseline: oracle restatement on this host's cores,
+    # the whole solve of the headline workload itself to convergence, all
+    # cores (`value`) and 1 core; its KL() runs from the GPU run's split and
+    # its swap log is compared with the GPU's
     cpu = None
     if extras and not args.no_cpu_baseline:
         split_npz = os.path.join(work, "split.npz")
         np.savez(split_npz, bits=res_bits, log=res_log)
         ncpu = len(os.sched_getaffinity(0))
         all_cores = min(16, ncpu)  # the GPU box grants each job a 16-CPU share
-        gmv = last["lanczos"]["matvecs"]
+        cap = 0 if lcc else 3 * last["lanczos"]["matvecs"]  # a disconnected workload: capped (a lower bound)
         legs = {}
-        t = time.time()
-        legs["syn"] = cpu_baseline(path, split_npz, all_cores, 3 * gmv)
-        log(f"cpu baseline headline workload, {all_cores} threads: {time.time() - t:.1f} s: {legs['syn']}")
-        if lcc_bits is not None:
-            lcc_npz = os.path.join(work, "split_lcc.npz")
-            np.savez(lcc_npz, bits=lcc_bits, log=lcc_log)
-            for key, th in (("lcc", all_cores), ("lcc_1", 1)):
-                t = time.time()
-                legs[key] = cpu_baseline(lcc_path, lcc_npz, th, 0)
-                log(f"cpu baseline LCC, {th} thread(s): {time.time() - t:.1f} s: {legs[key]}")
-        best = legs.get("lcc", legs["syn"])
+        for key, th in (("all", all_cores), ("one", 1)):
+            t = time.time()
+            legs[key] = cpu_baseline(path, split_npz, th, cap)
+            log(f"cpu baseline, {th} thread(s): {time.time() - t:.1f} s: {legs[key]}")
+        best = legs["all"]
         if "error" not in best:
-            is_lcc = "lcc" in legs
-            gpu_same = subs["syn1_lcc"]["ms_per_step"] / 1e3 if is_lcc else sec_per_step
             cpu = {"value": round(best["total_s"], 3), "unit": "s", "cores": best["threads"], "kind": "port",
-                   "sample": ((f"the largest connected component of the headline workload ({subs['syn1_lcc']['nodes']:,}"
-                               f" of {n:,} nodes; the non-degenerate Fiedler problem), " if is_lcc else
-                               "the headline workload, ")
+                   "sample": ("the headline workload itself (" + f"{n:,} nodes), "
                               + "whole solve on the oracle restatement of cEIG+cKL (oracle/eko_eig.cpp, eko_kl.cpp), "
                               f"OpenMP on {best['threads']} pinned host cores: parse, Laplacian + Lanczos "
                               + (f"to convergence ({best['lanczos_matvecs']} matvecs)" if best["lanczos_converged"]
                                  else f"capped at {best['lanczos_matvecs']} matvecs, not converged (a lower bound)")
                               + f", KL() from the GPU run's split ({best['kl_iterations']} swaps, swap log "
                                 "compared with the GPU's)"),
-                   "gpu_same_sample_s": round(gpu_same, 4),
-                   "gpu_speedup_same_sample": round(best["total_s"] / gpu_same, 1),
+                   "gpu_same_sample_s": round(sec_per_step, 4),
+                   "gpu_speedup_same_sample": round(best["total_s"] / sec_per_step, 1),
                    "lanczos_converged": best["lanczos_converged"], "lanczos_matvecs": best["lanczos_matvecs"],
                    "parse_s": best["parse_s"], "lanczos_s": best["lanczos_s"], "kl_s": best["kl_s"],
                    "swap_log_match": best["swap_log_match"], "first_mismatch": best["first_mismatch"],
-                   "one_core": legs.get("lcc_1"),
-                   "headline_workload_capped": legs["syn"],
+                   "one_core": legs.get("one"),
                    "reference_cKL_note": "real cKL (oracle/_ref, built from /root/reference) is O(n^2) in setup and "
-                                         "per swap (cKL.cpp:53-72, 225-251): see BASELINE.md for its measured times "
-                                         "(2,440 s on this LCC)"}
+                                         "per swap (cKL.cpp:53-72, 225-251): tests/golden/ref_runs.json and "
+                                         "tests/golden/syn115_lcc/meta.json hold its measured times on the "
+                                         "1.0x LCC (2,440 s) and on this workload"}
         else:
             cpu = {"error": best["error"]}
 
@@ -503,7 +502,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f64 (Lanczos) + f32 (KL gains, bit-exact with cKL)",
         "data": "synthetic (seeded ISPD98-shaped generator written to .hgr; ibm18.hgr not shipped)",
-        "config": {"workload": f"ibm18-shape synthetic {args.mult:g}x seed {args.seed}: .hgr file -> results file",
+        "config": {"workload": (f"ibm18-size connected synthetic: largest component of the {args.mult:g}x seed-"
+                                f"{args.seed} generator output, .hgr file -> results file" if lcc else
+                                f"ibm18-shape synthetic {args.mult:g}x seed {args.seed}: .hgr file -> results file"),
                    "nodes": n, "nets": nets, "pins": npins, "laplacian_nnz": nnz_local if world == 1 else None,
                    "parallelism": f"lanczos row-shard x{world} ({comm if world > 1 else 'single'}), KL 1 GPU"},
         "roofline": roof,

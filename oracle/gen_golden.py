@@ -19,16 +19,18 @@ Runs in THIS container (the only place /root/reference exists):
    ``cKL <c>.hgr`` (random init, cKL.cpp:176-192) for the (circuit, seed)
    pairs in SEEDED and keeps ``results/<c>.hgr_KL_CutSize_output.txt`` as
    ``tests/golden/ref_results_seed/<c>.seed<S>.txt``.
-5. ``--lcc``: the largest connected component of the product generator's 1.0x
-   seed-1 synthetic (ek_hgr_largest_component; 184,306 nodes), its Fiedler
-   split from the oracle Lanczos (median split, sign: largest |v| positive),
-   and the REAL reference cKL run on it (``cKL syn1_lcc.hgr -EIG``, ~25 min on
-   4 cores): ``tests/golden/syn1_lcc/`` keeps the packed split bits, lambda /
-   median / the near-median nodes, and the gzipped reference results file.
+5. ``--lcc [MULT]``: the largest connected component of the product
+   generator's MULT x (default 1.0) seed-1 synthetic (ek_hgr_largest_component;
+   1.0x: 184,306 nodes; 1.15x: 211,813, the bench's headline workload), its
+   Fiedler split from the oracle Lanczos (median split, sign: largest |v|
+   positive), and the REAL reference cKL run on it (``cKL <name>.hgr -EIG``,
+   ~40 min on 4 cores at 1.0x): ``tests/golden/<name>/`` (syn1_lcc,
+   syn115_lcc) keeps the packed split bits, lambda / median / the near-median
+   nodes, and the gzipped reference results file.
 
 Usage: python oracle/gen_golden.py [circuit ...]   (default: all four)
        python oracle/gen_golden.py --seeded
-       python oracle/gen_golden.py --lcc [EIG_FILE REF_RESULTS_FILE]
+       python oracle/gen_golden.py --lcc [MULT [EIG_FILE REF_RESULTS_FILE]]
 """
 import json
 import os
@@ -72,11 +74,15 @@ def seeded():
     json.dump(runs, open(runs_path, "w"), indent=1, sort_keys=True)
 
 
-def lcc(eig_file=None, ref_results=None):
-    """syn1_lcc fixture.  eig_file / ref_results: an EIG file written for the
-    component and the reference results of a cKL run on it (the run takes
-    ~25 min on 4 cores), else both are made here (oracle Lanczos on all host
-    cores, then the reference)."""
+def lcc_name(mult):
+    return "syn1_lcc" if mult == 1.0 else "syn%s_lcc" % f"{mult:g}".replace(".", "")
+
+
+def lcc(mult="1.0", eig_file=None, ref_results=None):
+    """syn1_lcc / syn115_lcc fixture.  eig_file / ref_results: an EIG file
+    written for the component and the reference results of a cKL run on it
+    (the run takes ~40 min on 4 cores), else both are made here (oracle
+    Lanczos on all host cores, then the reference)."""
     import gzip
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -84,15 +90,17 @@ def lcc(eig_file=None, ref_results=None):
     from conftest import load_package
     import oracle
     ek = load_package()
-    dst = os.path.join(GOLD, "syn1_lcc")
+    mult = float(mult)
+    name = lcc_name(mult)
+    dst = os.path.join(GOLD, name)
     os.makedirs(dst, exist_ok=True)
-    h, _ = ek.Hypergraph.generate(1.0, 1).largest_component()
+    h, _ = ek.Hypergraph.generate(mult, 1).largest_component()
     with tempfile.TemporaryDirectory() as tmp:
-        path = os.path.join(tmp, "syn1_lcc.hgr")
+        path = os.path.join(tmp, f"{name}.hgr")
         h.write(path)
-        meta = {"nodes": h.nodes, "nets": h.nets,
-                "made_by": "oracle/gen_golden.py --lcc: oracle Lanczos (sign: largest |v| positive), median split, "
-                           "real reference cKL syn1_lcc.hgr -EIG"}
+        meta = {"nodes": h.nodes, "nets": h.nets, "generator": {"mult": mult, "seed": 1},
+                "made_by": f"oracle/gen_golden.py --lcc {mult:g}: oracle Lanczos (sign: largest |v| positive), "
+                           f"median split, real reference cKL {name}.hgr -EIG"}
         if eig_file is None:
             g = oracle.Graph.read(path)
             oracle.set_threads(os.cpu_count())
@@ -101,7 +109,7 @@ def lcc(eig_file=None, ref_results=None):
             med, bits = ek.median_split(v)
             meta.update(oracle_matvecs=st["matvecs"], oracle_residual=st["residual"])
             os.makedirs(os.path.join(tmp, "pre_saved_EIG"))
-            eig_file = os.path.join(tmp, "pre_saved_EIG", "syn1_lcc.hgr_out.txt")
+            eig_file = os.path.join(tmp, "pre_saved_EIG", f"{name}.hgr_out.txt")
             ek.eig_write(eig_file, lam, med, bits, v)
         lam, med, bits, v, _, _ = ek.eig_read(eig_file, h.nodes)
         near = np.flatnonzero(np.abs(v - med) <= 1e-8)
@@ -109,24 +117,26 @@ def lcc(eig_file=None, ref_results=None):
         np.save(os.path.join(dst, "split_bits.npy"), np.packbits(bits))
         if ref_results is None:
             os.makedirs(os.path.join(tmp, "pre_saved_EIG"), exist_ok=True)
-            if os.path.abspath(eig_file) != os.path.join(tmp, "pre_saved_EIG", "syn1_lcc.hgr_out.txt"):
-                shutil.copy(eig_file, os.path.join(tmp, "pre_saved_EIG", "syn1_lcc.hgr_out.txt"))
+            if os.path.abspath(eig_file) != os.path.join(tmp, "pre_saved_EIG", f"{name}.hgr_out.txt"):
+                shutil.copy(eig_file, os.path.join(tmp, "pre_saved_EIG", f"{name}.hgr_out.txt"))
             t0 = time.time()
-            subprocess.run([CKL, "syn1_lcc.hgr", "-EIG"], cwd=tmp, capture_output=True, text=True, check=True)
+            r = subprocess.run([CKL, f"{name}.hgr", "-EIG"], cwd=tmp, capture_output=True, text=True, check=True)
             meta["reference_wall_s"] = round(time.time() - t0, 1)
-            ref_results = os.path.join(tmp, "results", "syn1_lcc.hgr_KL_CutSize_EIG_output.txt")
+            meta["reference_summary"] = [ln.strip() for ln in r.stdout.splitlines() if ":" in ln and (
+                "Total iterations" in ln or "Initial cut" in ln or "Best cut" in ln or "Number of cores" in ln)]
+            ref_results = os.path.join(tmp, "results", f"{name}.hgr_KL_CutSize_EIG_output.txt")
         if os.path.exists(ref_results):
             with open(ref_results, "rb") as f, gzip.open(os.path.join(dst, "ref_results.txt.gz"), "wb", 9) as z:
                 z.write(f.read())
         json.dump(meta, open(os.path.join(dst, "meta.json"), "w"), indent=1)
-        print("lcc", {k: meta[k] for k in ("nodes", "lambda1", "median")}, len(near), "near-median")
+        print(name, {k: meta[k] for k in ("nodes", "lambda1", "median")}, len(near), "near-median", flush=True)
 
 
 def main(argv):
     if len(argv) > 1 and argv[1] == "--seeded":
         return seeded()
     if len(argv) > 1 and argv[1] == "--lcc":
-        return lcc(*argv[2:4])
+        return lcc(*argv[2:5])
     names = argv[1:] or CIRCUITS
     if not os.path.exists(CKL):
         subprocess.check_call(["make", "-f", os.path.join(HERE, "ref.mk")])

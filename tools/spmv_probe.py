@@ -14,6 +14,8 @@ the GPU itself, each pass a process of its own):
 
 usage: python tools/spmv_probe.py MODE MULT SEED [W K]
        python tools/spmv_probe.py MULT SEED          (= resident)
+MULT with the suffix "lcc" (e.g. 1.15lcc): the largest connected component of
+that synthetic (bench.py's headline workload).
 """
 import importlib.util
 import os
@@ -27,11 +29,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     args = sys.argv[1:]
     mode = args.pop(0) if args and args[0] in ("resident", "file") else "resident"
-    mult, seed = float(args[0]), int(args[1])
+    lcc = args[0].endswith("lcc")
+    mult, seed = float(args[0][:-3] if lcc else args[0]), int(args[1])
     spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
     ek = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ek)
     h = ek.Hypergraph.generate(mult, seed)
+    if lcc:
+        h, _ = h.largest_component()
     ctx = ek.Context(0)
     if mode == "resident":
         ctx.spmv_setup_pins(h)
