@@ -43,7 +43,7 @@ SWAP_DTYPE = np.dtype([("iter", "<u4"), ("node_left", "<u4"), ("node_right", "<u
 class LanczosOpts(ctypes.Structure):
     _fields_ = [("ncv", _I32), ("maxit", _I32), ("tol", ctypes.c_double), ("deflate", _I32),
                 ("time_spmv", _I32), ("reorth", _I32), ("check_every", _I32), ("basis32", _I32),
-                ("alpha_last", _I32)]
+                ("alpha_last", _I32), ("keep_min", _I32)]
 
 
 class LanczosStats(ctypes.Structure):
@@ -450,13 +450,14 @@ class Context:
         return us.value
 
     def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=1, check_every=8,
-                        basis32=True, alpha_last=False):
+                        basis32=True, alpha_last=False, keep_min=-1):
         """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207).  check_every: steps
         between mid-cycle convergence tests after the first cycle (0: at cycle ends only, Spectra's schedule).
         basis32: the update reads the basis's fp32 shadow when that is exact to fp64 rounding (ek_lanczos_opts).
-        alpha_last: the SpMV's last workgroup reduces alpha (default: every projection workgroup does)."""
+        alpha_last: the SpMV's last workgroup reduces alpha (default: every projection workgroup does).
+        keep_min: floor on the vectors an implicit restart keeps (-1: ncv/5, 0: Spectra's nev_adjusted alone)."""
         o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0, int(reorth),
-                        int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0)
+                        int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0, int(keep_min))
         st = LanczosStats()
         lam = ctypes.c_double()
         v = np.empty(self.n, np.float64)
@@ -508,7 +509,8 @@ class Context:
         return log[: min(r.iterations, cap)], res
 
     def solve_file(self, path, eig=1, seed=0, write_results=True, out_dir=None, limit=-1, sign_ref=None, ncv=0,
-                   tol=1e-10, deflate=True, time_spmv=False, log_cap=0, check_every=8, basis32=True, alpha_last=False):
+                   tol=1e-10, deflate=True, time_spmv=False, log_cap=0, check_every=8, basis32=True, alpha_last=False,
+                   keep_min=-1):
         """The whole path, .hgr -> results/ (ek_solve_file).  eig: 1 GPU Fiedler split (gKL2 -EIG), 2 the
         pre_saved_EIG file (cKL -EIG), 0 random split with std::mt19937(seed).  Returns (result dict, swap log)."""
         o = SolveOpts()
@@ -517,7 +519,7 @@ class Context:
         o.out_dir = os.fsencode(out_dir) if out_dir else None
         o.sign_ref = os.fsencode(sign_ref) if sign_ref else None
         o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, 1,
-                                int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0)
+                                int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0, int(keep_min))
         log = np.empty(max(int(log_cap), 1), SWAP_DTYPE)  # the library writes the first `iterations` records
         r = SolveResult()
         _chk(_lib.ek_solve_file(self._c, os.fsencode(path), ctypes.byref(o), _p(log), int(log_cap), ctypes.byref(r)),

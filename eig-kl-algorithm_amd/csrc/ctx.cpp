@@ -970,6 +970,7 @@ void ek_lanczos_default_opts(ek_lanczos_opts* o) {
     o->check_every = 8;
     o->basis32 = 1;
     o->alpha_last = 0;
+    o->keep_min = -1;
 }
 
 }  // extern "C"
@@ -1376,6 +1377,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
     std::vector<ek::QRot> rots;
     static const bool host_q = std::getenv("EK_DEVICE_Q") == nullptr;
+    // the restart's floor on the kept vectors (EK_KEEP_MIN overrides: A/B)
+    const int keep_min = std::getenv("EK_KEEP_MIN") ? std::atoi(std::getenv("EK_KEEP_MIN"))
+                         : o.keep_min < 0                ? m / 5
+                                                         : o.keep_min;
     int k = 0, restarts = 0, nconv = 0, injected = 0;
     double fn2_k = 1.0;  // ||f_k||^2 entering a cycle (after an implicit restart: the restart's residual)
     bool converged = false;
@@ -1528,7 +1533,13 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // (a fixed restart size of 8, 12 or 20 kept vectors, or a cap of 10-30,
         // was no better over ibm01 / industry2 / ibm10 / the 1x synthetic and
         // its largest component, and some sizes lost 3-12x on one of them)
-        const int knew = nev_adjusted(nev, m, nconv, zl);
+        int knew = nev_adjusted(nev, m, nconv, zl);
+        // a floor on Spectra's count: its rule keeps ncv/2 when no unwanted
+        // Ritz value has converged but only 1 + (those with |e_m^T y| < eps)
+        // otherwise, 2-4 vectors on these Laplacians, and a restart that
+        // keeps 3 of 100 throws the subspace away (the 1.15x LCC: 755
+        // matvecs with Spectra's rule, 527 with a floor of 20; tools/restart_ab.py)
+        if (keep_min > 0) knew = std::max(knew, std::min(keep_min, m - 1));
         if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
         std::vector<double> dd(d), ee(e);
         const auto tq0 = std::chrono::steady_clock::now();

@@ -212,6 +212,9 @@ typedef struct {
     int32_t alpha_last;  /* 0 (default): every projection workgroup re-reduces the SpMV's
                             alpha = v_i . w partials; 1: the SpMV's last workgroup does
                             (a serial tail on the SpMV; the same bits) */
+    int32_t keep_min;    /* implicit restarts keep at least this many vectors (floor on
+                            Spectra's nev_adjusted, which on these Laplacians often keeps
+                            2-4: DESIGN.md); < 0 (default): ncv / 5; 0: Spectra's rule */
 } ek_lanczos_opts;
 
 typedef struct {

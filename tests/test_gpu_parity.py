@@ -294,6 +294,31 @@ def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
         _fiedler_parity(name, lam_b, v_b, lam_ref, med_ref, bits_ref, v_ref, ek)
 
 
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2", "ibm10"])
+def test_lanczos_restart_floor_same_split_as_spectra_rule(ek, ctx, name):
+    """The implicit restart keeps at least ncv/5 vectors (keep_min default)
+    instead of Spectra's nev_adjusted alone (keep_min=0, which keeps 2-4 of
+    100 on these Laplacians): a different restart sequence, the same Fiedler
+    pair within the goldens' tolerances and the same median split."""
+    h = ek.Hypergraph.read(circuit_path(name))
+    L = h.laplacian()
+    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    lam_a, v_a, st_a = ctx.lanczos_fiedler()
+    lam_b, v_b, st_b = ctx.lanczos_fiedler(keep_min=0)
+    assert st_a["converged"] and st_b["converged"] and st_a["residual"] < 1e-9 and st_b["residual"] < 1e-9
+    assert abs(lam_a - lam_b) <= 1e-10
+    v_b = v_b * np.sign(v_a @ v_b)
+    assert np.abs(v_a - v_b).max() <= 1e-8
+    med_a, bits_a = ek.median_split(v_a)
+    med_b, bits_b = ek.median_split(v_b)
+    mask = (np.abs(v_a - med_a) > 1e-8) & (np.abs(v_b - med_b) > 1e-8)
+    assert np.array_equal(bits_a[mask], bits_b[mask])
+    if name != "ibm10":
+        lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
+        for lam, v in ((lam_a, v_a), (lam_b, v_b)):
+            _fiedler_parity(name, lam, v * np.sign(v @ v_ref), lam_ref, med_ref, bits_ref, v_ref, ek)
+
+
 @pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
 @pytest.mark.parametrize("deflate", [True, False])
 def test_lanczos_basis32_update_golden(ek, ctx, name, deflate):
@@ -319,14 +344,16 @@ def test_lanczos_basis32_update_golden(ek, ctx, name, deflate):
 def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
     """Disconnected synthetics (injected vectors, collapsed restart residuals):
     the shadow update converges to a null vector with the fp64 run's residual
-    bar, and the accuracy test never had to fall back on a regular step."""
+    bar.  The accuracy test falls back to the fp64 basis only on the rare
+    steps whose f' cancelled to near zero at an invariant subspace (a
+    breakdown: sum|h| ~ eps ||w|| then exceeds 2^-29 ||f'||)."""
     mult, seed = {"syn0.25": (0.25, 3), "syn2": (2.0, 2), "syn1": (1.0, 1)}[which]
     h = ek.Hypergraph.generate(mult, seed)
     ctx.spmv_setup_pins(h)
     lam, v, st = ctx.lanczos_fiedler()
     assert st["converged"] and st["residual"] < 1e-8 and abs(lam) < 1e-8
     assert np.all(np.isfinite(v)) and abs(np.linalg.norm(v) - 1) < 1e-10
-    assert st["update32_steps"] == st["matvecs"] and st["update32_fallbacks"] == 0, st
+    assert st["update32_steps"] == st["matvecs"] and st["update32_fallbacks"] <= 0.01 * st["matvecs"], st
 
 
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
