@@ -133,6 +133,7 @@ struct ek_ctx {
     DBuf V32, Vn32;  // the basis's fp32 shadow (ek_lanczos_opts::basis32) and its restart buffer
     DBuf fbk;        // launches whose fp32-shadow update fell back to V (a device counter)
     DBuf actr;  // the SpMV's last-block counter (alpha hand-off), zero between launches
+    DBuf gctr;  // the projection's column-group counters (k_gemvt hand-off), zero between launches
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
@@ -1134,10 +1135,14 @@ struct Lanczos {
     // ldv/512 workgroups reads all tot x nrb partials, quadratic in n) or one
     // k_reduce_cols launch ahead of k_update<false> (same col_sum2 order, the
     // same bits).  EK_UPD_RED=0/1 forces either (A/B).
-    static bool upd_reduces(int nrb) {
+    // 0: a k_reduce_cols launch; 1: every update workgroup; 2: the
+    // projection's last workgroup per column group (k_gemvt hand-off, the
+    // default up to 256 row blocks).  EK_UPD_RED=0/1/2 forces one (A/B; all
+    // three give the same bits).
+    static int upd_reduces(int nrb) {
         const char* e = std::getenv("EK_UPD_RED");
-        if (e && e[0]) return e[0] != '0';
-        return nrb <= EK_UPD_RED_MAX_NRB;
+        if (e && e[0]) return e[0] - '0';
+        return nrb <= EK_UPD_RED_MAX_NRB ? 2 : 0;
     }
     void factorize_fused(int k, int kend) {
         // EK_LANCZOS_TT=0: the separate three-term launch (A/B; the same bits)
@@ -1148,7 +1153,9 @@ struct Lanczos {
         double* fn2 = c->fn2.as<double>();
         double* a3 = c->scal.as<double>() + 2;
         const double* bov = c->bov.as<double>();
-        const bool upd_red = upd_reduces(nrb);
+        const int upd_red = upd_reduces(nrb);
+        unsigned* gctr = upd_red == 2 ? c->gctr.as<unsigned>() : nullptr;
+        double* hoff = upd_red == 2 ? c->h2.as<double>() : nullptr;
         for (int i = k; i < kend; ++i) {
             ek::dev::StepFin fin;
             if (i > seg0) {
@@ -1174,16 +1181,19 @@ struct Lanczos {
             if (tt_fused) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
                                   i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
-                                  col32(i), alpha_last ? nullptr : c->apart.as<double>(), c->nrb_spmv);
+                                  col32(i), alpha_last ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
                                     i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), col32(i));
                 ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>(),
-                               b32 ? 1 : 0);
+                               b32 ? 1 : 0, gctr, hoff);
             }
             // (b32: ||f'||^2 rides along as one more column of the partials)
             unsigned* fb = b32 ? c->fbk.as<unsigned>() : nullptr;
-            if (upd_red) {
+            if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
+                ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb);
+            } else if (upd_red == 1) {
                 ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
                                   c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb);
             } else {
@@ -1326,6 +1336,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     if (!c->actr.p) {
         c->actr.ensure((ek::dev::ALPHA_SUB + 1) * 256);
         HIPCHK(hipMemsetAsync(c->actr.p, 0, c->actr.bytes, s));
+    }
+    if (!c->gctr.p) {
+        c->gctr.ensure(size_t(ek::dev::GT_HANDOFF_UINTS) * 4);
+        HIPCHK(hipMemsetAsync(c->gctr.p, 0, c->gctr.bytes, s));
     }
     // padded rows must be exactly 0 (only those: every kernel writes real
     // rows before it reads them, and no kernel writes a padded row nonzero)

@@ -63,6 +63,19 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
     return r;
 }
 
+// Agent-scope (sc1) stores / loads: the hand-off of partials between
+// workgroups of one launch (MI355X_MICROARCH.md, inter-workgroup visibility)
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+constexpr int GT_SUB = 8;  // first-level counters per column group of the projection's hand-off
+constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (col_sum2)
+
 // partial dot products of w with GT_COLS basis columns over GT_ROWS rows.
 // 1-D grid of nrb * ncg blocks (ncg = ceil((ncols + has_u0) / GT_COLS));
 // 256 threads, each GT_ROWS/512 double2 rows; column ncols is the deflation
@@ -77,6 +90,15 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 // and the column-group-0 block of each row block stores it to fp for the
 // update: the three-term launch and its per-block re-reduction of the alpha
 // partials are gone, the bits are the same.
+// h_out != null (nrb <= 8 * 32): the column sums are reduced in this launch.
+// The partials are stored sc1; each workgroup's first wave waits for its
+// stores and adds to its column group's counter (GT_SUB first-level counters
+// on 256-B lines of their own, then a top counter); the workgroup completing
+// a column group sums that group's partials (sc1 loads) in col_sum2's order —
+// the bits k_reduce_cols and the update's in-kernel sums give — and writes
+// h_out, so the update needs no reduction of its own (its prologue was a
+// serial ~4 us of every update workgroup).  The counters are re-armed by
+// that workgroup for the next launch.
 // B32 (the fp32 basis shadow, k_update<_, true>): the column-group-0 block of
 // each row block also writes ||rhs||^2 over its rows to part column
 // ncols + has_u0 (the update's accuracy test reads the sum), and with TT
@@ -89,7 +111,8 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
                                                const double* __restrict__ fn2_i, const double* __restrict__ bov_i,
                                                double* __restrict__ fp, int nrm, float* __restrict__ v32col,
                                                const double* __restrict__ apart, int nparts,
-                                               double* __restrict__ alpha_pub) {
+                                               double* __restrict__ alpha_pub, unsigned* __restrict__ gctr,
+                                               double* __restrict__ h_out) {
     __shared__ double red[4][GT_COLS];
     __shared__ double nred[4];
     __shared__ double lds4[4];
@@ -203,10 +226,52 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     a1 += __shfl_xor(a1, 1, 64);
     if ((lane & 7) == 0) red[t >> 6][((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = a1;
     __syncthreads();
-    if (t < GT_COLS && j0 + t < ncols + has_u0)
-        part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-    if (nrm && j0 == 0 && t == 0)
-        part[size_t(ncols + has_u0) * nrb + rbk] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
+    const int tot = ncols + has_u0;
+    if (!h_out) {
+        if (t < GT_COLS && j0 + t < tot) part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+        if (nrm && j0 == 0 && t == 0) part[size_t(tot) * nrb + rbk] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
+        return;
+    }
+    // hand-off: every store below is made by wave 0
+    __shared__ int s_last;
+    if (t < GT_COLS && j0 + t < tot) st_sc1(part + size_t(j0 + t) * nrb + rbk, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]));
+    if (nrm && j0 == 0 && t == 0) st_sc1(part + size_t(tot) * nrb + rbk, (nred[0] + nred[1]) + (nred[2] + nred[3]));
+    const int cg = j0 / GT_COLS;
+    unsigned* ctr = gctr + size_t(cg) * (GT_SUB + 1) * 64;
+    if (t == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int g = rbk % GT_SUB;
+        const unsigned gsize = unsigned((nrb - g + GT_SUB - 1) / GT_SUB), ngroups = unsigned(nrb < GT_SUB ? nrb : GT_SUB);
+        int last = 0;
+        if (__hip_atomic_fetch_add(ctr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
+            last = __hip_atomic_fetch_add(ctr + GT_SUB * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   ngroups - 1u;
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // this group's columns (+ ||rhs||^2 in group 0): 8 lanes per column, lane
+    // l summing blocks l, l + 8, ... in order (col_sum2's loads and adds), then
+    // the xor tree
+    const int gq = t / CS_LANES, l = t % CS_LANES;
+    const int ncol = min(GT_COLS, tot - j0) + ((nrm && j0 == 0) ? 1 : 0);
+    if (gq < ncol) {
+        const int j = gq < GT_COLS && j0 + gq < tot ? j0 + gq : tot;  // (the last group member: the norm column)
+        const double* pc = part + size_t(j) * nrb;
+        constexpr int CB = 32;
+        double a = 0.0;
+        for (int b0 = l; b0 < nrb; b0 += CS_LANES * CB) {
+            double va[CB];
+#pragma unroll
+            for (int u = 0; u < CB; ++u) va[u] = ld_sc1(pc + min(b0 + CS_LANES * u, nrb - 1));
+#pragma unroll
+            for (int u = 0; u < CB; ++u) a += b0 + CS_LANES * u < nrb ? va[u] : 0.0;
+        }
+#pragma unroll
+        for (int o = 1; o < CS_LANES; o <<= 1) a += __shfl_xor(a, o, 64);
+        if (l == 0) h_out[j] = a;
+    }
+    if (t < GT_SUB + 1) ctr[t * 64] = 0u;  // re-armed for the next launch (visible at the kernel boundary)
 }
 
 // The sharded step's projection (ctx.cpp Lanczos::factorize_mr): the partial
@@ -311,7 +376,6 @@ __global__ __launch_bounds__(256) void k_gemvt3(int ldv, int nrb, const double* 
 // round trip for up to 8 * CB row blocks (ibm18 shape: 198).  (Two lanes per
 // column, as before, took four dependent round trips and every update
 // workgroup ~7.5 us of its 20.)
-constexpr int CS_LANES = 8;
 __device__ __forceinline__ void col_sum2(const double* __restrict__ pa, const double* __restrict__ pb, int nrb, int l,
                                          double* sa, double* sb) {
     constexpr int CB = 32;
@@ -807,21 +871,22 @@ __global__ __launch_bounds__(256) void k_sub_mean(double* __restrict__ x, int nr
 }
 
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
-           const double* w, double* part, int nrm) {
+           const double* w, double* part, int nrm, unsigned* gctr, double* h_out) {
     const int cols = ncols + has_u0;
     if (cols <= 0) return;
     hipLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
                        ncols, has_u0, u0val, nreal, w, part, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm,
-                       nullptr, nullptr, 0, nullptr);
+                       nullptr, nullptr, 0, nullptr, gctr, h_out);
 }
 
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
-              const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts) {
+              const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
+              unsigned* gctr, double* h_out) {
     const int cols = ncols + has_u0;
     hipLaunchKernelGGL(k_gemvt<true>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
                        ncols, has_u0, u0val, nreal, w, part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp,
-                       v32col ? 1 : 0, v32col, apart, nparts, apart ? const_cast<double*>(alpha) : nullptr);
+                       v32col ? 1 : 0, v32col, apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out);
 }
 
 

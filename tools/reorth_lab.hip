@@ -151,6 +151,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&V, hV.size() * 8));
     CK(hipMalloc(&V32, hV.size() * 4));
     CK(hipMalloc(&fb, 64));
+    unsigned* gctr;
+    CK(hipMalloc(&gctr, size_t(GT_HANDOFF_UINTS) * 4));
+    CK(hipMemset(gctr, 0, size_t(GT_HANDOFF_UINTS) * 4));
     CK(hipMalloc(&psm, size_t(NC + 3) * nrb * 8));
     CK(hipMalloc(&hsm, size_t(NC + 3) * 8));
     {
@@ -191,7 +194,13 @@ int main(int argc, char** argv) {
         rep("gemvt (prod, 1024x8 tiles)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
                                       b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr);
+                                      nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
+            }),
+            vbytes + 8.0 * n);
+        rep("gemvt + column-sum hand-off", timeit([&](hipEvent_t a, hipEvent_t b) {
+                hipExtLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
+                                      b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr, 1, nullptr, nullptr, 0, nullptr, gctr, h);
             }),
             vbytes + 8.0 * n);
         rep("update<true> (prod, RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
