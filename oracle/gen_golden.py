@@ -125,6 +125,11 @@ def lcc(mult="1.0", eig_file=None, ref_results=None):
             meta["reference_summary"] = [ln.strip() for ln in r.stdout.splitlines() if ":" in ln and (
                 "Total iterations" in ln or "Initial cut" in ln or "Best cut" in ln or "Number of cores" in ln)]
             ref_results = os.path.join(tmp, "results", f"{name}.hgr_KL_CutSize_EIG_output.txt")
+            val = lambda key: [ln.split(":", 1)[1].strip() for ln in meta["reference_summary"] if ln.startswith(key)][0]
+            meta["reference_run"] = {"binary": "oracle/_ref/cKL (built by oracle/ref.mk from /root/reference/cKL.cpp)",
+                                     "cmd": f"cKL {name}.hgr -EIG", "process_wall_s": meta["reference_wall_s"],
+                                     "iterations": int(val("Total iterations")),
+                                     "initial_cut": val("Initial cut size"), "best_cut": val("Best cut size achieved")}
         if os.path.exists(ref_results):
             with open(ref_results, "rb") as f, gzip.open(os.path.join(dst, "ref_results.txt.gz"), "wb", 9) as z:
                 z.write(f.read())

@@ -128,10 +128,17 @@ def test_solve_file_fresh_context_small(ek, tmp_path, name):
         c.close()
 
 
-def test_lcc_fiedler_and_kl_vs_reference(ek, oracle, ctx):
-    d = os.path.join(GOLD, "syn1_lcc")
+@pytest.mark.parametrize("name,mult", [("syn1_lcc", 1.0), ("syn115_lcc", 1.15)])
+def test_lcc_fiedler_and_kl_vs_reference(ek, oracle, ctx, name, mult):
+    """The connected synthetics (syn115_lcc: the bench's headline workload):
+    the Fiedler pair against the oracle's converged one and its median split,
+    then KL from that split against the REAL reference cKL's results file
+    (oracle/gen_golden.py --lcc) and the oracle swap by swap."""
+    d = os.path.join(GOLD, name)
+    if not os.path.exists(os.path.join(d, "ref_results.txt.gz")):
+        pytest.skip(f"{name}: reference run not committed")
     meta = json.load(open(os.path.join(d, "meta.json")))
-    h, _ = ek.Hypergraph.generate(1.0, 1).largest_component()
+    h, _ = ek.Hypergraph.generate(mult, 1).largest_component()
     n = h.nodes
     assert (n, h.nets) == (meta["nodes"], meta["nets"])
     bits_ref = np.unpackbits(np.load(os.path.join(d, "split_bits.npy")))[:n]
