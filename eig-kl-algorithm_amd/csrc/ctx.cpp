@@ -1553,7 +1553,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // otherwise, 2-4 vectors on these Laplacians, and a restart that
         // keeps 3 of 100 throws the subspace away (the 1.15x LCC: 755
         // matvecs with Spectra's rule, 527 with a floor of 20; tools/restart_ab.py)
-        if (keep_min > 0) knew = std::max(knew, std::min(keep_min, m - 1));
+        // Not when the wanted Ritz value is numerically zero: a disconnected
+        // graph, whose null space is degenerate; there keeping more vectors
+        // slowed convergence to a null vector (10x synthetic: 362 matvecs
+        // with Spectra's rule, 756 with a floor of 10, 994 with 20; the 1x
+        // and 2x synthetics likewise)
+        if (keep_min > 0 && std::fabs(theta[size_t(nev - 1)]) > 1e-8 * anorm_of()) knew = std::max(knew, std::min(keep_min, m - 1));
         if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
         std::vector<double> dd(d), ee(e);
         const auto tq0 = std::chrono::steady_clock::now();
