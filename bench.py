@@ -178,7 +178,18 @@ def main():
 
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo")
+        # gloo prints its peer connections on fd 1: rank 0's stdout must carry
+        # the JSON line alone, so fd 1 points at stderr while it connects
+        sys.stdout.flush()
+        fd1 = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(fd1, 1)
+            os.close(fd1)
 
     def barrier():
         if world > 1:
