@@ -714,14 +714,6 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     if (tid == 0 && (piece[0].x == -12345 || a.x == -12345)) s_stop[2] = 0;  // waits for the loads
                 }
                 stamp(10);
-                // the row's lock word and its chunk's current key depend on the
-                // descriptor alone (the row's first lane; 0 in the others:
-                // valid reads): issued with the decode's reads below, not after
-                // the sums (two more dependent LDS trips)
-                const uint32_t a_pl = uint32_t(a.w);
-                const int a_ls = int(a_pl >> 31), a_c = int(a_pl & 0x7fffffffu) / KL_CHUNK;
-                const uint32_t a_lockw = s_lock[a.x >> 5];
-                const u64 a_K = (a_ls ? ck1 : ck0)[a_c];  // stable until the barrier
                 v2f ie_seg = {0.0f, 0.0f};  // SEGC: the row's inline-segment sums (internal, external)
                 if constexpr (SEGC) {
                     // piece q = j8 + LPR*r holds entries 4q .. 4q+3.  Each lane
@@ -732,33 +724,14 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     // the pair to the next step.  No LDS staging round trip.
                     const uint32_t cmask = (1u << d.wcolbits) - 1u;
                     v2f cc[PPL][4];
-                    // every weight and side-word read of the lane's entries is
-                    // issued before the first use: one LDS round trip (the
-                    // compiler otherwise interleaved them with the decode,
-                    // four dependent trips)
-                    float wkv[PPL][4];
-                    uint32_t swv[PPL][4];
 #pragma unroll
                     for (int r = 0; r < PPL; ++r) {
                         const uint32_t wv4[4] = {uint32_t(piece[r].x), uint32_t(piece[r].y), uint32_t(piece[r].z),
                                                  uint32_t(piece[r].w)};
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            wkv[r][k] = s_wd[wv4[k] >> d.wcolbits];
-                            swv[r][k] = s_side[(wv4[k] & cmask) >> 5];
-                        }
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int r = 0; r < PPL; ++r) {
-                        const uint32_t wv4[4] = {uint32_t(piece[r].x), uint32_t(piece[r].y), uint32_t(piece[r].z),
-                                                 uint32_t(piece[r].w)};
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int x = int(wv4[k] & cmask);
-                            // side_now(x), from the word read above
-                            const bool ek = (((swv[r][k] >> (x & 31)) & 1u) != 0) ^ (x == A) ^ (x == B);
-                            const float wk = wkv[r][k];
+                            const float wk = s_wd[wv4[k] >> d.wcolbits];
+                            const bool ek = side_now(int(wv4[k] & cmask));
                             cc[r][k] = v2f{ek ? 0.0f : wk, ek ? wk : 0.0f};
                         }
                     }
@@ -798,11 +771,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[srow * KL_STAGE_ROW + j];
                 }
                 const int u = a.x, rp = a.y, len = a.z;
-                const bool act = !(((a_lockw >> (u & 31)) & 1u) || u == A || u == B);  // locked_now(u)
-                const uint32_t pl = a_pl;
-                const int ls = a_ls, pp = int(pl & 0x7fffffffu), c = a_c;
+                const bool act = !locked_now(u);
+                // the row's list, position, chunk and that chunk's current key
+                // depend on the descriptor only: read ahead of the sums
+                const uint32_t pl = uint32_t(a.w);
+                const int ls = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / KL_CHUNK;
                 const bool ab = ls ? c == cB : c == cA;  // node1's / node2's chunk: resolved in G2
-                const u64 K = a_K;
+                const u64 K = (ls ? ck1 : ck0)[c];       // stable until the barrier
                 stamp(6);
                 float internal = 0.0f, external = 0.0f;
                 {  // summed whether or not u is locked: a branch on `act` would let the
