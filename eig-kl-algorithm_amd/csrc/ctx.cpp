@@ -1169,6 +1169,7 @@ struct Lanczos {
                 fin.a3 = a3;
                 fin.fn2_i = fn2 + i - 1;
                 fin.bov_i = bov + i - 1;
+                fin.fast = b32 ? c->scal.as<double>() + 4 : nullptr;  // the update's ||f||^2 (or NaN)
             }
             const bool timed = spmv_timed_step(i);
             // the SpMV's last block also reduces alpha into a3 (k_three_term's bits)
@@ -1190,16 +1191,18 @@ struct Lanczos {
             }
             // (b32: ||f'||^2 rides along as one more column of the partials)
             unsigned* fb = b32 ? c->fbk.as<unsigned>() : nullptr;
+            // (b32: the update also leaves ||f||^2 = ||f'||^2 - ||h||^2 for the next SpMV)
+            double* fast = b32 ? c->scal.as<double>() + 4 : nullptr;
             if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast);
             } else if (upd_red == 1) {
                 ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
-                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb);
+                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast);
             } else {
                 ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0 + (b32 ? 1 : 0), c->h2.as<double>());
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast);
             }
             if (b32) ++u32_steps;
         }

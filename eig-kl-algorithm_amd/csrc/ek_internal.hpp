@@ -165,6 +165,9 @@ struct StepFin {
     const double* fn2_i = nullptr;
     const double* bov_i = nullptr;
     int nstride = 1;  // npart[k * nstride], k < nb (the sharded step: each rank's ||f||^2 in its all-gather slot)
+    // ||f||^2 from the update (||f'||^2 - ||h||^2, k_update B32) when not
+    // NaN; NaN: summed from npart
+    const double* fast = nullptr;
 };
 
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
@@ -326,11 +329,11 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
 // after u0's), else from V (*fb += 1 when fb != null)
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart,
-              const float* V32 = nullptr, unsigned* fb = nullptr);
+              const float* V32 = nullptr, unsigned* fb = nullptr, double* fn2_fast = nullptr);
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32 = nullptr,
-            unsigned* fb = nullptr);
+            unsigned* fb = nullptr, double* fn2_fast = nullptr);
 // fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
 // alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
 // alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]

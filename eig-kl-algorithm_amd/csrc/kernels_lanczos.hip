@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
                                                 const double* __restrict__ src, double* __restrict__ dst,
                                                 double* __restrict__ npart, const double* __restrict__ part, int nrb,
                                                 double* __restrict__ h_out, const float* __restrict__ V32,
-                                                unsigned* __restrict__ fb) {
+                                                unsigned* __restrict__ fb, double* __restrict__ fn2_fast) {
     constexpr int UB = EK_UPD_UB;
     constexpr int UB32 = 2 * EK_UPD_UB;  // fp32 columns per batch: the same bytes in flight
     constexpr int UBX = B32 ? UB32 : UB;
@@ -582,6 +582,18 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
         double a = (lane < ncols ? fabs(hc[lane]) : 0.0) + (lane + 64 < ncols ? fabs(hc[lane + 64]) : 0.0);
         a = wave_sum(a);
         const bool ok = a <= 0x1p-29 * sqrt(snrm);  // false for NaN
+        // ||f||^2 = ||f'||^2 - ||h||^2 - h_u0^2 (f = f' - V h - u0 h_u0 with
+        // the columns and u0 orthonormal): the next SpMV reads this one value
+        // instead of summing the ||f||^2 partials in every workgroup.  Exact
+        // to O(eps ||f'||^2) like the direct sum while ||h||^2 <= 2^-20
+        // ||f'||^2 (no cancellation); otherwise (a breakdown) NaN: the SpMV
+        // sums the partials
+        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) {
+            double q = 0.0;
+            for (int j = 0; j < ncols; ++j) q += hc[j] * hc[j];
+            if (has_u0) q += hu0 * hu0;
+            *fn2_fast = q <= 0x1p-20 * snrm ? snrm - q : __builtin_nan("");
+        }
         if (ok) {
             auto consume32 = [&](const float2* vb, int j0) {
 #pragma unroll
@@ -912,24 +924,25 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
 }
 
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
-            const double* h, const double* src, double* dst, double* npart, const float* V32, unsigned* fb) {
+            const double* h, const double* src, double* dst, double* npart, const float* V32, unsigned* fb,
+            double* fn2_fast) {
     if (V32)
         hipLaunchKernelGGL((k_update<false, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, h, src, dst, npart, nullptr, 0, nullptr, V32, fb);
+                           nreal, h, src, dst, npart, nullptr, 0, nullptr, V32, fb, fn2_fast);
     else
         hipLaunchKernelGGL((k_update<false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, h, src, dst, npart, nullptr, 0, nullptr, nullptr, nullptr);
+                           nreal, h, src, dst, npart, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
 }
 
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart,
-              const float* V32, unsigned* fb) {
+              const float* V32, unsigned* fb, double* fn2_fast) {
     if (V32)
         hipLaunchKernelGGL((k_update<true, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, nullptr, src, dst, npart, part, nrb, h_out, V32, fb);
+                           nreal, nullptr, src, dst, npart, part, nrb, h_out, V32, fb, fn2_fast);
     else
         hipLaunchKernelGGL((k_update<true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, nullptr, src, dst, npart, part, nrb, h_out, nullptr, nullptr);
+                           nreal, nullptr, src, dst, npart, part, nrb, h_out, nullptr, nullptr, nullptr);
 }
 
 void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1, const double* h2,

@@ -176,8 +176,11 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     const uint32_t pmask = (1u << pb) - 1u;
     for (int p = t; p <= P; p += PT) bst[p] = m.start[size_t(w) * P + p];
     for (int r = t; r < nr; r += PT) acc[r] = 0.0;
-    // ||f||^2 of the previous step (its partials' loads go out first)
-    const double npart_t = fin.npart ? panel_strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
+    // ||f||^2 of the previous step: the update's ||f'||^2 - ||h||^2 (fin.fast)
+    // or, when that is NaN (a breakdown), the partials, whose loads go out first
+    const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
+    const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
+    const double npart_t = sum_parts ? panel_strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
     __syncthreads();
     // The workgroup's chunks, panel by panel (every workgroup walks the panels
     // in the same order).  The next chunk's words and row indices are loaded
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     __syncthreads();  // the last chunk's runs are in acc
     double n2 = fn2 ? *fn2 : 1.0;
     if (fin.npart) {
-        n2 = panel_block_sum(npart_t, wsum);
+        n2 = sum_parts ? panel_block_sum(npart_t, wsum) : fastv;
         if (w == 0 && t == 0) {
             fin.fn2_out[0] = n2;
             if (fin.step >= 0) {

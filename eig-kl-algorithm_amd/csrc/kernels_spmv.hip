@@ -166,10 +166,14 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     // the solve: loading them in the segment's round trip, 13.1 us, or every
     // wave reducing all of them without barriers, 15.3 us, were both slower
     // than this form, 12.7 us.)
-    const double npart_t = fin.npart ? strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
+    // (fin.fast: the update's ||f'||^2 - ||h||^2, one value; the partials
+    // only when it is NaN, a breakdown)
+    const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
+    const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
+    const double npart_t = sum_parts ? strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
-            const double n2 = block_sum_all(npart_t, wsum);
+            const double n2 = sum_parts ? block_sum_all(npart_t, wsum) : fastv;
             if (blockIdx.x == 0 && t == 0) finalize_publish(fin, n2);
             return n2;
         }

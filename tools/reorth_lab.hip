@@ -205,12 +205,12 @@ int main(int argc, char** argv) {
             vbytes + 8.0 * n);
         rep("update<true> (prod, RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
-                                      1, u0val, n, nullptr, w, f1, npart, part, nrb, h, nullptr, nullptr);
+                                      1, u0val, n, nullptr, w, f1, npart, part, nrb, h, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
         rep("update<false> (prod, h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
-                                      J, 1, u0val, n, h, w, f2, npart, nullptr, 0, nullptr, nullptr, nullptr);
+                                      J, 1, u0val, n, h, w, f2, npart, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
         {  // the fp32 shadow: tiny coefficients (the accuracy test passes), ||src||^2 = 1
@@ -223,12 +223,12 @@ int main(int argc, char** argv) {
         }
         rep("update<true,B32> (RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<true, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
-                                      1, u0val, n, nullptr, w, f1, npart, psm, nrb, h, V32, fb);
+                                      1, u0val, n, nullptr, w, f1, npart, psm, nrb, h, V32, fb, nullptr);
             }),
             vbytes / 2 + 16.0 * n);
         rep("update<false,B32> (h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<false, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
-                                      J, 1, u0val, n, hsm, w, f2, npart, nullptr, 0, nullptr, V32, fb);
+                                      J, 1, u0val, n, hsm, w, f2, npart, nullptr, 0, nullptr, V32, fb, nullptr);
             }),
             vbytes / 2 + 16.0 * n);
         {
