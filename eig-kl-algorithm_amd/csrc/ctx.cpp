@@ -1034,6 +1034,9 @@ struct Lanczos {
     bool b32 = false;
     // alpha reduced by the SpMV's last workgroup (else by every projection workgroup)
     bool alpha_last = true;
+    // the basis passes read V (and V32) non-temporally: a basis larger than
+    // the MALL would otherwise evict the matrix and x every pass
+    bool nt = false;
     int u32_steps = 0;
     float* V32() { return b32 ? c->V32.as<float>() : nullptr; }
     float* col32(int j) { return b32 ? c->V32.as<float>() + size_t(j) * ldv : nullptr; }
@@ -1182,12 +1185,12 @@ struct Lanczos {
             if (tt_fused) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
                                   i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
-                                  col32(i), alpha_last ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff);
+                                  col32(i), alpha_last ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff, nt);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
                                     i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), col32(i));
                 ek::dev::gemvt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->f.as<double>(), c->part.as<double>(),
-                               b32 ? 1 : 0, gctr, hoff);
+                               b32 ? 1 : 0, gctr, hoff, nt);
             }
             // (b32: ||f'||^2 rides along as one more column of the partials)
             unsigned* fb = b32 ? c->fbk.as<unsigned>() : nullptr;
@@ -1195,14 +1198,14 @@ struct Lanczos {
             double* fast = b32 ? c->scal.as<double>() + 4 : nullptr;
             if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
             } else if (upd_red == 1) {
                 ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
-                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast);
+                                  c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
             } else {
                 ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0 + (b32 ? 1 : 0), c->h2.as<double>());
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
             }
             if (b32) ++u32_steps;
         }
@@ -1314,6 +1317,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.b32 = env_or("EK_BASIS32", o.basis32 != 0) && c->nranks == 1 && L.reorth == 1 &&
             std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
     L.alpha_last = env_or("EK_ALPHA_LAST", o.alpha_last != 0);
+    // non-temporal basis passes once the fp64 basis exceeds 768 MB (3x the
+    // 256 MB MALL): it cannot stay there, and sweeping it through evicts the
+    // matrix and x between SpMVs.  10x synthetic (1.6 GB): 404 -> 380 us per
+    // matvec; at 300 MB (the 2x synthetics) the basis still profits from the
+    // MALL (LCC 59.3 -> 61.2 ms with them).  EK_V_NT=0/1 forces either.
+    L.nt = env_or("EK_V_NT", ldv * size_t(m + 1) * 8 > (size_t(768) << 20));
     if (L.b32) {
         c->V32.ensure(ldv * size_t(m + 1) * 4);
         c->Vn32.ensure(ldv * size_t(m + 1) * 4);

@@ -290,12 +290,14 @@ constexpr int MAX_NCV = 128;
 // the implicit deflation vector u0 (value u0val on rows < nreal) if has_u0.
 // nrm: part column ncols + has_u0 also gets ||w||^2 over each row block
 // (the fp32-shadow update's accuracy test, k_update B32)
+// nt: the basis is read non-temporally (a basis larger than the MALL)
 // gctr / h_out (nrb <= 256): the column sums are also reduced in the launch
 // (the last workgroup of each column group; col_sum2's order) into h_out;
 // gctr: GT_HANDOFF_UINTS zeroed uints, re-armed by each launch
 constexpr int GT_HANDOFF_UINTS = ((MAX_NCV + 2 + GT_COLS - 1) / GT_COLS) * 9 * 64;
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val,
-           int nreal, const double* w, double* part, int nrm = 0, unsigned* gctr = nullptr, double* h_out = nullptr);
+           int nreal, const double* w, double* part, int nrm = 0, unsigned* gctr = nullptr, double* h_out = nullptr,
+           bool nt = false);
 // the sharded step (ctx.cpp factorize_mr): part for three vectors w, va, vb at
 // once, part[(k*tot + j)*nrb + b], tot = ncols + has_u0
 void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
@@ -317,7 +319,7 @@ void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, d
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col = nullptr, const double* apart = nullptr,
-              int nparts = 0, unsigned* gctr = nullptr, double* h_out = nullptr);
+              int nparts = 0, unsigned* gctr = nullptr, double* h_out = nullptr, bool nt = false);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 
@@ -329,11 +331,11 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
 // after u0's), else from V (*fb += 1 when fb != null)
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart,
-              const float* V32 = nullptr, unsigned* fb = nullptr, double* fn2_fast = nullptr);
+              const float* V32 = nullptr, unsigned* fb = nullptr, double* fn2_fast = nullptr, bool nt = false);
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32 = nullptr,
-            unsigned* fb = nullptr, double* fn2_fast = nullptr);
+            unsigned* fb = nullptr, double* fn2_fast = nullptr, bool nt = false);
 // fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
 // alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
 // alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]

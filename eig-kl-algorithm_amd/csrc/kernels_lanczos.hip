@@ -74,6 +74,30 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
         reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
 }
 constexpr int GT_SUB = 8;  // first-level counters per column group of the projection's hand-off
+
+// Basis loads.  NT: non-temporal (no Infinity-Cache allocation), for a basis
+// larger than the MALL, which it would otherwise sweep clean every pass,
+// evicting the matrix and x the next SpMV reads
+typedef double v2d_t __attribute__((ext_vector_type(2)));
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ double2 ld_basis(const double* p) {
+    if constexpr (NT) {
+        const v2d_t v = __builtin_nontemporal_load(reinterpret_cast<const v2d_t*>(p));
+        return make_double2(v.x, v.y);
+    } else {
+        return *reinterpret_cast<const double2*>(p);
+    }
+}
+template <bool NT>
+__device__ __forceinline__ float2 ld_basis32(const float* p) {
+    if constexpr (NT) {
+        const v2f_t v = __builtin_nontemporal_load(reinterpret_cast<const v2f_t*>(p));
+        return make_float2(v.x, v.y);
+    } else {
+        return *reinterpret_cast<const float2*>(p);
+    }
+}
 constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (col_sum2)
 
 // partial dot products of w with GT_COLS basis columns over GT_ROWS rows.
@@ -103,7 +127,7 @@ constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (co
 // each row block also writes ||rhs||^2 over its rows to part column
 // ncols + has_u0 (the update's accuracy test reads the sum), and with TT
 // the fp32 copy of v_i to v32col (vi rows are loaded here anyway).
-template <bool TT>
+template <bool TT, bool NT>
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part, const double* __restrict__ alpha,
@@ -143,7 +167,7 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
         }
 #pragma unroll
         for (int jj = 0; jj < GT_COLS; ++jj)
-            vs[k][jj] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+            vs[k][jj] = ld_basis<NT>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
     }
     if constexpr (TT) {  // k_three_term's f' (same operations, same order)
         // apart != null: alpha = sum of the SpMV's per-block partials, reduced
@@ -470,7 +494,7 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
 // zero) every workgroup takes the same decision (the same h and norm, the
 // same sums) and runs the fp64 loop (*fb counts those launches).
 // ||src||^2 comes as one more column of the partials (k_gemvt's nrm) or h.
-template <bool RED, bool B32>
+template <bool RED, bool B32, bool NT>
 __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restrict__ V, int ncols, int has_u0,
                                                 double u0val, int nreal, const double* __restrict__ h,
                                                 const double* __restrict__ src, double* __restrict__ dst,
@@ -507,7 +531,7 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
     auto load_batch = [&](double2* vb, int j0) {
 #pragma unroll
-        for (int u = 0; u < UB; ++u) vb[u] = *reinterpret_cast<const double2*>(V + size_t(min(j0 + u, jmax)) * ldv + r);
+        for (int u = 0; u < UB; ++u) vb[u] = ld_basis<NT>(V + size_t(min(j0 + u, jmax)) * ldv + r);
     };
     double2 x = *reinterpret_cast<const double2*>(src + r);
     auto consume = [&](const double2* vb, int j0) {
@@ -540,7 +564,7 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     auto load32 = [&](float2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB32; ++u)
-            vb[u] = *reinterpret_cast<const float2*>(V32 + size_t(min(j0 + u, jmax)) * ldv + r);
+            vb[u] = ld_basis32<NT>(V32 + size_t(min(j0 + u, jmax)) * ldv + r);
     };
     if constexpr (B32) {
         load32(fa, 0);
@@ -883,22 +907,34 @@ __global__ __launch_bounds__(256) void k_sub_mean(double* __restrict__ x, int nr
 }
 
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
-           const double* w, double* part, int nrm, unsigned* gctr, double* h_out) {
+           const double* w, double* part, int nrm, unsigned* gctr, double* h_out, bool nt) {
     const int cols = ncols + has_u0;
     if (cols <= 0) return;
-    hipLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
-                       ncols, has_u0, u0val, nreal, w, part, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm,
-                       nullptr, nullptr, 0, nullptr, gctr, h_out);
+    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS));
+    if (nt)
+        hipLaunchKernelGGL((k_gemvt<false, true>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
+                           h_out);
+    else
+        hipLaunchKernelGGL((k_gemvt<false, false>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
+                           h_out);
 }
 
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
-              unsigned* gctr, double* h_out) {
+              unsigned* gctr, double* h_out, bool nt) {
     const int cols = ncols + has_u0;
-    hipLaunchKernelGGL(k_gemvt<true>, dim3(nrb * ((cols + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, ldv, nrb, V,
-                       ncols, has_u0, u0val, nreal, w, part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp,
-                       v32col ? 1 : 0, v32col, apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out);
+    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS));
+    if (nt)
+        hipLaunchKernelGGL((k_gemvt<true, true>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
+                           apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, v32col ? 1 : 0, v32col, apart, nparts,
+                           apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out);
+    else
+        hipLaunchKernelGGL((k_gemvt<true, false>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
+                           apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, v32col ? 1 : 0, v32col, apart, nparts,
+                           apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out);
 }
 
 
@@ -923,27 +959,42 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
                        ncols_total, h);
 }
 
+#define EK_UPDATE_LAUNCH(RED, B32, NT, ...) \
+    hipLaunchKernelGGL((k_update<RED, B32, NT>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, __VA_ARGS__)
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32, unsigned* fb,
-            double* fn2_fast) {
-    if (V32)
-        hipLaunchKernelGGL((k_update<false, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, h, src, dst, npart, nullptr, 0, nullptr, V32, fb, fn2_fast);
+            double* fn2_fast, bool nt) {
+    if (V32 && nt)
+        EK_UPDATE_LAUNCH(false, true, true, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0, nullptr,
+                         V32, fb, fn2_fast);
+    else if (V32)
+        EK_UPDATE_LAUNCH(false, true, false, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
+                         nullptr, V32, fb, fn2_fast);
+    else if (nt)
+        EK_UPDATE_LAUNCH(false, false, true, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
+                         nullptr, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_update<false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, h, src, dst, npart, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
+        EK_UPDATE_LAUNCH(false, false, false, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
+                         nullptr, nullptr, nullptr, nullptr);
 }
 
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* part, int nrb, double* h_out, const double* src, double* dst, double* npart,
-              const float* V32, unsigned* fb, double* fn2_fast) {
-    if (V32)
-        hipLaunchKernelGGL((k_update<true, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, nullptr, src, dst, npart, part, nrb, h_out, V32, fb, fn2_fast);
+              const float* V32, unsigned* fb, double* fn2_fast, bool nt) {
+    if (V32 && nt)
+        EK_UPDATE_LAUNCH(true, true, true, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
+                         h_out, V32, fb, fn2_fast);
+    else if (V32)
+        EK_UPDATE_LAUNCH(true, true, false, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
+                         h_out, V32, fb, fn2_fast);
+    else if (nt)
+        EK_UPDATE_LAUNCH(true, false, true, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
+                         h_out, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_update<true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val,
-                           nreal, nullptr, src, dst, npart, part, nrb, h_out, nullptr, nullptr, nullptr);
+        EK_UPDATE_LAUNCH(true, false, false, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
+                         h_out, nullptr, nullptr, nullptr);
 }
+#undef EK_UPDATE_LAUNCH
 
 void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, const double* h1, const double* h2,
                    int step, double* alpha, double* offd, const double* a3, const double* fn2_i, const double* bov_i) {

@@ -192,24 +192,24 @@ int main(int argc, char** argv) {
             std::printf("J=%3d %-34s %8.2f us  %7.1f GB/s\n", J, name, us, bytes / us / 1e3);
         };
         rep("gemvt (prod, 1024x8 tiles)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
+                hipExtLaunchKernelGGL((k_gemvt<false, false>), dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
                                       b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
                                       nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
             }),
             vbytes + 8.0 * n);
         rep("gemvt + column-sum hand-off", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL(k_gemvt<false>, dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
+                hipExtLaunchKernelGGL((k_gemvt<false, false>), dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
                                       b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
                                       nullptr, nullptr, 1, nullptr, nullptr, 0, nullptr, gctr, h);
             }),
             vbytes + 8.0 * n);
         rep("update<true> (prod, RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL((k_update<true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
+                hipExtLaunchKernelGGL((k_update<true, false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
                                       1, u0val, n, nullptr, w, f1, npart, part, nrb, h, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
         rep("update<false> (prod, h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL((k_update<false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
+                hipExtLaunchKernelGGL((k_update<false, false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
                                       J, 1, u0val, n, h, w, f2, npart, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
@@ -222,12 +222,12 @@ int main(int argc, char** argv) {
             CK(hipMemset(fb, 0, 4));
         }
         rep("update<true,B32> (RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL((k_update<true, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
+                hipExtLaunchKernelGGL((k_update<true, true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
                                       1, u0val, n, nullptr, w, f1, npart, psm, nrb, h, V32, fb, nullptr);
             }),
             vbytes / 2 + 16.0 * n);
         rep("update<false,B32> (h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
-                hipExtLaunchKernelGGL((k_update<false, true>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
+                hipExtLaunchKernelGGL((k_update<false, true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
                                       J, 1, u0val, n, hsm, w, f2, npart, nullptr, 0, nullptr, V32, fb, nullptr);
             }),
             vbytes / 2 + 16.0 * n);
