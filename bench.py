@@ -416,7 +416,7 @@ def main():
         else:
             fresh = fb["exit"]
             fresh_breakdown = {"offsets_s": fb, "what": (
-                "median offsets from the spawn of `gKL2 <1x .hgr> -EIG --quiet` (5 runs): lib_loaded = exec + "
+                "median offsets from the spawn of `gKL2 <headline .hgr> -EIG --quiet` (5 runs): lib_loaded = exec + "
                 "dynamic loading; hip_first_call..hip_streams = ek_init on its thread (beside the parse); "
                 "laplacian/lanczos/kl = the solve's phases incl. first-launch costs; exit = the child reaped "
                 "(the executables leave the context to the process exit: EK_CLI_NO_TEARDOWN)")}

@@ -154,8 +154,6 @@ struct ek_ctx {
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
     double* chk_pin = nullptr;
     double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1))
-    ek::QRot* rot_pin = nullptr;  // ... and of its rotations (MAX_NCV x MAX_NCV)
-    DBuf rotd;
     // the last Fiedler vector as returned (normalised, sign fixed), kept on
     // the device for ek_kl_set_partition_fiedler, and that split's scratch
     DBuf fied, sp_sorted, sp_flag, sp_pos, sp_tmp;
@@ -358,7 +356,6 @@ void ek_destroy(ek_ctx* c) {
     (void)hipStreamDestroy(c->stream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
     if (c->q_pin) (void)hipHostFree(c->q_pin);
-    if (c->rot_pin) (void)hipHostFree(c->rot_pin);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->up) (void)hipHostFree(c->up);
@@ -1370,9 +1367,6 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                              hipHostMallocDefault));
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
                              size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) * 8, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->rot_pin),
-                             size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV) * sizeof(ek::QRot),
-                             hipHostMallocDefault));
     }
     if (L.time_spmv) {  // created once per context: ~200 creations per solve cost milliseconds
         while (c->spmv_ev.size() < size_t(2 * m)) {
@@ -1402,7 +1396,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     std::vector<double> d(size_t(m), 0.0), e(size_t(m), 0.0), theta(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
     std::vector<double> alpha_h(size_t(m + 1)), offd_h(size_t(m + 1)), fn2_h(size_t(m + 2));
     std::vector<ek::QRot> rots;
-    static const bool host_q = std::getenv("EK_DEVICE_Q") == nullptr;
+    std::vector<double> qscratch;
     // the restart's floor on the kept vectors (EK_KEEP_MIN overrides: A/B)
     const int keep_min = std::getenv("EK_KEEP_MIN") ? std::atoi(std::getenv("EK_KEEP_MIN"))
                          : o.keep_min < 0                ? m / 5
@@ -1574,40 +1568,23 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
         std::vector<double> dd(d), ee(e);
         const auto tq0 = std::chrono::steady_clock::now();
-        double sigma = 0.0;               // Q(m-1, knew-1)
-        const double* sigma_dev = nullptr;  // ... or where the device left it
-        if (!host_q) {
-            // EK_DEVICE_Q=1 (A/B): the shifts' rotations recorded on the host
-            // (O(m) each: the tridiagonal only), Q accumulated from them on
-            // the device (k_apply_rots, the host's operations: the same
-            // bits).  One workgroup walking ~9k dependent rotations is
-            // latency-bound: 1.36 ms per restart against ~0.02 ms of extra
-            // host time for accumulating Q beside the shifts, so the host
-            // form is the default
-            rots.clear();
-            for (int i = knew; i < m; ++i)  // Q starts as the identity: lower bandwidth i - knew
-                ek::tridiag_qr_shift_rots(m, dd.data(), ee.data(), theta[size_t(i)], i - knew, rots);
-            const size_t rb = rots.size() * sizeof(ek::QRot);
-            std::memcpy(c->rot_pin, rots.data(), rb);  // pinned: the upload is a plain DMA
-            c->rotd.ensure(std::max<size_t>(rb, 64));
-            if (rb) HIPCHK(hipMemcpyAsync(c->rotd.p, c->rot_pin, rb, hipMemcpyHostToDevice, s));
-            ek::dev::apply_rots(s, m, c->rotd.as<ek::QRot>(), int(rots.size()), knew + 1, c->Qd.as<double>());
-            sigma_dev = c->Qd.as<double>() + size_t(knew - 1) * m + size_t(m - 1);
-        } else {  // default: Q accumulated on the host beside the shifts
-            double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
-            std::fill(Q, Q + size_t(m) * size_t(m), 0.0);
-            for (int i = 0; i < m; ++i) Q[size_t(i) * m + i] = 1.0;
-            for (int i = knew; i < m; ++i)
-                ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], Q, i - knew);
-            sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];
-            HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
-        }
+        // the unwanted Ritz values as shifts; of Q only the kept columns and
+        // the residual's are used: formed right to left from the rotations
+        // (ek::accumulate_q).  (A device form that applied the rotations with
+        // one workgroup, k_apply_rots, lost: ~9k dependent rotations took 1.36
+        // ms per restart against ~0.3 ms on the host for all of Q.)
+        rots.clear();
+        for (int i = knew; i < m; ++i) ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], rots);
+        double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
+        ek::accumulate_q(m, rots, knew + 1, Q, qscratch);
+        const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
+        HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
         const double hk = ee[size_t(knew - 1)];  // H(knew, knew-1)
         ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>(),
                          L.b32 ? c->Vn32.as<float>() : nullptr);
         ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
-                            c->npart.as<double>(), sigma_dev);
+                            c->npart.as<double>());
         L.reduce_scalar(c->fn2.as<double>() + knew);
         HIPCHK(hipMemcpyAsync(&fn2_k, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
         std::swap(c->V.p, c->Vn.p);

@@ -110,19 +110,17 @@ uint64_t hashtable_next_buckets(uint64_t cur);  // bucket count after the rehash
 // eigenvalues (ascending) of the symmetric tridiagonal (d, e), e[i] = T(i+1,i);
 // zlast[j] = last component of eigenvector j; full Z (m x m col-major) if Z != null.
 bool tridiag_eig(int m, const double* d, const double* e, double* evals, double* zlast, double* Z);
-// one implicit symmetric QR step with shift mu on (d, e); accumulates Q (m x m col-major) <- Q G.
-// band >= 0: Q's lower bandwidth before this step (0 for the identity, +1 per
-// step), so rows below it are skipped; -1: full columns.
-void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int band = -1);
-// the same step, Q's Givens rotations recorded in order instead of applied:
-// rotation {p, iend, c, s} is Q[i][p], Q[i][p+1] <- c a + s b, -s a + c b
-// (a, b their old values) on rows i < iend
+// one implicit symmetric QR step with shift mu on (d, e); the rotations of
+// its Q factor appended to rots in order: {p, c, s} is Q <- Q G_p, i.e.
+// Q[i][p], Q[i][p+1] <- c a + s b, -s a + c b (a, b their old values)
 struct QRot {
-    int32_t p, iend;
+    int32_t p;
     double c, s;
 };
-void tridiag_qr_shift_rots(int m, double* d, double* e, double mu, int band, std::vector<QRot>& rots);
-void tridiag_qr_shift_impl(int m, double* d, double* e, double mu, double* Q, int band, std::vector<QRot>* rots);
+void tridiag_qr_shift(int m, double* d, double* e, double mu, std::vector<QRot>& rots);
+// columns [0, kk) of Q = I G_1 ... G_R (rots in order) into Qcm (col-major
+// m x kk); X is scratch
+void accumulate_q(int m, const std::vector<QRot>& rots, int kk, double* Qcm, std::vector<double>& X);
 }  // namespace ek
 
 // ---------------------------------------------------------------------------
@@ -362,14 +360,8 @@ void split_flags_scan(hipStream_t s, void* tmp, size_t tmp_bytes, const double* 
                       uint32_t* pos0);
 void split_scatter(hipStream_t s, const double* v, const uint32_t* pos0, int n, double med, int32_t* order0,
                    int32_t* order1, uint32_t* plist, uint8_t* side);
-// f = f*sigma + x*hk ; per-block sum of f^2 -> npart (sigma_dev: read sigma
-// from device memory instead, when not null)
-void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart,
-                const double* sigma_dev = nullptr);
-// Q = I_m with the recorded rotations applied in order (the host's
-// accumulation in tridiag_qr_shift, same operations), columns [0, kk) to
-// Qout (column-major m x kk): one workgroup, each lane owning a row of Q
-void apply_rots(hipStream_t s, int m, const QRot* rots, int nrot, int kk, double* Qout);
+// f = f*sigma + x*hk ; per-block sum of f^2 -> npart
+void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart);
 // x = x / sqrt(*n2) ... and deflate helpers
 void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* mean_sum, double inv_n);
 void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares);

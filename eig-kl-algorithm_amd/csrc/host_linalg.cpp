@@ -96,25 +96,16 @@ bool tridiag_eig(int m, const double* d_in, const double* e_in, double* evals, d
 }
 
 // One implicitly shifted symmetric QR step (bulge chase) with shift mu:
-// T <- G^T T G, Q <- Q G, where G = G_0 ... G_{m-2} is the orthogonal factor
-// of the QR decomposition of T - mu I (implicit-Q theorem).  Equivalent to
-// Spectra's explicit TridiagQR(H - mu I) followed by R Q + mu I.  The
-// implicit-Q theorem needs an unreduced matrix, so negligible off-diagonals
-// (|e_i| <= eps (|d_i| + |d_i+1|), zeroed as TridiagQR does) split T into
-// blocks and the chase restarts at the top of every block — a chase that
-// simply ran through a split would stop there and never shift the trailing
-// block, which is the one that carries the residual row (Q(m-1, :)).
-void tridiag_qr_shift(int m, double* d, double* e, double mu, double* Q, int band) {
-    tridiag_qr_shift_impl(m, d, e, mu, Q, band, nullptr);
-}
-
-// The same step with Q's rotations recorded instead of applied ({p, iend, c,
-// s} in order: Q <- Q G_p on rows < iend), for the device accumulation
-void tridiag_qr_shift_rots(int m, double* d, double* e, double mu, int band, std::vector<QRot>& rots) {
-    tridiag_qr_shift_impl(m, d, e, mu, nullptr, band, &rots);
-}
-
-void tridiag_qr_shift_impl(int m, double* d, double* e, double mu, double* Q, int band, std::vector<QRot>* rots) {
+// T <- G^T T G, where G = G_0 ... G_{m-2} is the orthogonal factor of the QR
+// decomposition of T - mu I (implicit-Q theorem); G's rotations are appended
+// to rots in order (Q <- Q G_p each).  Equivalent to Spectra's explicit
+// TridiagQR(H - mu I) followed by R Q + mu I.  The implicit-Q theorem needs an
+// unreduced matrix, so negligible off-diagonals (|e_i| <= eps (|d_i| +
+// |d_i+1|), zeroed as TridiagQR does) split T into blocks and the chase
+// restarts at the top of every block — a chase that simply ran through a
+// split would stop there and never shift the trailing block, which is the one
+// that carries the residual row (Q(m-1, :)).
+void tridiag_qr_shift(int m, double* d, double* e, double mu, std::vector<QRot>& rots) {
     if (m < 2) return;
     // band scratch: only |i-j| <= 2 is ever non-zero (the chase's bulge), so
     // row i keeps columns i-2 .. i+2 (5 entries; same operations, same order
@@ -154,23 +145,41 @@ void tridiag_qr_shift_impl(int m, double* d, double* e, double mu, double* Q, in
             at(i, q) = -s * ap + c * aq;
         }
         if (!split[size_t(p)]) at(q, p - 1) = at(p - 1, q) = 0.0;  // bulge annihilated
-        // Q has lower bandwidth `band` before this sweep, so columns p and q
-        // are zero below row q + band: the rotation leaves those rows alone
-        const int iend = band >= 0 ? std::min(m, q + band + 1) : m;
-        if (rots) {
-            rots->push_back(QRot{p, iend, c, s});
-            continue;
-        }
-        double* qp = Q + size_t(p) * m;
-        double* qq = Q + size_t(q) * m;
-        for (int i = 0; i < iend; ++i) {
-            const double a = qp[i], b = qq[i];
-            qp[i] = c * a + s * b;
-            qq[i] = -s * a + c * b;
-        }
+        rots.push_back(QRot{p, c, s});
     }
     for (int i = 0; i < m; ++i) d[i] = at(i, i);
     for (int i = 0; i + 1 < m; ++i) e[i] = 0.5 * (at(i + 1, i) + at(i, i + 1));
+}
+
+// Columns [0, kk) of Q = G_1 G_2 ... G_R (the recorded rotations, in order)
+// into Qcm (column-major m x kk).  The restart needs only those kk columns,
+// so Q E (E = I(:, 0:kk)) is formed right to left, G_1 (G_2 (... (G_R E))):
+// each rotation then mixes two ROWS of an m x kk matrix X (kk contiguous
+// doubles each) instead of two length-m columns of the full m x m Q, and X
+// is zero below a row `hi` that a rotation (p, p+1) can raise only to p+1 —
+// one row per shift sweep walked backwards — so rotations below it are
+// skipped.  At ncv 100 with 20 kept: ~100k row-element updates instead of
+// ~600k for the forward accumulation of all of Q.
+void accumulate_q(int m, const std::vector<QRot>& rots, int kk, double* Qcm, std::vector<double>& X) {
+    X.assign(size_t(m) * size_t(kk), 0.0);
+    for (int i = 0; i < kk; ++i) X[size_t(i) * kk + i] = 1.0;
+    int hi = kk - 1;  // rows > hi of X are zero
+    for (size_t r = rots.size(); r-- > 0;) {
+        const QRot g = rots[r];
+        const int p = g.p;
+        if (p > hi) continue;
+        if (p + 1 > hi) hi = p + 1;
+        // G_p X on rows p, p+1: G_p(p,p) = c, G_p(p,q) = -s, G_p(q,p) = s, G_p(q,q) = c
+        double* xp = X.data() + size_t(p) * kk;
+        double* xq = xp + kk;
+        for (int j = 0; j < kk; ++j) {
+            const double a = xp[j], b = xq[j];
+            xp[j] = g.c * a - g.s * b;
+            xq[j] = g.s * a + g.c * b;
+        }
+    }
+    for (int j = 0; j < kk; ++j)
+        for (int i = 0; i < m; ++i) Qcm[size_t(j) * m + i] = X[size_t(i) * kk + j];
 }
 
 }  // namespace ek

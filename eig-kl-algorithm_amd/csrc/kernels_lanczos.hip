@@ -875,9 +875,8 @@ __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restri
 // f = f*sigma + x*hk, per-block sum of f^2
 __global__ __launch_bounds__(256) void k_axpby_norm(double* __restrict__ f, double sigma,
                                                     const double* __restrict__ x, double hk,
-                                                    double* __restrict__ npart, const double* __restrict__ sigma_dev) {
+                                                    double* __restrict__ npart) {
     __shared__ double lds4[4];
-    if (sigma_dev) sigma = *sigma_dev;
     const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
     double2 a = *reinterpret_cast<const double2*>(f + r);
     const double2 b = *reinterpret_cast<const double2*>(x + r);
@@ -1057,79 +1056,8 @@ void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, in
                        out32);
 }
 
-void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart,
-                const double* sigma_dev) {
-    hipLaunchKernelGGL(k_axpby_norm, dim3(ldv / UPD_ROWS), dim3(256), 0, s, f, sigma, x, hk, npart, sigma_dev);
-}
-
-// The restart's Q on the device (ctx.cpp implicit restart): lane i owns row i
-// of Q (in LDS, odd stride) and applies every rotation in order, so no lane
-// ever reads another's data and no barrier is needed.  Within a sweep,
-// rotation p+1 takes column p+1 as rotation p left it: that value stays in a
-// register.  The host's rows-below-band skip is kept (a skipped row keeps its
-// exact zeros, as on the host), and the products and sums are separate
-// roundings (no contraction), so Q has the host's bits.
-// The rotation list is read 64 at a time, one rotation per lane, the next 64
-// in flight while these are applied, and broadcast by readlane: a load per
-// rotation on the chain costs ~0.3 us each (thousands per restart).
-__device__ __forceinline__ double readlane_f64(double x, int j) {
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_readlane(int(b & 0xffffffffll), j);
-    const int hi = __builtin_amdgcn_readlane(int(b >> 32), j);
-    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
-}
-
-__global__ __launch_bounds__(MAX_NCV) void k_apply_rots(int m, const QRot* __restrict__ rots, int nrot, int kk,
-                                                      double* __restrict__ Qout) {
-#pragma clang fp contract(off)
-    extern __shared__ double qs[];  // [MAX_NCV][m | 1]
-    const int i = threadIdx.x, ld = m | 1, lane = i & 63;
-    const bool own = i < m;
-    if (own)
-        for (int j = 0; j < m; ++j) qs[i * ld + j] = i == j ? 1.0 : 0.0;
-    // (no barrier: every lane touches its own row only)
-    double carry = 0.0;
-    int cq = -1;  // column whose current value is `carry` (-1: none)
-    QRot nx{0, 0, 0.0, 0.0};
-    if (lane < nrot) nx = rots[lane];
-    for (int base = 0; base < nrot; base += 64) {
-        const QRot cur = nx;
-        if (base + 64 + lane < nrot) nx = rots[base + 64 + lane];
-        const int cnt = nrot - base < 64 ? nrot - base : 64;
-        for (int j = 0; j < cnt; ++j) {
-            const int p = __builtin_amdgcn_readlane(cur.p, j), iend = __builtin_amdgcn_readlane(cur.iend, j);
-            const double gc = readlane_f64(cur.c, j), gs = readlane_f64(cur.s, j);
-            if (!own) continue;
-            const int q = p + 1;
-            if (i >= iend) {  // below the band: the host leaves this row alone
-                if (cq >= 0) qs[i * ld + cq] = carry;
-                cq = -1;
-                continue;
-            }
-            double a;
-            if (cq == p) a = carry;
-            else {
-                if (cq >= 0) qs[i * ld + cq] = carry;
-                a = qs[i * ld + p];
-            }
-            const double b = qs[i * ld + q];
-            const double t1 = gc * a, t2 = gs * b;
-            const double t3 = -gs * a, t4 = gc * b;
-            qs[i * ld + p] = t1 + t2;
-            carry = t3 + t4;
-            cq = q;
-        }
-    }
-    if (own) {
-        if (cq >= 0) qs[i * ld + cq] = carry;
-        for (int j = 0; j < kk; ++j) Qout[size_t(j) * m + i] = qs[i * ld + j];
-    }
-}
-
-void apply_rots(hipStream_t s, int m, const QRot* rots, int nrot, int kk, double* Qout) {
-    const int threads = (m + 63) / 64 * 64;
-    hipLaunchKernelGGL(k_apply_rots, dim3(1), dim3(threads), size_t(MAX_NCV) * size_t(m | 1) * 8, s, m, rots, nrot,
-                       kk, Qout);
+void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart) {
+    hipLaunchKernelGGL(k_axpby_norm, dim3(ldv / UPD_ROWS), dim3(256), 0, s, f, sigma, x, hk, npart);
 }
 
 // Lanczos start vector: x[r] = st_{row0+r+1} / (2^31 - 1) - 0.5 for the

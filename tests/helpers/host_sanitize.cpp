@@ -3,6 +3,7 @@
 // synthetic generator, malformed inputs and edge-case hypergraphs, and the
 // drop-in CLIs' argument / file error paths.  Exits non-zero on a wrong
 // result; the sanitizers abort on any memory or UB error.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -113,7 +114,23 @@ int main(int argc, char** argv) {
         Q[size_t(i) * m + size_t(i)] = 1.0;
     }
     REQUIRE(ek::tridiag_eig(m, d.data(), e.data(), th.data(), zl.data(), Z.data()));
-    for (int i = 10; i < m; ++i) ek::tridiag_qr_shift(m, d.data(), e.data(), th[size_t(i)], Q.data(), i - 10);
+    std::vector<ek::QRot> rots;
+    for (int i = 10; i < m; ++i) ek::tridiag_qr_shift(m, d.data(), e.data(), th[size_t(i)], rots);
+    // the restart's right-to-left column accumulation against all of Q
+    // formed left to right (Q <- Q G_p, rotation by rotation)
+    for (const ek::QRot& r : rots)
+        for (int i = 0; i < m; ++i) {
+            double* qp = Q.data() + size_t(r.p) * m;
+            const double a = qp[i], b = qp[size_t(m) + size_t(i)];
+            qp[i] = r.c * a + r.s * b;
+            qp[size_t(m) + size_t(i)] = -r.s * a + r.c * b;
+        }
+    const int kk = 11;
+    std::vector<double> Qk(size_t(m) * kk), X;
+    ek::accumulate_q(m, rots, kk, Qk.data(), X);
+    double dmax = 0.0;
+    for (size_t i = 0; i < Qk.size(); ++i) dmax = std::max(dmax, std::fabs(Qk[i] - Q[i]));
+    REQUIRE(dmax < 1e-13);
     // CLI paths that end before the GPU (usage, missing files) or at it
     auto cli = [&](std::vector<std::string> a) {
         std::vector<char*> av;

@@ -357,7 +357,7 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
 
 
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
-@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_DEVICE_Q=1", "EK_ALPHA_LAST=1", "EK_UPD_RED=0", "EK_UPD_RED=1",
+@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_ALPHA_LAST=1", "EK_UPD_RED=0", "EK_UPD_RED=1",
                                     "EK_UPD_RED=2", "EK_V_NT=1"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Device-side restructurings give the bits of the forms they replace:
@@ -369,9 +369,7 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
       group (EK_UPD_RED=2, the default up to 256 row blocks), by every update
       workgroup (1) or by a k_reduce_cols launch (0, the default above);
     * the basis passes' non-temporal loads (EK_V_NT=1; the default above 768
-      MB of basis) against plain ones;
-    * the implicit restart's Q accumulated on the device from the host's
-      rotation list (EK_DEVICE_Q=1, k_apply_rots) vs on the host (default).
+      MB of basis) against plain ones.
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses."""
     import subprocess
