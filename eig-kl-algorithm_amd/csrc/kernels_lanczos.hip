@@ -157,6 +157,15 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     constexpr int KR = GT_ROWS / 512;
     const int jmax = ncols > 0 ? ncols - 1 : 0;
     double2 xs[KR], vs[KR][GT_COLS], tv[KR], tu[KR];
+    // up to AP_EARLY * 256 alpha partials: their loads go out FIRST (in-order
+    // returns: alpha is then reduced while the tile is still in flight)
+    constexpr int AP_EARLY = 12;
+    const bool ap_early = TT && apart && nparts <= AP_EARLY * 256;
+    double apv[AP_EARLY];
+    if (ap_early) {
+#pragma unroll
+        for (int u = 0; u < AP_EARLY; ++u) apv[u] = apart[min(t + u * 256, nparts - 1)];
+    }
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
         const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
@@ -172,10 +181,19 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     if constexpr (TT) {  // k_three_term's f' (same operations, same order)
         // apart != null: alpha = sum of the SpMV's per-block partials, reduced
         // by this workgroup in k_three_term's order (the same bits as the
-        // SpMV's last-block reduction), its loads behind the tile's; the
-        // first workgroup publishes it for the finalize
+        // SpMV's last-block reduction); the first workgroup publishes it for
+        // the finalize.  Up to 3,072 partials their loads go out ahead of the
+        // tile's (ap_early): the wave's loads return in order, so with them
+        // behind the tile alpha waited for the whole tile and then for its
+        // own round trip (projection 21.9 -> 20.5 us at the headline, rocprof)
         if (apart) {
-            double sa = strided_sum256(apart, nparts);
+            double sa = 0.0;  // strided_sum256's order: t, t + 256, ..., then + 0.0 past the end
+            if (ap_early) {
+#pragma unroll
+                for (int u = 0; u < AP_EARLY; ++u) sa += t + u * 256 < nparts ? apv[u] : 0.0;
+            } else {
+                sa = strided_sum256(apart, nparts);
+            }
             sa = block_sum256(sa, lds4);
             if (t == 0) {
                 s_alpha = sa;
