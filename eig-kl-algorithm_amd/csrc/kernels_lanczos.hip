@@ -127,7 +127,7 @@ constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (co
 // each row block also writes ||rhs||^2 over its rows to part column
 // ncols + has_u0 (the update's accuracy test reads the sum), and with TT
 // the fp32 copy of v_i to v32col (vi rows are loaded here anyway).
-template <bool TT, bool NT>
+template <bool TT, bool NT, int APE = 12>
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part, const double* __restrict__ alpha,
@@ -158,8 +158,9 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     const int jmax = ncols > 0 ? ncols - 1 : 0;
     double2 xs[KR], vs[KR][GT_COLS], tv[KR], tu[KR];
     // up to AP_EARLY * 256 alpha partials: their loads go out FIRST (in-order
-    // returns: alpha is then reduced while the tile is still in flight)
-    constexpr int AP_EARLY = 12;
+    // returns: alpha is then reduced while the tile is still in flight);
+    // APE 12 up to 3,072 partials, 24 up to 6,144 (the 2x synthetics)
+    constexpr int AP_EARLY = APE;
     const bool ap_early = TT && apart && nparts <= AP_EARLY * 256;
     double apv[AP_EARLY];
     if (ap_early) {
@@ -944,14 +945,19 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
               unsigned* gctr, double* h_out, bool nt) {
     const int cols = ncols + has_u0;
     const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS));
-    if (nt)
-        hipLaunchKernelGGL((k_gemvt<true, true>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
-                           apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, v32col ? 1 : 0, v32col, apart, nparts,
-                           apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out);
-    else
-        hipLaunchKernelGGL((k_gemvt<true, false>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
-                           apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, v32col ? 1 : 0, v32col, apart, nparts,
-                           apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out);
+#define EK_GEMVT_TT(NT_, APE_)                                                                                    \
+    hipLaunchKernelGGL((k_gemvt<true, NT_, APE_>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, \
+                       part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, v32col ? 1 : 0, v32col, apart,     \
+                       nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out)
+    const bool wide = apart && nparts > 12 * 256;  // 24 partials a thread (up to 6,144; beyond: strided_sum256)
+    if (nt) {
+        if (wide) EK_GEMVT_TT(true, 24);
+        else EK_GEMVT_TT(true, 12);
+    } else {
+        if (wide) EK_GEMVT_TT(false, 24);
+        else EK_GEMVT_TT(false, 12);
+    }
+#undef EK_GEMVT_TT
 }
 
 
