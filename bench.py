@@ -90,28 +90,84 @@ def rocprof_pass(what, probe_args, work, tag):
     files = glob.glob(os.path.join(d, "**", pat), recursive=True)
     if r.returncode != 0 or not files:
         log(f"rocprofv3 {what} pass ({tag}) failed (rc {r.returncode}): {r.stderr[-300:]}")
-        return None
+        return {"error": f"rc {r.returncode}, {len(files)} output files"}
     if what == "trace":
         return {row["Name"]: (int(row["Calls"]), float(row["AverageNs"])) for row in csv.DictReader(open(files[0]))}
-    vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(files[0]))
-            if "k_spmv_adaptive" in row["Kernel_Name"]]
+    # every SpMV form: k_spmv_adaptive (CSR segments) and k_spmv_panel (the
+    # column-panel form of a large x: the 10x synthetic)
+    rows = list(csv.DictReader(open(files[0])))
+    vals = [float(row["Counter_Value"]) for row in rows
+            if "k_spmv_adaptive" in row["Kernel_Name"] or "k_spmv_panel" in row["Kernel_Name"]]
+    kernels = sorted({row["Kernel_Name"].split("(")[0][:60] for row in rows if "k_spmv" in row["Kernel_Name"]})
     if not vals:
-        return None
-    return {"bytes": sum(vals) / len(vals) * 1024.0, "dispatches": len(vals)}
+        names = sorted({row["Kernel_Name"].split("(")[0][:50] for row in rows})
+        log(f"rocprofv3 {what} pass ({tag}): NO SpMV dispatch among {len(rows)} rows (kernels: {names[:12]})")
+        return {"error": f"no k_spmv dispatch in {len(rows)} counter rows"}
+    return {"bytes": sum(vals) / len(vals) * 1024.0, "dispatches": len(vals), "kernels": kernels}
 
 
 def kernel_avg_us(stats, needle):
     """(calls, average us) of the kernels whose name holds `needle` (calls-weighted)."""
-    rows = [v for k, v in (stats or {}).items() if needle in k]
+    if not stats or "error" in stats:
+        return 0, None
+    rows = [v for k, v in stats.items() if needle in k]
     calls = sum(c for c, _ in rows)
     return (calls, sum(c * a for c, a in rows) / calls / 1e3) if calls else (0, None)
 
 
 def traffic_of(fetch, write):
+    """PMC traffic per SpMV launch, or {"error": ...} naming the pass that failed (never a silent None)."""
     if not fetch or not write:
-        return None
+        return {"error": "PMC passes not run"}
+    bad = {k: v["error"] for k, v in (("FETCH_SIZE", fetch), ("WRITE_SIZE", write)) if "error" in v}
+    if bad:
+        return {"error": bad}
     return {"traffic": round(2 * fetch["bytes"] + write["bytes"]), "fetch_raw_bytes": round(fetch["bytes"]),
-            "write_bytes": round(write["bytes"]), "dispatches": fetch["dispatches"]}
+            "write_bytes": round(write["bytes"]), "dispatches": fetch["dispatches"], "kernels": fetch["kernels"]}
+
+
+def compare_results(mine, ref):
+    """cKL results rows 'iter\\tcut\\tgain' (cKL.cpp:315,380): iteration and gain
+    columns as printed, the cut within max(0.05, 3e-5 |cut0|) (the reference's
+    initial cut is a racy OpenMP fp32 sum, cKL.cpp:203).  Returns (ok, detail)."""
+    a = [ln.split("\t") for ln in mine.strip().splitlines()]
+    b = [ln.split("\t") for ln in ref.strip().splitlines()]
+    if len(a) != len(b):
+        return False, f"{len(a)} rows vs {len(b)}"
+    tol = max(0.05, 3e-5 * abs(float(b[0][1])))
+    worst = 0.0
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x[0] != y[0] or x[2] != y[2]:
+            return False, f"row {i}: {x} vs {y}"
+        worst = max(worst, abs(float(x[1]) - float(y[1])))
+        if worst > tol:
+            return False, f"row {i}: cut {x[1]} vs {y[1]}"
+    return True, f"{len(a)} rows equal (iteration, gain as printed; cut within {worst:.3g} <= {tol:.3g})"
+
+
+def headline_parity(ctx, path, out_dir, n, last, is_headline):
+    """The timed step's own output against the committed REFERENCE fixture
+    (tests/golden/syn115_lcc: the real cKL's results file on the split of the
+    converged Fiedler vector; data, not the oracle): its device split on every
+    node, and its results file row by row (cKL.cpp:436-444, cEIG.cpp:204-209)."""
+    import gzip
+    gold = os.path.join(REPO, "tests", "golden", "syn115_lcc")
+    if not is_headline or not os.path.exists(os.path.join(gold, "ref_results.txt.gz")):
+        return {"headline_vs_reference": None, "why": "no reference fixture for this workload"}
+    meta = json.load(open(os.path.join(gold, "meta.json")))
+    bits_ref = np.unpackbits(np.load(os.path.join(gold, "split_bits.npy")))[:n]
+    sides = ctx.kl_sides(0)  # the initial partition the last timed step's device split left
+    ndiff = int(np.count_nonzero(sides != bits_ref))
+    near = np.zeros(n, bool)
+    near[meta["near_median_nodes"]] = True
+    mine = open(os.path.join(out_dir, "results", os.path.basename(path) + "_KL_CutSize_EIG_output.txt")).read()
+    ok, detail = compare_results(mine, gzip.open(os.path.join(gold, "ref_results.txt.gz"), "rt").read())
+    iters_ok = last["kl"]["iterations"] == meta["reference_run"]["iterations"]
+    return {"headline_vs_reference": bool(ok and ndiff == 0 and iters_ok),
+            "split_nodes_differing": ndiff, "near_median_nodes_differing": int(np.count_nonzero((sides != bits_ref) & near)),
+            "near_median_nodes": int(near.sum()), "results_file": detail,
+            "iterations": [last["kl"]["iterations"], meta["reference_run"]["iterations"]],
+            "reference": "tests/golden/syn115_lcc: real cKL (built from cKL.cpp) run on the converged Fiedler split"}
 
 
 def cpu_baseline(hgr, split_npz, threads, max_matvec):
@@ -126,7 +182,40 @@ def cpu_baseline(hgr, split_npz, threads, max_matvec):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
+def become_subreaper():
+    """Orphans of this bench's children (a profiler's helper, a tool's child)
+    are re-parented to this process instead of init, so reap_strays() sees and
+    ends exactly the processes this run left behind (procs_at_end 1)."""
+    import ctypes
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(36, 1, 0, 0, 0)  # PR_SET_CHILD_SUBREAPER
+    except (OSError, AttributeError):
+        pass
+
+
+def reap_strays():
+    """Descendants still alive at the end: logged by command line, then ended (by PID)."""
+    try:
+        import psutil
+    except ImportError:
+        return None
+    left = []
+    for p in psutil.Process().children(recursive=True):
+        try:
+            left.append({"pid": p.pid, "cmd": " ".join(p.cmdline())[:160]})
+            p.terminate()
+        except psutil.Error:
+            pass
+    if left:
+        log(f"processes this bench left behind (terminated): {left}")
+        _, alive = psutil.wait_procs([psutil.Process(x["pid"]) for x in left if psutil.pid_exists(x["pid"])], timeout=5)
+        for p in alive:
+            p.kill()
+    return left
+
+
 def main():
+    become_subreaper()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -260,6 +349,10 @@ def main():
     log(f"timed: {args.steps} steps, {sec_per_step * 1e3:.2f} ms/step; last step {last['t_total']:.4f} s "
         f"(lanczos {last['t_lanczos']:.4f}, kl {last['t_kl']:.4f}, {last['lanczos']['matvecs']} matvecs, "
         f"{last['kl']['iterations']} swaps)")
+    parity = None
+    if rank == 0:
+        parity = headline_parity(ctx, path, out_dir, n, last, lcc and args.mult == 1.15 and args.seed == 1)
+        log(f"parity: {parity}")
     lz = [r[0]["lanczos"] for r in results]
     spmv_timed = sum(x["spmv_timed"] for x in lz)
     spmv_us = 1e3 * sum(x["spmv_ms"] for x in lz) / max(1, spmv_timed)
@@ -345,9 +438,14 @@ def main():
             syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,
                                 "achieved_GBps": round(b10 / us10_rp / 1e3, 1),
                                 "frac": round(b10 / us10_rp / 1e3 / HBM_PEAK_GBS, 4)}
-        t10 = traffic_of(prof.get("fetch10"), prof.get("write10"))
-        if t10:
-            t10["per_algorithmic_byte"] = round(t10["traffic"] / b10, 3)
+        if extras and not args.no_pmc:
+            t10 = traffic_of(prof.get("fetch10"), prof.get("write10"))
+            if "error" not in t10:
+                t10["per_algorithmic_byte"] = round(t10["traffic"] / b10, 3)
+                t10["stored_bytes_per_rank"] = int(c10.spmv_format(fused=False)[1])
+                t10["per_stored_byte"] = round(t10["traffic"] / t10["stored_bytes_per_rank"], 3)
+            else:
+                log(f"syn10 traffic: {t10['error']}")
             syn10["traffic"] = t10
         del h10
 
@@ -491,8 +589,11 @@ def main():
         roof["kernel_trace_top"] = {
             name.split("(")[0].replace("void ", "")[:60]: {"calls": c, "avg_us": round(a / 1e3, 3)}
             for name, (c, a) in sorted(prof["trace"].items(), key=lambda kv: -kv[1][0] * kv[1][1])[:8]}
-    t1 = traffic_of(prof.get("fetch"), prof.get("write"))
-    if t1:
+    t1 = traffic_of(prof.get("fetch"), prof.get("write")) if extras and not args.no_pmc else None
+    if t1 and "error" in t1:
+        log(f"headline traffic: {t1['error']}")
+        roof["traffic_error"] = t1["error"]
+    elif t1:
         roof["traffic"] = t1.pop("traffic")
         roof["traffic_detail"] = dict(t1, per_algorithmic_byte=round(roof["traffic"] / alg_bytes, 3),
             correction="traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide reads, "
@@ -500,6 +601,7 @@ def main():
                        "requests, Infinity-Cache hits included",
             source="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over tools/spmv_probe.py resident in this run")
 
+    strays = reap_strays()
     out = {
         "metric": "wall-clock to final cut (s) + cut size, ibm18.hgr; SpMV GB/s vs HBM peak",
         "value": round(sec_per_step, 6),
@@ -520,6 +622,7 @@ def main():
                    "parallelism": f"lanczos row-shard x{world} ({comm if world > 1 else 'single'}), KL 1 GPU"},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "parity": parity,
         "result": {"lambda1": last["lambda"], "lanczos_matvecs": last["lanczos"]["matvecs"],
                    "lanczos_restarts": last["lanczos"]["restarts"], "residual": last["lanczos"]["residual"],
                    "kl_iterations": last["kl"]["iterations"], "kl_loop_ms": round(last["kl"]["loop_ms"], 3),
@@ -534,6 +637,7 @@ def main():
         "e2e_fresh_breakdown": fresh_breakdown,
         "configs": subs,
         "syn10_sharded_lanczos": syn10,
+        "stray_processes_reaped": strays,
     }
     print(json.dumps(out), flush=True)
     ctx.close()

@@ -43,14 +43,15 @@ SWAP_DTYPE = np.dtype([("iter", "<u4"), ("node_left", "<u4"), ("node_right", "<u
 class LanczosOpts(ctypes.Structure):
     _fields_ = [("ncv", _I32), ("maxit", _I32), ("tol", ctypes.c_double), ("deflate", _I32),
                 ("time_spmv", _I32), ("reorth", _I32), ("check_every", _I32), ("basis32", _I32),
-                ("alpha_last", _I32), ("keep_min", _I32)]
+                ("alpha_last", _I32), ("keep_min", _I32), ("reorth_thresh", ctypes.c_double)]
 
 
 class LanczosStats(ctypes.Structure):
     _fields_ = [("restarts", _I32), ("matvecs", _I32), ("converged", _I32), ("residual", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double), ("spmv_timed", _I32),
                 ("comm_ms", ctypes.c_double), ("allgathers", _I32), ("allreduces", _I32),
-                ("update32_steps", _I32), ("update32_fallbacks", _I32)]
+                ("update32_steps", _I32), ("update32_fallbacks", _I32), ("projected_steps", _I32),
+                ("ortho_max", ctypes.c_double)]
 
 
 class KLResult(ctypes.Structure):
@@ -449,15 +450,18 @@ class Context:
         _chk(_lib.ek_spmv_bench(self._c, int(iters), 1 if fused else 0, ctypes.byref(us)), "spmv_bench")
         return us.value
 
-    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=1, check_every=8,
-                        basis32=True, alpha_last=False, keep_min=-1):
+    def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=3, check_every=8,
+                        basis32=True, alpha_last=False, keep_min=-1, reorth_thresh=0.0):
         """Fiedler pair (Spectra SymEigsSolver(nev=2, ncv=min(100,n/2)), cEIG.cpp:194-207).  check_every: steps
         between mid-cycle convergence tests after the first cycle (0: at cycle ends only, Spectra's schedule).
         basis32: the update reads the basis's fp32 shadow when that is exact to fp64 rounding (ek_lanczos_opts).
         alpha_last: the SpMV's last workgroup reduces alpha (default: every projection workgroup does).
-        keep_min: floor on the vectors an implicit restart keeps (-1: ncv/5, 0: Spectra's nev_adjusted alone)."""
+        keep_min: floor on the vectors an implicit restart keeps (-1: ncv/5, 0: Spectra's nev_adjusted alone).
+        reorth: 3 partial reorthogonalisation (Simon's omega recurrence, threshold reorth_thresh, <= 0:
+        1e-10), 1 full (every step), 2 CGS2."""
         o = LanczosOpts(int(ncv), int(maxit), float(tol), 1 if deflate else 0, 1 if time_spmv else 0, int(reorth),
-                        int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0, int(keep_min))
+                        int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0, int(keep_min),
+                        float(reorth_thresh))
         st = LanczosStats()
         lam = ctypes.c_double()
         v = np.empty(self.n, np.float64)
@@ -510,7 +514,7 @@ class Context:
 
     def solve_file(self, path, eig=1, seed=0, write_results=True, out_dir=None, limit=-1, sign_ref=None, ncv=0,
                    tol=1e-10, deflate=True, time_spmv=False, log_cap=0, check_every=8, basis32=True, alpha_last=False,
-                   keep_min=-1):
+                   keep_min=-1, reorth=3, reorth_thresh=0.0):
         """The whole path, .hgr -> results/ (ek_solve_file).  eig: 1 GPU Fiedler split (gKL2 -EIG), 2 the
         pre_saved_EIG file (cKL -EIG), 0 random split with std::mt19937(seed).  Returns (result dict, swap log)."""
         o = SolveOpts()
@@ -518,8 +522,9 @@ class Context:
         o.eig, o.seed, o.write_results, o.limit = int(eig), int(seed) & 0xFFFFFFFF, 1 if write_results else 0, int(limit)
         o.out_dir = os.fsencode(out_dir) if out_dir else None
         o.sign_ref = os.fsencode(sign_ref) if sign_ref else None
-        o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, 1,
-                                int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0, int(keep_min))
+        o.lanczos = LanczosOpts(int(ncv), 1000, float(tol), 1 if deflate else 0, 1 if time_spmv else 0, int(reorth),
+                                int(check_every), 1 if basis32 else 0, 1 if alpha_last else 0, int(keep_min),
+                                float(reorth_thresh))
         log = np.empty(max(int(log_cap), 1), SWAP_DTYPE)  # the library writes the first `iterations` records
         r = SolveResult()
         _chk(_lib.ek_solve_file(self._c, os.fsencode(path), ctypes.byref(o), _p(log), int(log_cap), ctypes.byref(r)),
@@ -528,6 +533,7 @@ class Context:
         out["lambda"] = r.lambda_
         out["lanczos"] = {k: getattr(r.lanczos, k) for k, _ in LanczosStats._fields_}
         out["kl"] = {k: getattr(r.kl, k) for k, _ in KLResult._fields_}
+        self.kl_n = r.nodes  # (kl_sides: the partition this solve left on the context)
         return out, log[: min(int(log_cap), r.kl.iterations)]
 
     def kl_sides(self, which):

@@ -15,6 +15,13 @@
 // on the GPU through the C-ABI; there is no CPU path.  Additive flags:
 //   --device D  --seed S (random init)  --sign-ref FILE  --no-deflate
 //   --ncv N  --tol T  --quiet
+//   --spectra            the Lanczos of the reference's Spectra SymEigsSolver
+//                        (cEIG.cpp:195-198): a full reorthogonalisation every
+//                        step, restarts keeping Spectra's nev_adjusted, fp64
+//                        basis reads (ek_lanczos_opts reorth 1, keep_min 0,
+//                        basis32 0); default: partial reorthogonalisation, the
+//                        ncv/5 restart floor and the fp32 basis shadow
+//   --reorth full|partial  only the reorthogonalisation rule
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -38,6 +45,8 @@ struct Opts {
     std::string tool, input;
     bool eig = false, quiet = false, have_seed = false, deflate = true, teardown = true;
     int device = 0, ncv = 0;
+    bool spectra = false;
+    int reorth = 0;  // 0: default (partial)
     double tol = 0.0;
     uint64_t seed = 0;
     std::string sign_ref;
@@ -110,6 +119,12 @@ ek_solve_opts solve_opts(const Opts& o) {
     so.lanczos.deflate = o.deflate ? 1 : 0;
     if (o.ncv > 0) so.lanczos.ncv = o.ncv;
     if (o.tol > 0) so.lanczos.tol = o.tol;
+    if (o.spectra) {  // Spectra SymEigsSolver's rule set
+        so.lanczos.reorth = 1;
+        so.lanczos.keep_min = 0;
+        so.lanczos.basis32 = 0;
+    }
+    if (o.reorth) so.lanczos.reorth = o.reorth;
     so.sign_ref = o.sign_ref.empty() ? nullptr : o.sign_ref.c_str();
     so.seed = o.have_seed ? uint32_t(o.seed) : std::random_device{}();  // cKL.cpp:179-180 when unseeded
     return so;
@@ -237,6 +252,13 @@ extern "C" int ek_cli_main_ex(const char* tool_c, int argc, char** argv, int fla
             else if (a == "--ncv") o.ncv = std::stoi(need("--ncv"));
             else if (a == "--tol") o.tol = std::stod(need("--tol"));
             else if (a == "--quiet") o.quiet = true;
+            else if (a == "--spectra") o.spectra = true;
+            else if (a == "--reorth") {
+                const std::string v = need("--reorth");
+                if (v == "full") o.reorth = 1;
+                else if (v == "partial") o.reorth = 3;
+                else throw Fail{"--reorth takes full or partial"};
+            }
             else pos.push_back(a);
         } catch (const Fail& e) {
             std::fprintf(stderr, "Error: %s\n", e.msg.c_str());

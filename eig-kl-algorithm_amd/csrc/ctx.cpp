@@ -134,6 +134,9 @@ struct ek_ctx {
     DBuf fbk;        // launches whose fp32-shadow update fell back to V (a device counter)
     DBuf actr;  // the SpMV's last-block counter (alpha hand-off), zero between launches
     DBuf gctr;  // the projection's column-group counters (k_gemvt hand-off), zero between launches
+    // partial reorthogonalisation (reorth 3): the SpMV's ||w||^2 partials, the
+    // omega ring (3 x OMEGA_LD), k_pro's state and its per-step decisions
+    DBuf wpart, omega, prost, pflags;
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
@@ -153,7 +156,8 @@ struct ek_ctx {
     hipStream_t cstream = nullptr;
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
     double* chk_pin = nullptr;
-    double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1))
+    double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1)), then the kept
+                              // projected matrix for k_pro (2 x (MAX_NCV + 2))
     // the last Fiedler vector as returned (normalised, sign fixed), kept on
     // the device for ek_kl_set_partition_fiedler, and that split's scratch
     DBuf fied, sp_sorted, sp_flag, sp_pos, sp_tmp;
@@ -964,11 +968,12 @@ void ek_lanczos_default_opts(ek_lanczos_opts* o) {
     o->tol = 1e-10;
     o->deflate = 1;
     o->time_spmv = 0;
-    o->reorth = 1;
+    o->reorth = 3;
     o->check_every = 8;
     o->basis32 = 1;
     o->alpha_last = 0;
     o->keep_min = -1;
+    o->reorth_thresh = 0.0;
 }
 
 }  // extern "C"
@@ -1035,6 +1040,11 @@ struct Lanczos {
     // the MALL would otherwise evict the matrix and x every pass
     bool nt = false;
     int u32_steps = 0;
+    // partial reorthogonalisation (reorth 3, single context): k_pro decides
+    // per step whether the projection and the update run (Simon's omega
+    // recurrence against thresh; eps1 = eps sqrt(n), its rounding term)
+    bool pro = false;
+    double pro_thresh = 0.0, pro_eps1 = 0.0;
     float* V32() { return b32 ? c->V32.as<float>() : nullptr; }
     float* col32(int j) { return b32 ? c->V32.as<float>() + size_t(j) * ldv : nullptr; }
     int seg0 = 0;  // first step of the current run of steps (cycle start or injected vector)
@@ -1153,7 +1163,12 @@ struct Lanczos {
         double* fn2 = c->fn2.as<double>();
         double* a3 = c->scal.as<double>() + 2;
         const double* bov = c->bov.as<double>();
-        const int upd_red = upd_reduces(nrb);
+        // (partial reorthogonalisation: a skipped step has no partials for
+        // every update workgroup to reduce, so the update_r form is not used)
+        const int upd_red = pro && upd_reduces(nrb) == 1 ? 0 : upd_reduces(nrb);
+        // ||f||^2 for the next SpMV from the update (or, on a skipped step, ||f'||^2)
+        double* fast = (b32 || pro) ? c->scal.as<double>() + 4 : nullptr;
+        const bool tt = tt_fused || pro;
         unsigned* gctr = upd_red == 2 ? c->gctr.as<unsigned>() : nullptr;
         double* hoff = upd_red == 2 ? c->h2.as<double>() : nullptr;
         for (int i = k; i < kend; ++i) {
@@ -1169,20 +1184,28 @@ struct Lanczos {
                 fin.a3 = a3;
                 fin.fn2_i = fn2 + i - 1;
                 fin.bov_i = bov + i - 1;
-                fin.fast = b32 ? c->scal.as<double>() + 4 : nullptr;  // the update's ||f||^2 (or NaN)
+                fin.fast = fast;  // the update's ||f||^2 (or NaN)
             }
+            if (pro) fin.wpart = c->wpart.as<double>();  // ||w||^2 partials for k_pro (also at i == seg0)
             const bool timed = spmv_timed_step(i);
             // the SpMV's last block also reduces alpha into a3 (k_three_term's bits)
             ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
-                          c->apart.as<double>(), i > seg0 ? &fin : nullptr,
+                          c->apart.as<double>(), (i > seg0 || pro) ? &fin : nullptr,
                           timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr,
-                          tt_fused && alpha_last ? a3 : nullptr, c->actr.as<unsigned>());
+                          !pro && tt_fused && alpha_last ? a3 : nullptr, c->actr.as<unsigned>());
             ++matvecs;
             const int nc = i + 1;
-            if (tt_fused) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
+            // partial reorthogonalisation: alpha, and whether this step projects
+            const int* flag = pro ? c->pflags.as<int>() + i : nullptr;
+            if (pro)
+                ek::dev::pro_step(s, c->apart.as<double>(), c->wpart.as<double>(), c->nrb_spmv, a3, fn2 + i, bov + i,
+                                  c->alpha.as<double>(), c->offd.as<double>(), c->omega.as<double>(),
+                                  c->prost.as<ek::dev::ProState>(), c->pflags.as<int>(), i, seg0, m, pro_thresh, pro_eps1);
+            if (tt) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
                                   i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
-                                  col32(i), alpha_last ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff, nt);
+                                  col32(i), (alpha_last || pro) ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff,
+                                  nt, flag);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
                                     i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), col32(i));
@@ -1192,17 +1215,17 @@ struct Lanczos {
             // (b32: ||f'||^2 rides along as one more column of the partials)
             unsigned* fb = b32 ? c->fbk.as<unsigned>() : nullptr;
             // (b32: the update also leaves ||f||^2 = ||f'||^2 - ||h||^2 for the next SpMV)
-            double* fast = b32 ? c->scal.as<double>() + 4 : nullptr;
             if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt, flag);
             } else if (upd_red == 1) {
                 ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
                                   c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
             } else {
-                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0 + (b32 ? 1 : 0), c->h2.as<double>());
+                ek::dev::reduce_cols(s, c->part.as<double>(), nrb, nc + has_u0 + ((b32 || pro) ? 1 : 0),
+                                     c->h2.as<double>());
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt, flag);
             }
             if (b32) ++u32_steps;
         }
@@ -1286,6 +1309,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     const int maxit = o.maxit > 0 ? o.maxit : 1000;
     const double eps23 = std::pow(std::numeric_limits<double>::epsilon(), 2.0 / 3.0);
     const bool trace = std::getenv("EK_LANCZOS_TRACE") != nullptr;
+    const bool ortho_check = std::getenv("EK_LANCZOS_ORTHO") != nullptr;
+    double ortho_max = 0.0;
 
     Lanczos L{};
     L.c = c;
@@ -1300,6 +1325,20 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.time_spmv = o.time_spmv != 0;
     L.reorth = o.reorth == 2 ? 2 : 1;
     hipStream_t s = c->stream;
+    // reorth 3: partial reorthogonalisation on the single-context step (the
+    // sharded and CGS2 steps always project).  EK_REORTH=1|3 overrides (A/B).
+    int reorth_mode = o.reorth;
+    if (const char* e = std::getenv("EK_REORTH"); e && e[0]) reorth_mode = std::atoi(e);
+    L.pro = reorth_mode == 3 && c->nranks == 1 && std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
+    // threshold 1e-10, not Simon's sqrt(eps): across implicit restarts the
+    // kept Ritz block carries the basis's loss of orthogonality into the next
+    // cycle, and the dropped projection coefficients (O(threshold) beta) stay
+    // in the Lanczos relation.  tools/pro_model.py on ibm10 (15 restarts):
+    // sqrt(eps) -> max|V^T V - I| 1e-7, residual 2e-9, lambda off by 5e-10;
+    // 1e-9 -> 3e-8, 1.4e-9; 1e-10 -> 1.4e-10, 1.9e-10 (full: 5e-14, 1e-12),
+    // 44 % of the steps projected; the headline LCC 32 %, residual unchanged
+    L.pro_thresh = o.reorth_thresh > 0 ? o.reorth_thresh : 1e-10;
+    L.pro_eps1 = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
 
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);
@@ -1342,13 +1381,18 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     c->apart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
     c->Qd.ensure(size_t(m) * size_t(m + 1) * 8);
     c->scal.ensure(64);
-    if (!c->actr.p) {
-        c->actr.ensure((ek::dev::ALPHA_SUB + 1) * 256);
-        HIPCHK(hipMemsetAsync(c->actr.p, 0, c->actr.bytes, s));
-    }
-    if (!c->gctr.p) {
-        c->gctr.ensure(size_t(ek::dev::GT_HANDOFF_UINTS) * 4);
-        HIPCHK(hipMemsetAsync(c->gctr.p, 0, c->gctr.bytes, s));
+    // the hand-off counters are zero between launches; re-armed here too, so a
+    // launch that died part-way cannot leave them out of step for this solve
+    c->actr.ensure((ek::dev::ALPHA_SUB + 1) * 256);
+    HIPCHK(hipMemsetAsync(c->actr.p, 0, c->actr.bytes, s));
+    c->gctr.ensure(size_t(ek::dev::GT_HANDOFF_UINTS) * 4);
+    HIPCHK(hipMemsetAsync(c->gctr.p, 0, c->gctr.bytes, s));
+    if (L.pro) {
+        c->wpart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
+        c->omega.ensure(3 * size_t(ek::dev::OMEGA_LD) * 8);
+        c->prost.ensure(sizeof(ek::dev::ProState));
+        c->pflags.ensure(size_t(m + 2) * 4);
+        HIPCHK(hipMemsetAsync(c->prost.p, 0, sizeof(ek::dev::ProState), s));
     }
     // padded rows must be exactly 0 (only those: every kernel writes real
     // rows before it reads them, and no kernel writes a padded row nonzero)
@@ -1366,7 +1410,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 3 * size_t(ek::dev::MAX_NCV + 2) * 8,
                              hipHostMallocDefault));
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
-                             size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) * 8, hipHostMallocDefault));
+                             (size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) + 2 * size_t(ek::dev::MAX_NCV + 2)) * 8,
+                             hipHostMallocDefault));
     }
     if (L.time_spmv) {  // created once per context: ~200 creations per solve cost milliseconds
         while (c->spmv_ev.size() < size_t(2 * m)) {
@@ -1549,6 +1594,19 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             break;
         }
         if (++restarts >= maxit) break;
+        // EK_LANCZOS_ORTHO=1 (tests): max |[V u0]^T [V u0] - I| over the
+        // cycle's basis at every restart (one projection per column)
+        if (ortho_check && c->nranks == 1) {
+            std::vector<double> hh(size_t(m + L.has_u0));
+            for (int j = 0; j < m; ++j) {
+                ek::dev::gemvt(s, L.ldv, L.nrb, L.V(), m, L.has_u0, L.u0val, L.nreal, L.col(j), c->part.as<double>());
+                ek::dev::reduce_cols(s, c->part.as<double>(), L.nrb, m + L.has_u0, c->h1.as<double>());
+                HIPCHK(hipMemcpyAsync(hh.data(), c->h1.p, hh.size() * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                for (int q = 0; q < m + L.has_u0; ++q)
+                    ortho_max = std::max(ortho_max, std::fabs(hh[size_t(q)] - (q == j ? 1.0 : 0.0)));
+            }
+        }
         // implicit restart with the m-knew unwanted Ritz values as shifts
         // (a fixed restart size of 8, 12 or 20 kept vectors, or a cap of 10-30,
         // was no better over ibm01 / industry2 / ibm10 / the 1x synthetic and
@@ -1593,7 +1651,16 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             std::swap(c->V32.p, c->Vn32.p);
             std::swap(c->V32.bytes, c->Vn32.bytes);
         }
-        HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read
+        if (L.pro) {  // the kept projected matrix, for k_pro's omega recurrence (alpha[j], offd[j] of j < knew)
+            double* kp = c->q_pin + size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1);
+            for (int i = 0; i < knew; ++i) kp[i] = dd[size_t(i)];
+            for (int i = 1; i < knew; ++i) kp[knew + i] = ee[size_t(i - 1)];
+            HIPCHK(hipMemcpyAsync(c->alpha.p, kp, size_t(knew) * 8, hipMemcpyHostToDevice, s));
+            if (knew > 1)
+                HIPCHK(hipMemcpyAsync(c->offd.as<double>() + 1, kp + knew + 1, size_t(knew - 1) * 8,
+                                      hipMemcpyHostToDevice, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read (and k_pro's staging)
         for (int i = 0; i < knew; ++i) d[size_t(i)] = dd[size_t(i)];
         for (int i = 0; i + 1 < knew; ++i) e[size_t(i)] = ee[size_t(i)];
         k = knew;
@@ -1684,6 +1751,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         stats->allreduces = int32_t(c->n_ar);
         stats->update32_steps = L.u32_steps;
         stats->update32_fallbacks = 0;
+        stats->projected_steps = L.matvecs;  // every step projects unless partial reorthogonalisation ran
+        stats->ortho_max = ortho_max;
+        if (L.pro) {
+            ek::dev::ProState ps{};
+            HIPCHK(hipMemcpyAsync(&ps, c->prost.p, sizeof(ps), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            stats->projected_steps = ps.projected;
+        }
         if (L.b32) {
             unsigned fbn = 0;
             HIPCHK(hipMemcpyAsync(&fbn, c->fbk.p, 4, hipMemcpyDeviceToHost, c->stream));

@@ -166,6 +166,10 @@ struct StepFin {
     // ||f||^2 from the update (||f'||^2 - ||h||^2, k_update B32) when not
     // NaN; NaN: summed from npart
     const double* fast = nullptr;
+    // partial reorthogonalisation: the block's partial of ||w||^2 (w = the
+    // scaled product) beside its alpha partial, for k_pro's estimate of
+    // beta_{i+1}.  Read whether or not npart is set.
+    double* wpart = nullptr;
 };
 
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
@@ -317,7 +321,8 @@ void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, d
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col = nullptr, const double* apart = nullptr,
-              int nparts = 0, unsigned* gctr = nullptr, double* h_out = nullptr, bool nt = false);
+              int nparts = 0, unsigned* gctr = nullptr, double* h_out = nullptr, bool nt = false,
+              const int* flag = nullptr);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 
@@ -333,7 +338,27 @@ void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, do
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32 = nullptr,
-            unsigned* fb = nullptr, double* fn2_fast = nullptr, bool nt = false);
+            unsigned* fb = nullptr, double* fn2_fast = nullptr, bool nt = false, const int* flag = nullptr);
+// Partial reorthogonalisation (Lanczos reorth 3; one workgroup per step,
+// between the SpMV and the projection): alpha = sum(apart) (k_three_term's
+// order: the bits every other alpha path gives) -> *a3; beta_{i+1} estimated
+// as sqrt(||w||^2 - alpha^2 - beta_i^2); Simon's omega recurrence (PROPACK
+// update_mu) for the next vector against v_0..v_i and u0 from the two
+// previous rows of the ring `omega` (3 rows of OMEGA_LD) and the projected
+// matrix (alpha[j], offd[j] for j < i: final; the kept ones uploaded after a
+// restart); flags[i] = 1 when max |omega| > thresh or the step is forced (the
+// first step of a run, the step after a triggered one, the cycle's last step,
+// an estimate lost to cancellation).  The projection and the update of the
+// step read flags[i] (0: f = f', no pass over the basis).
+constexpr int OMEGA_LD = MAX_NCV + 8;  // ring row: [0, MAX_NCV) basis columns, [MAX_NCV] u0
+struct ProState {
+    double anorm;   // running estimate of ||L|| (max |alpha_j| + beta_j + beta_{j+1})
+    int force;      // the next step projects (the second of a pair)
+    int projected;  // steps that projected, this solve
+};
+void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,
+              const double* bov_i, const double* alpha, const double* offd, double* omega, ProState* st, int* flags,
+              int i, int seg0, int m, double thresh, double eps1);
 // fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
 // alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
 // alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]

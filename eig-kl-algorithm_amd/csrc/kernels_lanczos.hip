@@ -127,6 +127,59 @@ constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (co
 // each row block also writes ||rhs||^2 over its rows to part column
 // ncols + has_u0 (the update's accuracy test reads the sum), and with TT
 // the fp32 copy of v_i to v32col (vi rows are loaded here anyway).
+// The end of a projection launch for a step that does not project (k_pro):
+// column group 0 only.  The block's ||f'||^2 partial goes to column tot (the
+// update's accuracy test and the next SpMV's ||f||^2 read its sum); the
+// column sums h are zero (no correction of H: the finalize adds h[i], h[i-1]).
+// With the hand-off the workgroup completing column group 0 writes them; else
+// (k_reduce_cols sums the partials) this block's partials of columns i and
+// i-1, the two the finalize reads, are zeroed.
+__device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, int rbk, int t,
+                                                double* __restrict__ part, const double* nred,
+                                                unsigned* __restrict__ gctr, double* __restrict__ h_out) {
+    const int tot = ncols + has_u0, i = ncols - 1;
+    __syncthreads();  // nred complete
+    const double nb = (nred[0] + nred[1]) + (nred[2] + nred[3]);
+    if (!h_out) {
+        if (t == 0) part[size_t(tot) * nrb + rbk] = nb;
+        if (t == 1) part[size_t(i) * nrb + rbk] = 0.0;
+        if (t == 2 && i > 0) part[size_t(i - 1) * nrb + rbk] = 0.0;
+        return;
+    }
+    __shared__ int s_last;
+    if (t == 0) {
+        st_sc1(part + size_t(tot) * nrb + rbk, nb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int g = rbk % GT_SUB;
+        const unsigned gsize = unsigned((nrb - g + GT_SUB - 1) / GT_SUB), ngroups = unsigned(nrb < GT_SUB ? nrb : GT_SUB);
+        int last = 0;
+        if (__hip_atomic_fetch_add(gctr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
+            last = __hip_atomic_fetch_add(gctr + GT_SUB * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   ngroups - 1u;
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int j = t; j < tot; j += 256) h_out[j] = 0.0;
+    // the norm column in col_sum2's order (8 lanes, every 8th block, xor tree)
+    if (t < CS_LANES) {
+        const double* pc = part + size_t(tot) * nrb;
+        constexpr int CB = 32;
+        double a = 0.0;
+        for (int b0 = t; b0 < nrb; b0 += CS_LANES * CB) {
+            double va[CB];
+#pragma unroll
+            for (int u = 0; u < CB; ++u) va[u] = ld_sc1(pc + min(b0 + CS_LANES * u, nrb - 1));
+#pragma unroll
+            for (int u = 0; u < CB; ++u) a += b0 + CS_LANES * u < nrb ? va[u] : 0.0;
+        }
+#pragma unroll
+        for (int o = 1; o < CS_LANES; o <<= 1) a += __shfl_xor(a, o, 64);
+        if (t == 0) h_out[tot] = a;
+    }
+    if (t < GT_SUB + 1) gctr[t * 64] = 0u;  // re-armed (column group 0's counters)
+}
+
 template <bool TT, bool NT, int APE = 12>
 __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
@@ -136,7 +189,7 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
                                                double* __restrict__ fp, int nrm, float* __restrict__ v32col,
                                                const double* __restrict__ apart, int nparts,
                                                double* __restrict__ alpha_pub, unsigned* __restrict__ gctr,
-                                               double* __restrict__ h_out) {
+                                               double* __restrict__ h_out, const int* __restrict__ flag) {
     __shared__ double red[4][GT_COLS];
     __shared__ double nred[4];
     __shared__ double lds4[4];
@@ -146,6 +199,11 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
     const int v = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
     const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
+    // partial reorthogonalisation (k_pro's decision for this step, uniform
+    // over the launch): a step that does not project only forms f' and its
+    // ||f'||^2 partials (column group 0); the other column groups have no work
+    const bool skip = flag && *flag == 0;
+    if (skip && j0 != 0) return;
     double acc[GT_COLS];
 #pragma unroll
     for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
@@ -175,9 +233,11 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
             tv[k] = *reinterpret_cast<const double2*>(vi + r);
             tu[k] = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
         }
+        if (!skip) {
 #pragma unroll
-        for (int jj = 0; jj < GT_COLS; ++jj)
-            vs[k][jj] = ld_basis<NT>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+            for (int jj = 0; jj < GT_COLS; ++jj)
+                vs[k][jj] = ld_basis<NT>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+        }
     }
     if constexpr (TT) {  // k_three_term's f' (same operations, same order)
         // apart != null: alpha = sum of the SpMV's per-block partials, reduced
@@ -227,6 +287,10 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
         for (int k = 0; k < KR; ++k) s += xs[k].x * xs[k].x + xs[k].y * xs[k].y;
         s = wave_sum(s);
         if ((t & 63) == 0) nred[t >> 6] = s;
+    }
+    if (skip) {
+        gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr, h_out);
+        return;
     }
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -519,7 +583,18 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
                                                 const double* __restrict__ src, double* __restrict__ dst,
                                                 double* __restrict__ npart, const double* __restrict__ part, int nrb,
                                                 double* __restrict__ h_out, const float* __restrict__ V32,
-                                                unsigned* __restrict__ fb, double* __restrict__ fn2_fast) {
+                                                unsigned* __restrict__ fb, double* __restrict__ fn2_fast,
+                                                const int* __restrict__ flag) {
+    // partial reorthogonalisation: a step k_pro left unprojected keeps f = f'
+    // (the projection kernel stored it); ||f||^2 = ||f'||^2 (h[tot]) for the
+    // next SpMV
+    if (flag && *flag == 0) {
+        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = h[ncols + has_u0];
+        return;
+    }
+    if constexpr (!B32) {  // the next SpMV sums this launch's ||f||^2 partials
+        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = __builtin_nan("");
+    }
     constexpr int UB = EK_UPD_UB;
     constexpr int UB32 = 2 * EK_UPD_UB;  // fp32 columns per batch: the same bytes in flight
     constexpr int UBX = B32 ? UB32 : UB;
@@ -784,6 +859,91 @@ __global__ __launch_bounds__(256) void k_finalize_step(const double* __restrict_
     }
 }
 
+// Partial reorthogonalisation: the decision for step i (ek_internal.hpp
+// pro_step).  Simon's omega recurrence (Simon 1984; PROPACK's update_mu) for
+// omega_{i+1,j} ~ v_{i+1}^T v_j:
+//   beta_{i+1} omega_{i+1,j} = beta_{j+1} omega_{i,j+1} + (alpha_j - alpha_i) omega_{i,j}
+//                              + beta_j omega_{i,j-1} - beta_i omega_{i-1,j}  (+- eps1 ||L||)
+// with omega_{k,k} = 1; against u0 (L u0 = 0) the same with alpha_j = 0 and no
+// neighbours.  beta_{i+1} is not known before the projection kernel forms f',
+// so it is estimated from ||w||^2 - alpha^2 - beta_i^2 (w = L v_i, v_i and
+// v_{i-1} orthonormal to far better than the threshold); a step whose
+// estimate cancels below 2^-20 ||w||^2 projects.  One workgroup; thread j < i
+// owns omega_{i+1,j}, thread 255 the u0 entry.
+__global__ __launch_bounds__(256) void k_pro(const double* __restrict__ apart, const double* __restrict__ wpart,
+                                             int nparts, double* __restrict__ a3, const double* __restrict__ fn2_i,
+                                             const double* __restrict__ bov_i, const double* __restrict__ alpha,
+                                             const double* __restrict__ offd, double* __restrict__ omega,
+                                             ProState* __restrict__ st, int* __restrict__ flags, int i, int seg0, int m,
+                                             double thresh, double eps1) {
+    __shared__ double lds4[4];
+    __shared__ double sh[4];
+    __shared__ double mx4[4];
+    __shared__ int s_pair, s_forced;
+    const int t = int(threadIdx.x);
+    constexpr int U = MAX_NCV;  // the u0 entry of a ring row
+    double* onew = omega + size_t((i + 1) % 3) * OMEGA_LD;       // omega_{i+1}
+    double* ocur = omega + size_t(i % 3) * OMEGA_LD;             // omega_i
+    const double* oprev = omega + size_t((i + 2) % 3) * OMEGA_LD;  // omega_{i-1}
+    // alpha in k_three_term's order (the bits of every other alpha path), ||w||^2 alike
+    const double sa = block_sum256(strided_sum256(apart, nparts), lds4);
+    const double sw = block_sum256(strided_sum256(wpart, nparts), lds4);
+    if (t == 0) {
+        const double a = sa;
+        *a3 = a;
+        const double b = i > 0 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
+        const double b2 = sw - a * a - b * b;
+        const bool valid = b2 > 0x1p-20 * sw;  // false for NaN
+        const double bn = valid ? sqrt(b2) : 0.0;
+        const double an = fmax(st->anorm, fabs(a) + b + bn);
+        st->anorm = an;
+        const int pair = st->force || i == seg0;  // the first step of a run starts a pair like a triggered one
+        sh[0] = a;
+        sh[1] = b;
+        sh[2] = bn;
+        sh[3] = an;
+        s_pair = pair;
+        s_forced = pair || i == m - 1 || !valid;  // (the cycle's last step: f_m orthogonal for the restart)
+    }
+    __syncthreads();
+    const double a = sh[0], b = sh[1], bn = sh[2], an = sh[3];
+    const bool forced = s_forced != 0;
+    double nv = 0.0;
+    if (!forced) {
+        if (t < i) {
+            const int j = t;
+            double x = j + 1 < i ? offd[j + 1] * ocur[j + 1] : b;  // (omega_{i,i} = 1)
+            x += (alpha[j] - a) * ocur[j];
+            if (j > 0) x += offd[j] * ocur[j - 1];
+            x -= b * (j < i - 1 ? oprev[j] : 1.0);  // (omega_{i-1,i-1} = 1)
+            nv = (x + copysign(eps1 * an, x)) / bn;
+        } else if (t == 255) {
+            const double x = -a * ocur[U] - b * oprev[U];
+            nv = (x + copysign(eps1 * an, x)) / bn;
+        }
+    }
+    double mx = fabs(nv);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((t & 63) == 0) mx4[t >> 6] = mx;
+    __syncthreads();
+    const double mxa = fmax(fmax(mx4[0], mx4[1]), fmax(mx4[2], mx4[3]));
+    const bool d = forced || !(mxa <= thresh);  // (NaN: project)
+    // after a projection the next vector is orthogonal to rounding: omega = eps1
+    if (t < i) onew[t] = d ? eps1 : nv;
+    if (t == i) onew[i] = eps1;
+    if (t == 255) onew[U] = d ? eps1 : nv;
+    if (i == seg0) {  // omega_i of a run's first vector (a restart's kept basis, an injected vector)
+        if (t < i) ocur[t] = eps1;
+        if (t == 255) ocur[U] = eps1;
+    }
+    if (t == 0) {
+        flags[i] = d ? 1 : 0;
+        st->force = (d && !s_pair) ? 1 : 0;
+        if (d) st->projected += 1;
+    }
+}
+
 // Three-term recurrence f' = w - alpha v_i - beta_i v_{i-1}, alpha = sum of the
 // SpMV's per-block partials (nparts > 0: every block reduces them itself, in
 // the same fixed order, so no extra launch; nparts == 0: alpha precomputed,
@@ -932,23 +1092,23 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
     if (nt)
         hipLaunchKernelGGL((k_gemvt<false, true>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
-                           h_out);
+                           h_out, nullptr);
     else
         hipLaunchKernelGGL((k_gemvt<false, false>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
-                           h_out);
+                           h_out, nullptr);
 }
 
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
-              unsigned* gctr, double* h_out, bool nt) {
+              unsigned* gctr, double* h_out, bool nt, const int* flag) {
     const int cols = ncols + has_u0;
     const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS));
 #define EK_GEMVT_TT(NT_, APE_)                                                                                    \
     hipLaunchKernelGGL((k_gemvt<true, NT_, APE_>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, \
-                       part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, v32col ? 1 : 0, v32col, apart,     \
-                       nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out)
+                       part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, (v32col || flag) ? 1 : 0, v32col, \
+                       apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out, flag)
     const bool wide = apart && nparts > 12 * 256;  // 24 partials a thread (up to 6,144; beyond: strided_sum256)
     if (nt) {
         if (wide) EK_GEMVT_TT(true, 24);
@@ -986,19 +1146,19 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
     hipLaunchKernelGGL((k_update<RED, B32, NT>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, __VA_ARGS__)
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32, unsigned* fb,
-            double* fn2_fast, bool nt) {
+            double* fn2_fast, bool nt, const int* flag) {
     if (V32 && nt)
         EK_UPDATE_LAUNCH(false, true, true, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0, nullptr,
-                         V32, fb, fn2_fast);
+                         V32, fb, fn2_fast, flag);
     else if (V32)
         EK_UPDATE_LAUNCH(false, true, false, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
-                         nullptr, V32, fb, fn2_fast);
+                         nullptr, V32, fb, fn2_fast, flag);
     else if (nt)
         EK_UPDATE_LAUNCH(false, false, true, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
-                         nullptr, nullptr, nullptr, nullptr);
+                         nullptr, nullptr, nullptr, flag ? fn2_fast : nullptr, flag);
     else
         EK_UPDATE_LAUNCH(false, false, false, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
-                         nullptr, nullptr, nullptr, nullptr);
+                         nullptr, nullptr, nullptr, flag ? fn2_fast : nullptr, flag);
 }
 
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
@@ -1006,16 +1166,16 @@ void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, do
               const float* V32, unsigned* fb, double* fn2_fast, bool nt) {
     if (V32 && nt)
         EK_UPDATE_LAUNCH(true, true, true, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, V32, fb, fn2_fast);
+                         h_out, V32, fb, fn2_fast, nullptr);
     else if (V32)
         EK_UPDATE_LAUNCH(true, true, false, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, V32, fb, fn2_fast);
+                         h_out, V32, fb, fn2_fast, nullptr);
     else if (nt)
         EK_UPDATE_LAUNCH(true, false, true, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, nullptr, nullptr, nullptr);
+                         h_out, nullptr, nullptr, nullptr, nullptr);
     else
         EK_UPDATE_LAUNCH(true, false, false, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, nullptr, nullptr, nullptr);
+                         h_out, nullptr, nullptr, nullptr, nullptr);
 }
 #undef EK_UPDATE_LAUNCH
 
@@ -1023,6 +1183,13 @@ void finalize_step(hipStream_t s, const double* npart, int nb, double* fn2_out, 
                    int step, double* alpha, double* offd, const double* a3, const double* fn2_i, const double* bov_i) {
     hipLaunchKernelGGL(k_finalize_step, dim3(1), dim3(256), 0, s, npart, nb, fn2_out, h1, h2, step, alpha, offd, a3,
                        fn2_i, bov_i);
+}
+
+void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,
+              const double* bov_i, const double* alpha, const double* offd, double* omega, ProState* st, int* flags,
+              int i, int seg0, int m, double thresh, double eps1) {
+    hipLaunchKernelGGL(k_pro, dim3(1), dim3(256), 0, s, apart, wpart, nparts, a3, fn2_i, bov_i, alpha, offd, omega, st,
+                       flags, i, seg0, m, thresh, eps1);
 }
 
 void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,

@@ -318,7 +318,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
         }
     }
     const double scale = (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0;
-    double av = 0.0;
+    double av = 0.0, wv = 0.0;
     for (int r = t; r < nr; r += PT) {
         const double yr = acc[r] * scale;
         y[r0 + r] = yr;
@@ -326,11 +326,16 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
             const double v = f[r0 + r] * scale;
             vcol[r0 + r] = v;
             av += v * yr;
+            wv += yr * yr;
         }
     }
     if (apart) {
         const double s = panel_block_sum(av, wsum);
         if (t == 0) panel_store_sc1(apart + w, s);
+        if (fin.wpart) {  // ||w||^2 partial (partial reorthogonalisation's beta estimate)
+            const double q = panel_block_sum(wv, wsum);
+            if (t == 0) fin.wpart[w] = q;
+        }
     }
     if (alpha_out) {  // kernels_spmv.hip alpha_handoff: the last workgroup reduces alpha
         if (t == 0) {

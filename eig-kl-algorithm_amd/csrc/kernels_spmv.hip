@@ -146,6 +146,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     __shared__ int rbeg[SPMV_THREADS + 1];
     __shared__ double yrow[SPMV_THREADS];
     __shared__ double wsum[SPMV_THREADS / 64];
+    __shared__ double wsum2[SPMV_THREADS / 64];
     __shared__ int s_last;
     const int t = threadIdx.x;
     uint32_t wd[PER];
@@ -206,6 +207,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
                 const double v = f[r0] * scale;
                 vcol[r0] = v;
                 if (apart) store_sc1(apart + blockIdx.x, v * (a * scale));
+                if (fin.wpart) fin.wpart[blockIdx.x] = (a * scale) * (a * scale);
             }
         }
         if (alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
@@ -262,19 +264,28 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     }
     // basis column + alpha partial: thread t owns row t (its f was prefetched)
     if (vcol) {
-        double av = 0.0;
+        double av = 0.0, wv = 0.0;
         if (apart) __syncthreads();  // yrow complete
         if (t < nr) {
             const double v = fr * scale;
             vcol[r0 + t] = v;
-            if (apart) av = v * yrow[t];
+            if (apart) {
+                av = v * yrow[t];
+                wv = yrow[t] * yrow[t];
+            }
         }
         if (apart) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) av += __shfl_xor(av, o, 64);
             if ((t & 63) == 0) wsum[t >> 6] = av;
+            if (fin.wpart) {  // ||w||^2 partial (partial reorthogonalisation's beta estimate)
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) wv += __shfl_xor(wv, o, 64);
+                if ((t & 63) == 0) wsum2[t >> 6] = wv;
+            }
             __syncthreads();
             if (t == 0) store_sc1(apart + blockIdx.x, (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]));
+            if (t == 0 && fin.wpart) fin.wpart[blockIdx.x] = (wsum2[0] + wsum2[1]) + (wsum2[2] + wsum2[3]);
         }
     }
     if (alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);

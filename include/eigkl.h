@@ -199,8 +199,14 @@ typedef struct {
     int32_t deflate;    /* 1 (default): deflate the constant null vector, nev=1;
                            0: Spectra-equivalent nev=2, Fiedler = 2nd smallest */
     int32_t time_spmv;  /* 1: bracket every SpMV launch with HIP events (stats) */
-    int32_t reorth;     /* 1 (default): three-term recurrence + one full classical
-                           Gram-Schmidt pass; 2: CGS2 (twice) from the matvec */
+    int32_t reorth;     /* 3 (default): partial reorthogonalisation — the three-term
+                           recurrence, and the full classical Gram-Schmidt pass of 1
+                           only on the steps Simon's omega recurrence asks for (loss of
+                           orthogonality estimate > reorth_thresh), the step after each,
+                           every cycle's first and last step (single context; sharded
+                           steps always project); 1: that pass on every step
+                           (Spectra's full reorthogonalisation); 2: CGS2 (twice) from
+                           the matvec; 0: as 1 */
     int32_t check_every; /* after the first restart cycle, test Spectra's convergence
                             criterion on the projected matrix every this many steps
                             (and stop there) instead of at cycle ends only; 0: cycle
@@ -215,6 +221,10 @@ typedef struct {
     int32_t keep_min;    /* implicit restarts keep at least this many vectors (floor on
                             Spectra's nev_adjusted, which on these Laplacians often keeps
                             2-4: DESIGN.md); < 0 (default): ncv / 5; 0: Spectra's rule */
+    double reorth_thresh; /* reorth 3: project when the estimated |v_{i+1}^T v_j| exceeds
+                             this; <= 0 (default): 1e-10 (Simon's
+                             sqrt(DBL_EPSILON) lets the loss compound across implicit
+                             restarts) */
 } ek_lanczos_opts;
 
 typedef struct {
@@ -230,6 +240,8 @@ typedef struct {
     int32_t allreduces;   /* one of each per Lanczos step, plus restarts/injections/end) */
     int32_t update32_steps;     /* steps whose update was enqueued with the fp32 shadow */
     int32_t update32_fallbacks; /* ... of which took the fp64 basis (the accuracy test failed) */
+    int32_t projected_steps;    /* steps that ran the Gram-Schmidt pass (= matvecs unless reorth 3) */
+    double ortho_max;           /* EK_LANCZOS_ORTHO=1: max |[V u0]^T [V u0] - I| at the restarts */
 } ek_lanczos_stats;
 
 void ek_lanczos_default_opts(ek_lanczos_opts* o);

@@ -269,6 +269,38 @@ def test_lanczos_golden(ek, ctx, name, deflate, reorth):
 
 
 @pytest.mark.parametrize("name", ["fract", "ibm01", "industry2", "ibm10"])
+def test_lanczos_partial_reorth_vs_full(ek, ctx, monkeypatch, name):
+    """Partial reorthogonalisation (reorth=3, the default; k_pro: Simon's
+    omega recurrence) against the full Gram-Schmidt pass on every step
+    (reorth=1, Spectra's rule, cEIG.cpp:195-198): fewer projected steps, the
+    basis orthonormal to 1e-8 at every restart (max |[V u0]^T [V u0] - I|,
+    EK_LANCZOS_ORTHO), lambda within 1e-10 of the full run, the matvec count
+    within 5 %, and both held to the reference's pre_saved_EIG tolerances
+    (ibm10's golden is unconverged: residual and the converged lambda)."""
+    h = ek.Hypergraph.read(circuit_path(name))
+    L = h.laplacian()
+    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    monkeypatch.setenv("EK_LANCZOS_ORTHO", "1")
+    lam_p, v_p, st_p = ctx.lanczos_fiedler()
+    lam_f, v_f, st_f = ctx.lanczos_fiedler(reorth=1)
+    print(name, {k: st_p[k] for k in ("matvecs", "projected_steps", "restarts", "ortho_max", "residual")},
+          {k: st_f[k] for k in ("matvecs", "projected_steps", "ortho_max")})
+    assert st_p["converged"] and st_p["residual"] < 1e-9 and st_f["residual"] < 1e-9
+    assert st_f["projected_steps"] == st_f["matvecs"]
+    assert st_p["projected_steps"] < st_p["matvecs"]
+    assert st_p["ortho_max"] <= 1e-8 and st_f["ortho_max"] <= 1e-12
+    assert abs(lam_p - lam_f) <= 1e-10
+    assert st_p["matvecs"] <= 1.05 * st_f["matvecs"] + 8
+    v_f = v_f * np.sign(v_p @ v_f)
+    assert np.abs(v_p - v_f).max() <= 1e-8
+    if name != "ibm10":
+        lam_ref, med_ref, bits_ref, v_ref, _, _ = ek.eig_read(eig_path(name), h.nodes)
+        _fiedler_parity(name, lam_p, v_p, lam_ref, med_ref, bits_ref, v_ref, ek)
+    else:
+        assert abs(lam_p - 0.0185035852) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["fract", "ibm01", "industry2", "ibm10"])
 def test_lanczos_midcycle_check_same_split_as_end_of_cycle(ek, ctx, name):
     """The mid-cycle convergence test (check_every > 0) may stop a cycle early
     and take the Ritz pair from a j < ncv projection; check_every=0 is
@@ -329,8 +361,11 @@ def test_lanczos_basis32_update_golden(ek, ctx, name, deflate):
     h = ek.Hypergraph.read(circuit_path(name))
     L = h.laplacian()
     ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
-    lam_a, v_a, st_a = ctx.lanczos_fiedler(deflate=deflate, basis32=True)
-    lam_b, v_b, st_b = ctx.lanczos_fiedler(deflate=deflate, basis32=False)
+    # (reorth=1: every step projects, h is the O(eps) loss of orthogonality;
+    # under partial reorthogonalisation the projecting steps carry a loss of
+    # up to the threshold and mostly take the fp64 basis)
+    lam_a, v_a, st_a = ctx.lanczos_fiedler(deflate=deflate, basis32=True, reorth=1)
+    lam_b, v_b, st_b = ctx.lanczos_fiedler(deflate=deflate, basis32=False, reorth=1)
     assert st_a["converged"] and st_a["residual"] < 1e-9 and st_b["residual"] < 1e-9
     assert st_a["update32_steps"] == st_a["matvecs"] and st_b["update32_steps"] == 0
     assert st_a["update32_fallbacks"] == 0, st_a
@@ -350,15 +385,21 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
     mult, seed = {"syn0.25": (0.25, 3), "syn2": (2.0, 2), "syn1": (1.0, 1)}[which]
     h = ek.Hypergraph.generate(mult, seed)
     ctx.spmv_setup_pins(h)
-    lam, v, st = ctx.lanczos_fiedler()
+    lam, v, st = ctx.lanczos_fiedler(reorth=1)
     assert st["converged"] and st["residual"] < 1e-8 and abs(lam) < 1e-8
     assert np.all(np.isfinite(v)) and abs(np.linalg.norm(v) - 1) < 1e-10
     assert st["update32_steps"] == st["matvecs"] and st["update32_fallbacks"] <= 0.01 * st["matvecs"], st
+    # the default, partial reorthogonalisation, through the same breakdowns
+    lam, v, st = ctx.lanczos_fiedler()
+    assert st["converged"] and st["residual"] < 1e-8 and abs(lam) < 1e-8
+    assert np.all(np.isfinite(v)) and abs(np.linalg.norm(v) - 1) < 1e-10
+    assert 0 < st["projected_steps"] < st["matvecs"], st
 
 
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
 @pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_ALPHA_LAST=1", "EK_UPD_RED=0", "EK_UPD_RED=1",
-                                    "EK_UPD_RED=2", "EK_V_NT=1"])
+                                    "EK_UPD_RED=2", "EK_V_NT=1", "pro:EK_UPD_RED=0", "pro:EK_UPD_RED=2",
+                                    "pro:EK_V_NT=1"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
@@ -371,7 +412,11 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     * the basis passes' non-temporal loads (EK_V_NT=1; the default above 768
       MB of basis) against plain ones.
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
-    syn2 through restarts whose residual collapses."""
+    syn2 through restarts whose residual collapses.  These run the full
+    reorthogonalisation (EK_REORTH=1); "pro:" switches hold the partial one
+    (the default) to the same rule: the skipped steps' paths (the projection's
+    norm-only hand-off or its zeroed partials under k_reduce_cols, the
+    update's early exit) give the same bits whichever form runs."""
     import subprocess
     import sys
     gen = {"ibm01": "ek.Hypergraph.read(circuit_path('ibm01'))", "syn0.25": "ek.Hypergraph.generate(0.25, 3)",
@@ -382,6 +427,11 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
         "np.save(sys.argv[1], np.concatenate([[lam, st['matvecs'], st['residual']], v]))"
     ) % (os.path.dirname(os.path.abspath(__file__)), gen)
     env = dict(os.environ)
+    if switch.startswith("pro:"):
+        switch = switch[4:]
+        env["EK_REORTH"] = "3"
+    else:
+        env["EK_REORTH"] = "1"
     a, b = str(tmp_path / "new.npy"), str(tmp_path / "old.npy")
     subprocess.run([sys.executable, "-c", code, a], check=True, timeout=180, env=env)
     k, v = switch.split("=")

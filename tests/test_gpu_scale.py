@@ -157,6 +157,66 @@ def test_lcc_fiedler_and_kl_vs_reference(ek, oracle, ctx, name, mult):
     assert res["iterations"] == meta["reference_run"]["iterations"]
 
 
+def test_lcc_partial_reorth_vs_full(ek, ctx, monkeypatch):
+    """The headline LCC under partial reorthogonalisation (the default) and
+    the full Gram-Schmidt pass on every step (reorth=1): lambda within 1e-10,
+    the matvec count within 5 %, the basis orthonormal to 1e-8 at every
+    restart, and the same median split as the reference run on every node."""
+    d = os.path.join(GOLD, "syn115_lcc")
+    meta = json.load(open(os.path.join(d, "meta.json")))
+    h, _ = ek.Hypergraph.generate(1.15, 1).largest_component()
+    L = h.laplacian()
+    ctx.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+    monkeypatch.setenv("EK_LANCZOS_ORTHO", "1")
+    lam_p, v_p, st_p = ctx.lanczos_fiedler()
+    lam_f, v_f, st_f = ctx.lanczos_fiedler(reorth=1)
+    print({k: st_p[k] for k in ("matvecs", "projected_steps", "restarts", "ortho_max", "residual")},
+          {k: st_f[k] for k in ("matvecs", "restarts", "ortho_max", "residual")})
+    assert st_p["projected_steps"] < 0.5 * st_p["matvecs"]
+    assert st_p["ortho_max"] <= 1e-8
+    assert abs(lam_p - lam_f) <= 1e-10 and abs(lam_p - meta["lambda1"]) <= 1e-10
+    assert st_p["matvecs"] <= 1.05 * st_f["matvecs"]
+    bits_ref = np.unpackbits(np.load(os.path.join(d, "split_bits.npy")))[:h.nodes]
+    for v in (v_p, v_f):
+        _, bits = ek.median_split(v)
+        assert np.array_equal(bits, bits_ref)
+
+
+def test_headline_solve_file_vs_reference(ek, tmp_path):
+    """bench.py's timed call itself: ek_solve_file -EIG on
+    the 211,813-node headline LCC with its OWN Fiedler vector, the device
+    median split (odd n: the median is one entry, cEIG.cpp:55-65, 204-209) and
+    no sign reference.  Its split must equal the reference run's split on
+    EVERY node, including the near-median ones, and its results file must be
+    the real cKL's on that split (cKL.cpp:436-444)."""
+    d = os.path.join(GOLD, "syn115_lcc")
+    meta = json.load(open(os.path.join(d, "meta.json")))
+    h, _ = ek.Hypergraph.generate(1.15, 1).largest_component()
+    n = h.nodes
+    assert (n, h.nets) == (meta["nodes"], meta["nets"])
+    p = str(tmp_path / "syn1.15x_seed1_lcc.hgr")
+    h.write(p)
+    bits_ref = np.unpackbits(np.load(os.path.join(d, "split_bits.npy")))[:n]
+    c = ek.Context(0)
+    try:
+        r, _ = c.solve_file(p, eig=1, out_dir=str(tmp_path), log_cap=n // 2)
+        sides = c.kl_sides(0)  # the initial partition the device split produced
+    finally:
+        c.close()
+    near = np.zeros(n, bool)
+    near[meta["near_median_nodes"]] = True
+    diff = sides != bits_ref
+    print(f"headline split: {int(diff.sum())} nodes differ ({int((diff & near).sum())} of {int(near.sum())} "
+          f"near-median), median {r['median']!r} vs {meta['median']!r}, lambda {r['lambda']!r}, "
+          f"{r['lanczos']['matvecs']} matvecs, {r['kl']['iterations']} swaps")
+    assert abs(r["lambda"] - meta["lambda1"]) <= 1e-10
+    assert not diff.any(), f"{int(diff.sum())} nodes on the other side of the reference split"
+    ref = gzip.open(os.path.join(d, "ref_results.txt.gz"), "rt").read()
+    mine = (tmp_path / "results" / "syn1.15x_seed1_lcc.hgr_KL_CutSize_EIG_output.txt").read_text()
+    compare_results_text(mine, ref)
+    assert r["kl"]["iterations"] == meta["reference_run"]["iterations"] == 19853
+
+
 @pytest.mark.parametrize("name,seed", [("fract", 1), ("fract", 7), ("fract", 12345), ("ibm01", 1)])
 def test_cli_random_init_matches_seeded_reference(tmp_path, name, seed):
     """configs[0]: `cKL <c>.hgr --seed S` = the reference's random branch
