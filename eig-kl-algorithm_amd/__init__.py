@@ -51,7 +51,7 @@ class LanczosStats(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double), ("spmv_timed", _I32),
                 ("comm_ms", ctypes.c_double), ("allgathers", _I32), ("allreduces", _I32),
                 ("update32_steps", _I32), ("update32_fallbacks", _I32), ("projected_steps", _I32),
-                ("ortho_max", ctypes.c_double)]
+                ("reprojected", _I32), ("ortho_max", ctypes.c_double)]
 
 
 class KLResult(ctypes.Structure):

@@ -101,6 +101,10 @@ struct ek_ctx {
     // RCCL, or the host-staged exchange of ek_comm_init_host
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // the sharded layout and exchange (slot-padded all-gather, the one-all-
+    // reduce step): nranks > 1, or a forced 1-rank communicator (EK_COMM_FORCE,
+    // which runs the RCCL production path on one GPU: tests)
+    bool mr = false;
     ek_allgather_fn host_ag = nullptr;
     ek_allreduce_fn host_ar = nullptr;
     void* host_user = nullptr;
@@ -121,6 +125,7 @@ struct ek_ctx {
     std::vector<int64_t> shard_off;
     int64_t slot = 0;
     DBuf off_d, xexp;
+    DBuf spx;  // ek_spmv's x in the all-gather layout (sharded), sized when the shard map is set
     // the column-panel form of the SpMV (pn_G > 0; kernels_panel.hip)
     int pn_G = 0, pn_P = 0, pn_pb = 0, pn_max_rows = 0, pn_ndict = 0;
     DBuf pn_wrow, pn_start, pn_word, pn_rid;
@@ -137,6 +142,7 @@ struct ek_ctx {
     // partial reorthogonalisation (reorth 3): the SpMV's ||w||^2 partials, the
     // omega ring (3 x OMEGA_LD), k_pro's state and its per-step decisions
     DBuf wpart, omega, prost, pflags;
+    DBuf cflag;  // the sharded step's cancellation flags (update_mr), one double per step
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
@@ -260,7 +266,7 @@ namespace {
 // stream.  RCCL: enqueued on the stream.  Host-staged: stream drained, the
 // operand staged through pinned memory around the caller's collective.
 void allreduce(ek_ctx* c, double* p, size_t count) {
-    if (c->nranks <= 1 || !count) return;
+    if (!c->mr || !count) return;
     ++c->n_ar;
     if (c->comm) {
         NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, c->comm, c->stream));
@@ -301,6 +307,13 @@ void comm_reset(ek_ctx* c) {
     c->host_user = nullptr;
     c->nranks = 1;
     c->rank = 0;
+    c->mr = false;
+}
+
+// EK_COMM_FORCE=1: a 1-rank communicator still takes the multi-rank path
+bool comm_forced() {
+    const char* e = std::getenv("EK_COMM_FORCE");
+    return e && e[0] && e[0] != '0';
 }
 
 }  // namespace
@@ -398,13 +411,15 @@ int ek_comm_init(ek_ctx* c, int nranks, int rank, const void* id128) {
     check_ctx(c);
     if (nranks < 1 || rank < 0 || rank >= nranks || !id128) ek::fail(EK_EINVAL, "ek_comm_init: bad argument");
     comm_reset(c);
-    if (nranks > 1) {
+    const bool mr = nranks > 1 || comm_forced();
+    if (mr) {  // (nranks 1 under EK_COMM_FORCE: a real one-rank RCCL communicator)
         ncclUniqueId id;
         std::memcpy(&id, id128, sizeof id);
         NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
     }
     c->nranks = nranks;
     c->rank = rank;
+    c->mr = mr;
     c->n = 0;  // the shard map changed: ek_spmv_setup again
     return EK_OK;
     EK_CATCH
@@ -413,11 +428,13 @@ int ek_comm_init(ek_ctx* c, int nranks, int rank, const void* id128) {
 int ek_comm_init_host(ek_ctx* c, int nranks, int rank, ek_allgather_fn ag, ek_allreduce_fn ar, void* user) {
     EK_TRY
     check_ctx(c);
-    if (nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && (!ag || !ar)))
+    const bool mr = nranks > 1 || comm_forced();
+    if (nranks < 1 || rank < 0 || rank >= nranks || (mr && (!ag || !ar)))
         ek::fail(EK_EINVAL, "ek_comm_init_host: bad argument");
     comm_reset(c);
     c->nranks = nranks;
     c->rank = rank;
+    c->mr = mr;
     c->host_ag = ag;
     c->host_ar = ar;
     c->host_user = user;
@@ -445,14 +462,17 @@ void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
     c->shard_off = off;
     c->row0 = off[size_t(c->rank)];
     c->nrows = off[size_t(c->rank) + 1] - c->row0;
-    c->nloc = c->nranks > 1 ? mx : n;
+    c->nloc = c->mr ? mx : n;
     // sharded: the Lanczos vectors' rows (ldv) + 64, the rank's ||f||^2 at [ldv]
-    c->slot = c->nranks > 1 ? gt_round(mx) + 64 : n;
-    if (c->nranks > 1 && c->slot * c->nranks > INT32_MAX) ek::fail(EK_EINVAL, "sharded vector layout exceeds int32");
+    c->slot = c->mr ? gt_round(mx) + 64 : n;
+    if (c->mr && c->slot * c->nranks > INT32_MAX) ek::fail(EK_EINVAL, "sharded vector layout exceeds int32");
+    // (allocated here, not inside ek_spmv: a reallocation there could free
+    // memory that work queued earlier still reads)
+    if (c->mr) c->spx.ensure(size_t(c->slot * c->nranks) * 8);
 }
 
 // The column space the SpMV reads: global ids, or the padded all-gather layout
-int64_t x_extent(const ek_ctx* c) { return c->nranks > 1 ? c->slot * c->nranks : c->n; }
+int64_t x_extent(const ek_ctx* c) { return c->mr ? c->slot * c->nranks : c->n; }
 
 // The column-panel form when x outgrows an XCD's L2 (EK_SPMV_PANEL=0/1 forces
 // it off/on; default: x > 8 MB, the 10x synthetic.  At 2x (3.2 MB) the two
@@ -538,7 +558,7 @@ void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, cons
     for (int64_t p = 0; p < nnz; ++p)
         if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup: column %d out of range", col[p]);
     std::vector<int32_t> colx;  // sharded: the columns in the all-gather layout
-    if (c->nranks > 1) {
+    if (c->mr) {
         remap_cols_host(c, col, nnz, colx);
         col = colx.data();
     }
@@ -620,7 +640,7 @@ int ek_spmv_setup(ek_ctx* c, int64_t n, int64_t row0, int64_t nrows, const int32
     if (n <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > n || !rowptr || (nrows && (!col || !val)))
         ek::fail(EK_EINVAL, "ek_spmv_setup: bad argument");
     std::vector<int64_t> off{0, n};
-    if (c->nranks > 1) {
+    if (c->mr) {
         c->scal.ensure(64);
         c->xexp.ensure(size_t(2 * c->nranks) * 8);
         const double mine[2] = {double(row0), double(nrows)};
@@ -673,7 +693,7 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
     // identically on every rank (no collective)
     std::vector<int64_t> off(size_t(c->nranks) + 1, 0);
     off[1] = n;
-    if (c->nranks > 1) {
+    if (c->mr) {
         const int rc = ek_shard_map(n, nets, net_ptr, pins, c->nranks, off.data());
         if (rc != EK_OK) throw ek::Error{rc};
     }
@@ -776,7 +796,7 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
     c->n = n;
     c->nnz = nnz;
     const std::vector<long long> offll(off.begin(), off.end());  // (alive until the stream is drained below)
-    if (c->nranks > 1) {  // global columns -> the all-gather layout (monotone: rows stay sorted)
+    if (c->mr) {  // global columns -> the all-gather layout (monotone: rows stay sorted)
         upload(c->off_d, offll.data(), offll.size(), s);
         ek::dev::remap_cols(s, nnz, c->col.as<int>(), c->off_d.as<long long>(), c->nranks, c->slot);
     }
@@ -852,22 +872,24 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
 }
 
 // x is the global n-vector; a sharded context reads it through its padded
-// all-gather layout, so the ranks' slices are copied into that first
+// all-gather layout, so the ranks' slices are copied into that first (into a
+// buffer of its own, not the solve's scratch: one ek_spmv at a time per
+// sharded context, on any stream)
 int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
     EK_TRY
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv before ek_spmv_setup");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     const double* xs = x;
-    if (c->nranks > 1) {
-        c->xexp.ensure(size_t(x_extent(c)) * 8);
+    if (c->mr) {
+        if (c->spx.bytes < size_t(x_extent(c)) * 8) ek::fail(EK_ESTATE, "ek_spmv: shard layout not set up");
         for (int r = 0; r < c->nranks; ++r) {
             const int64_t a = c->shard_off[size_t(r)], b = c->shard_off[size_t(r) + 1];
             if (b > a)
-                HIPCHK(hipMemcpyAsync(c->xexp.as<double>() + r * c->slot, x + a, size_t(b - a) * 8,
+                HIPCHK(hipMemcpyAsync(c->spx.as<double>() + r * c->slot, x + a, size_t(b - a) * 8,
                                       hipMemcpyDeviceToDevice, s));
         }
-        xs = c->xexp.as<double>();
+        xs = c->spx.as<double>();
     }
     ek::dev::spmv(s, spmv_mat(c), xs, y, nullptr, nullptr, nullptr, nullptr);
     HIPCHK(hipGetLastError());
@@ -881,7 +903,7 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_host before ek_spmv_setup");
     DBuf dx, dy;
     std::vector<double> xp;  // sharded: the padded all-gather layout
-    if (c->nranks > 1) {
+    if (c->mr) {
         xp.assign(size_t(x_extent(c)), 0.0);
         for (int r = 0; r < c->nranks; ++r)
             std::copy(x + c->shard_off[size_t(r)], x + c->shard_off[size_t(r) + 1], xp.begin() + r * c->slot);
@@ -902,7 +924,7 @@ int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_bench before ek_spmv_setup");
     if (iters <= 0 || !avg_us) ek::fail(EK_EINVAL, "ek_spmv_bench: bad argument");
-    if (c->nranks > 1) ek::fail(EK_EINVAL, "ek_spmv_bench: single-context measurement");
+    if (c->mr) ek::fail(EK_EINVAL, "ek_spmv_bench: single-context measurement");
     hipStream_t s = c->stream;
     const size_t n = size_t(c->n);
     DBuf x, y, vcol, apart, fn2;
@@ -1013,7 +1035,7 @@ struct Lanczos {
     // x for the matvec: the full vector (gathered when sharded, in the padded
     // slot layout the matrix's columns were remapped to)
     const double* gather_f() {
-        if (c->nranks == 1) return c->f.as<double>();
+        if (!c->mr) return c->f.as<double>();
         allgather(c, c->f.as<double>(), size_t(c->slot), c->xfull.as<double>());
         return c->xfull.as<double>();
     }
@@ -1054,7 +1076,7 @@ struct Lanczos {
         // EK_LANCZOS_UNFUSED: run the sharded step sequence on one GPU (tests)
         static const bool unfused = std::getenv("EK_LANCZOS_UNFUSED") != nullptr;
         if (reorth == 1) {
-            if (c->nranks == 1 && !unfused) return factorize_fused(k, kend);
+            if (!c->mr && !unfused) return factorize_fused(k, kend);
             return factorize_mr(k, kend);
         }
         double* fn2 = c->fn2.as<double>();
@@ -1102,7 +1124,7 @@ struct Lanczos {
     void factorize_mr(int k, int kend) {
         double* fn2 = c->fn2.as<double>();
         double* f = c->f.as<double>();
-        const bool sharded = c->nranks > 1;
+        const bool sharded = c->mr;
         for (int i = k; i < kend; ++i) {
             ek::dev::finalize_step(s, c->npart.as<double>(), nub, f + ldv, nullptr, nullptr, -1, nullptr, nullptr);
             const double* x = f;
@@ -1122,11 +1144,13 @@ struct Lanczos {
             const int nc = i + 1, tot = nc + has_u0;
             ek::dev::gemvt3(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), col(i),
                             i > 0 ? col(i - 1) : col(i), c->part.as<double>());
-            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, 3 * tot, c->h2.as<double>());
-            allreduce(c, c->h2.as<double>(), size_t(3 * tot));
+            // (+ ||w||^2: the cancellation test of update_mr)
+            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, 3 * tot + 1, c->h2.as<double>());
+            allreduce(c, c->h2.as<double>(), size_t(3 * tot + 1));
             ek::dev::update_mr(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->w.as<double>(), col(i),
                                i > 0 ? col(i - 1) : nullptr, fn2 + i, c->bov.as<double>() + i, f,
-                               c->npart.as<double>(), c->alpha.as<double>(), c->offd.as<double>());
+                               c->npart.as<double>(), c->alpha.as<double>(), c->offd.as<double>(),
+                               c->cflag.as<double>(), mr_cancel);
         }
         if (kend == m) reduce_scalar(fn2 + m);  // the cycle's last residual norm
         HIPCHK(hipGetLastError());
@@ -1235,6 +1259,54 @@ struct Lanczos {
         HIPCHK(hipGetLastError());
     }
 
+    // The sharded step projects f' by linearity (V^T f' = V^T w - alpha V^T v_i
+    // - beta V^T v_{i-1}), exact to eps ||w||.  When f' cancelled (update_mr's
+    // cflag: ||f'||^2 < mr_cancel ||w||^2, near an invariant subspace) that is
+    // not small against ||f'||, and v_{j1} = f_{j1}/||f_{j1}|| would carry a
+    // loss of orthogonality of eps ||w|| / beta_{j1}.  The driver sees the flag
+    // at its next check and re-projects: f = v_{j1} (unit; or f_m itself at
+    // the cycle's end, j1 == m) against V[:, :j1] and u0 — one more CGS pass,
+    // the CGS2 path's second pass — with Spectra's H += V^T f correction
+    // (scaled by beta_{j1}: f_{j1} = beta_{j1} v_{j1}) and T(j1, j1-1) =
+    // beta_{j1} ||f|| through the beta override; the cycle continues at j1.
+    // beta_j1: sqrt(fn2[j1]) as the run left it (host copy); returns the
+    // corrections (h[j1-1], h[j1-2]) to add to the host's T.
+    std::pair<double, double> repair(int j1, double beta_j1) {
+        double* f = c->f.as<double>();
+        double* fn2 = c->fn2.as<double>();
+        const double sc = j1 < m ? beta_j1 : 1.0;
+        if (j1 < m) HIPCHK(hipMemcpyAsync(f, col(j1), size_t(ldv) * 8, hipMemcpyDeviceToDevice, s));
+        ek::dev::gemvt(s, ldv, nrb, V(), j1, has_u0, u0val, nreal, f, c->part.as<double>());
+        ek::dev::reduce_cols(s, c->part.as<double>(), nrb, j1 + has_u0, c->h1.as<double>());
+        allreduce(c, c->h1.as<double>(), size_t(j1 + has_u0));
+        ek::dev::update(s, ldv, V(), j1, has_u0, u0val, nreal, c->h1.as<double>(), f, f, c->npart.as<double>());
+        reduce_scalar(fn2 + j1);
+        double hh[2] = {0.0, 0.0}, n2 = 0.0;
+        HIPCHK(hipMemcpyAsync(hh, c->h1.as<double>() + std::max(j1 - 2, 0), size_t(std::min(j1, 2)) * 8,
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&n2, fn2 + j1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const double h1 = sc * (j1 >= 2 ? hh[1] : hh[0]), h2 = j1 >= 2 ? sc * hh[0] : 0.0;  // h[j1-1], h[j1-2]
+        // device T entries (the host's are corrected by the caller)
+        double a = 0.0, o = 0.0;
+        HIPCHK(hipMemcpyAsync(&a, c->alpha.as<double>() + j1 - 1, 8, hipMemcpyDeviceToHost, s));
+        if (j1 >= 2) HIPCHK(hipMemcpyAsync(&o, c->offd.as<double>() + j1 - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        a += h1;
+        o += h2;
+        HIPCHK(hipMemcpyAsync(c->alpha.as<double>() + j1 - 1, &a, 8, hipMemcpyHostToDevice, s));
+        if (j1 >= 2) HIPCHK(hipMemcpyAsync(c->offd.as<double>() + j1 - 1, &o, 8, hipMemcpyHostToDevice, s));
+        if (j1 < m) {
+            const double bo = beta_j1 * std::sqrt(std::max(0.0, n2));
+            HIPCHK(hipMemcpyAsync(c->bov.as<double>() + j1, &bo, 8, hipMemcpyHostToDevice, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));  // (host operands)
+        ++repairs;
+        return {h1, h2};
+    }
+    int repairs = 0;
+    double mr_cancel = 0x1p-20;
+
     // Invariant subspace found at step j1-1 (||f|| collapsed, as on a graph
     // with several components): continue the sequence from a fresh random
     // vector orthogonal to V[:, :j1] and u0, with H(j1, j1-1) = 0 — Spectra's
@@ -1259,7 +1331,10 @@ struct Lanczos {
     }
 
     // pinned slot i of the mid-cycle checks: alpha[m], offd[m], fn2[m]
-    double* chk_slot(int i) { return c->chk_pin + size_t(i) * 3 * size_t(ek::dev::MAX_NCV + 2); }
+    // (four regions: alpha, offd, fn2 at m-based offsets; the sharded step's
+    // cancellation flags at CHK_FLAGS)
+    static constexpr size_t CHK_FLAGS = 3 * size_t(ek::dev::MAX_NCV + 2);
+    double* chk_slot(int i) { return c->chk_pin + size_t(i) * 4 * size_t(ek::dev::MAX_NCV + 2); }
 
     // The SpMV's kernel timestamps are taken on every 4th step of a cycle: a
     // launch with timing events costs the host ~7 us more, which the timed
@@ -1329,7 +1404,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // sharded and CGS2 steps always project).  EK_REORTH=1|3 overrides (A/B).
     int reorth_mode = o.reorth;
     if (const char* e = std::getenv("EK_REORTH"); e && e[0]) reorth_mode = std::atoi(e);
-    L.pro = reorth_mode == 3 && c->nranks == 1 && std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
+    L.pro = reorth_mode == 3 && !c->mr && std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
     // threshold 1e-10, not Simon's sqrt(eps): across implicit restarts the
     // kept Ritz block carries the basis's loss of orthogonality into the next
     // cycle, and the dropped projection coefficients (O(threshold) beta) stay
@@ -1350,7 +1425,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         const char* e = std::getenv(k);
         return e && e[0] ? e[0] != '0' : dflt;
     };
-    L.b32 = env_or("EK_BASIS32", o.basis32 != 0) && c->nranks == 1 && L.reorth == 1 &&
+    L.b32 = env_or("EK_BASIS32", o.basis32 != 0) && !c->mr && L.reorth == 1 &&
             std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
     L.alpha_last = env_or("EK_ALPHA_LAST", o.alpha_last != 0);
     // non-temporal basis passes once the fp64 basis exceeds 768 MB (3x the
@@ -1366,10 +1441,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         HIPCHK(hipMemsetAsync(c->fbk.p, 0, 4, c->stream));
     }
     // f: + 64 (the sharded step's all-gather slot carries the rank's ||f||^2 at [ldv])
-    if (c->nranks > 1 && c->slot != int64_t(ldv) + 64) ek::fail(EK_ESTATE, "shard slot %lld != ldv + 64", (long long)c->slot);
+    if (c->mr && c->slot != int64_t(ldv) + 64) ek::fail(EK_ESTATE, "shard slot %lld != ldv + 64", (long long)c->slot);
     c->f.ensure((ldv + 64) * 8);
     c->w.ensure(ldv * 8);
-    if (c->nranks > 1) c->xfull.ensure(size_t(c->slot) * size_t(c->nranks) * 8);
+    if (c->mr) c->xfull.ensure(size_t(c->slot) * size_t(c->nranks) * 8);
     c->part.ensure(3 * size_t(m + 2) * size_t(L.nrb) * 8);  // x 3: gemvt3 (sharded step)
     c->h1.ensure(size_t(m + 2) * 8);
     c->h2.ensure(3 * size_t(m + 2) * 8);
@@ -1400,14 +1475,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     ek::dev::zero_pad_rows(s, c->Vn.as<double>(), L.ldv, L.nreal, m + 1);
     HIPCHK(hipMemsetAsync(c->w.p, 0, c->w.bytes, s));
     HIPCHK(hipMemsetAsync(c->f.p, 0, c->f.bytes, s));
-    if (c->nranks > 1) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
+    if (c->mr) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
     if (!c->cstream) {  // mid-cycle check resources, created once per context
         HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
         for (int i = 0; i < 2; ++i) {
             HIPCHK(hipEventCreateWithFlags(&c->chk_done[i], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&c->chk_copied[i], hipEventDisableTiming));
         }
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 3 * size_t(ek::dev::MAX_NCV + 2) * 8,
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 4 * size_t(ek::dev::MAX_NCV + 2) * 8,
                              hipHostMallocDefault));
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
                              (size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) + 2 * size_t(ek::dev::MAX_NCV + 2)) * 8,
@@ -1457,8 +1532,15 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         for (int i = 0; i < m; ++i) a = std::max(a, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
         return a;
     };
+    // the sharded step's re-projection of a cancelled f' (Lanczos::repair)
+    const bool mr_step = c->mr && L.reorth == 1;
+    if (mr_step) {
+        c->cflag.ensure(size_t(m + 2) * 8);
+        if (const char* e = std::getenv("EK_MR_CANCEL"); e && e[0]) L.mr_cancel = std::atof(e);  // (tests)
+    }
     for (;;) {
         HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
+        if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));
         const auto tc = std::chrono::steady_clock::now();
         int cycle_breakdowns = 0;  // bounded per cycle: each one moves the factorisation forward
         int from = k;
@@ -1472,6 +1554,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             L.inject(k, ++injected);
         }
         int jconv = -1;  // > 0: converged on the projected matrix of the first jconv steps (mid-cycle check)
+        double beta_r = 0.0;  // ||f_jr|| as the run left it (a re-projection's scale)
         for (;;) {
             L.seg0 = from;
             // After the first cycle the cycle is enqueued in chunks; the host
@@ -1488,7 +1571,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             const int chunk = (restarts > 0 && o.check_every > 0)
                                   ? std::max({2, int(o.check_every), int(std::ceil(500.0 / (12.0 + 2.3e-4 * double(n))))})
                                   : m;
-            int a = from, launched = from, j1 = -1;
+            int a = from, launched = from, j1 = -1, jr = -1;  // breakdown / re-projection at
             int pend = -1, pend_slot = 0, slot = 0;
             while (a < m) {
                 const int b = std::min(m, a + chunk);
@@ -1502,6 +1585,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                     HIPCHK(hipMemcpyAsync(pinned, c->alpha.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
                     HIPCHK(hipMemcpyAsync(pinned + m, c->offd.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
                     HIPCHK(hipMemcpyAsync(pinned + 2 * m, c->fn2.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                    if (mr_step)
+                        HIPCHK(hipMemcpyAsync(pinned + L.CHK_FLAGS, c->cflag.p, size_t(b) * 8, hipMemcpyDeviceToHost,
+                                              c->cstream));
                     HIPCHK(hipEventRecord(c->chk_copied[slot], c->cstream));
                     cur = b - 1;  // complete: alpha, offd of steps < b - 1 (the fused finalize lags one step), fn2 <= b - 1
                 }
@@ -1517,7 +1603,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                     for (int i = 0; i < j; ++i) an = std::max(an, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
                     for (int i = std::max(from, 1); i <= j && j1 < 0; ++i)
                         if (!(std::sqrt(std::max(0.0, pa[2 * m + i])) > beta_eps * an)) j1 = i;
-                    if (j1 >= 0) break;
+                    for (int i = from; mr_step && i < j && jr < 0; ++i)
+                        if (pa[L.CHK_FLAGS + size_t(i)] != 0.0) {
+                            jr = i + 1;
+                            beta_r = std::sqrt(std::max(0.0, pa[2 * m + jr]));
+                        }
+                    if (j1 >= 0 || jr >= 0) break;
                     if (!ek::tridiag_eig(j, d.data(), e.data(), theta.data(), zl.data(), nullptr))
                         ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
                     const double fj = std::sqrt(std::max(0.0, pa[2 * m + j]));
@@ -1539,7 +1630,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             }
             L.collect_spmv_times(launched);
             if (jconv > 0) break;
-            if (j1 < 0) {  // the whole cycle ran: its projected matrix and residuals (pinned slot 0:
+            if (j1 < 0 && jr < 0) {  // the whole cycle ran: its projected matrix and residuals (pinned slot 0:
                            // no check copy is in flight at the cycle's end)
                 double* pin0 = L.chk_slot(0);
                 HIPCHK(hipMemcpyAsync(pin0, c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
@@ -1559,14 +1650,38 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                         j1 = i;
                         break;
                     }
-                if (j1 < 0) break;
+                if (mr_step && j1 < 0) {
+                    std::vector<double> cf(static_cast<size_t>(m));
+                    HIPCHK(hipMemcpyAsync(cf.data(), c->cflag.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipStreamSynchronize(s));
+                    for (int i = from; i < m && jr < 0; ++i)
+                        if (cf[size_t(i)] != 0.0) {
+                            jr = i + 1;
+                            beta_r = std::sqrt(std::max(0.0, fn2_h[size_t(jr)]));
+                        }
+                }
+                if (j1 < 0 && jr < 0) break;
             } else {
-                HIPCHK(hipStreamSynchronize(s));  // the chunk launched beyond the breakdown
+                HIPCHK(hipStreamSynchronize(s));  // the chunk launched beyond the breakdown / cancellation
             }
-            if (trace) std::fprintf(stderr, "[lanczos] breakdown at step %d\n", j1);
-            if (++cycle_breakdowns > m) ek::fail(EK_ENOCONV, "Lanczos: repeated breakdown within one cycle");
-            L.inject(j1, ++injected);
-            from = j1;
+            if (j1 >= 0 && (jr < 0 || j1 <= jr)) {
+                if (trace) std::fprintf(stderr, "[lanczos] breakdown at step %d\n", j1);
+                if (++cycle_breakdowns > m) ek::fail(EK_ENOCONV, "Lanczos: repeated breakdown within one cycle");
+                L.inject(j1, ++injected);
+                from = j1;
+            } else {
+                if (trace) std::fprintf(stderr, "[lanczos] cancelled f' at step %d: re-projected\n", jr - 1);
+                const auto corr = L.repair(jr, beta_r);
+                d[size_t(jr - 1)] += corr.first;
+                if (jr >= 2) e[size_t(jr - 2)] += corr.second;
+                HIPCHK(hipMemsetAsync(c->cflag.as<double>() + jr - 1, 0, 8, s));
+                if (jr == m) {  // f_m re-projected in place: the cycle's residual norm again
+                    HIPCHK(hipMemcpyAsync(&fn2_h[size_t(m)], c->fn2.as<double>() + m, 8, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipStreamSynchronize(s));
+                    break;
+                }
+                from = jr;
+            }
         }
         if (jconv > 0) {
             HIPCHK(hipStreamSynchronize(s));
@@ -1596,11 +1711,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         if (++restarts >= maxit) break;
         // EK_LANCZOS_ORTHO=1 (tests): max |[V u0]^T [V u0] - I| over the
         // cycle's basis at every restart (one projection per column)
-        if (ortho_check && c->nranks == 1) {
+        if (ortho_check) {
             std::vector<double> hh(size_t(m + L.has_u0));
             for (int j = 0; j < m; ++j) {
                 ek::dev::gemvt(s, L.ldv, L.nrb, L.V(), m, L.has_u0, L.u0val, L.nreal, L.col(j), c->part.as<double>());
                 ek::dev::reduce_cols(s, c->part.as<double>(), L.nrb, m + L.has_u0, c->h1.as<double>());
+                allreduce(c, c->h1.as<double>(), size_t(m + L.has_u0));  // (sharded: each rank's rows)
                 HIPCHK(hipMemcpyAsync(hh.data(), c->h1.p, hh.size() * 8, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
                 for (int q = 0; q < m + L.has_u0; ++q)
@@ -1694,7 +1810,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     double* y = c->pin + n;
     double* xg = xloc;   // the vector as the SpMV reads it
     double* xc = xloc;   // ... and contiguous over the global rows
-    if (c->nranks > 1) {  // the padded slot layout, then compacted
+    if (c->mr) {  // the padded slot layout, then compacted
         allgather(c, xloc, size_t(c->slot), c->xfull.as<double>());
         xg = c->xfull.as<double>();
         c->xexp.ensure(size_t(n) * 8);
@@ -1719,7 +1835,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         const double t = (y[i] - lambda * v[c->row0 + i]) * inv;
         r2 += t * t;
     }
-    if (c->nranks > 1) {
+    if (c->mr) {
         double* sc = c->scal.as<double>();
         HIPCHK(hipMemcpyAsync(sc, &r2, 8, hipMemcpyHostToDevice, s));
         allreduce(c, sc, 1);
@@ -1752,6 +1868,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         stats->update32_steps = L.u32_steps;
         stats->update32_fallbacks = 0;
         stats->projected_steps = L.matvecs;  // every step projects unless partial reorthogonalisation ran
+        stats->reprojected = L.repairs;
         stats->ortho_max = ortho_max;
         if (L.pro) {
             ek::dev::ProState ps{};

@@ -301,17 +301,20 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
            int nreal, const double* w, double* part, int nrm = 0, unsigned* gctr = nullptr, double* h_out = nullptr,
            bool nt = false);
 // the sharded step (ctx.cpp factorize_mr): part for three vectors w, va, vb at
-// once, part[(k*tot + j)*nrb + b], tot = ncols + has_u0
+// once, part[(k*tot + j)*nrb + b], tot = ncols + has_u0, and ||w||^2 partials
+// at part[3*tot*nrb + b]
 void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* w, const double* va, const double* vb, double* part);
 // hall = the all-reduced column sums of gemvt3 (3 x tot): alpha = hall[i],
 // h = hall[0:tot] - alpha hall[tot:2tot] - beta hall[2tot:3tot] (i = ncols-1),
 // dst = w - alpha vi - beta vim1 - V h - u0 h[ncols] (+ ||dst||^2 partials);
-// block 0 writes alpha[i] = alpha + h[i] and offd[i] = beta_i + h[i-1].
+// block 0 writes alpha[i] = alpha + h[i] and offd[i] = beta_i + h[i-1], and
+// cflag[i] = 1.0 when ||f'||^2 < cancel ||w||^2 (hall[3*tot] = ||w||^2).
 // beta = sqrt(*fn2_i) unless the override *bov_i is not NaN; vim1 null: 0.
 void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
                const double* hall, const double* w, const double* vi, const double* vim1, const double* fn2_i,
-               const double* bov_i, double* dst, double* npart, double* alpha, double* offd);
+               const double* bov_i, double* dst, double* npart, double* alpha, double* offd, double* cflag,
+               double cancel);
 // gemvt of the three-term residual f' = w - *alpha vi - beta_i vim1 (vim1 may
 // be null; beta_i as three_term), formed per row; f' is also stored to fp.
 // v32col != null: the fp32 basis shadow's column i = fl32(vi) is written and

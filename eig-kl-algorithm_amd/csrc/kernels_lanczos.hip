@@ -387,13 +387,15 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
 // Gram-Schmidt coefficients of f' = w - alpha v_i - beta v_{i-1} come out of
 // ONE all-reduce: V^T f' = V^T w - alpha V^T v_i - beta V^T v_{i-1}, with
 // alpha = (V^T w)_i.  part[(k * tot + j) * nrb + b] for vector k (0: w, 1: v_i,
-// 2: v_{i-1}), column j < tot = ncols + has_u0 (column ncols = u0).  Same
-// tiling, XCD remap and fixed-shape reductions as k_gemvt.
+// 2: v_{i-1}), column j < tot = ncols + has_u0 (column ncols = u0), and
+// part[3 tot * nrb + b] = ||w||^2 over row block b (k_update_mr's test for a
+// cancelled f').  Same tiling, XCD remap and fixed-shape reductions as k_gemvt.
 __global__ __launch_bounds__(256) void k_gemvt3(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                 int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                 const double* __restrict__ va, const double* __restrict__ vb,
                                                 double* __restrict__ part) {
     __shared__ double red[3][4][GT_COLS];
+    __shared__ double nred[4];
     const int t = threadIdx.x;
     const int tot = ncols + has_u0;
     const int ncg = (tot + GT_COLS - 1) / GT_COLS;
@@ -437,6 +439,13 @@ __global__ __launch_bounds__(256) void k_gemvt3(int ldv, int nrb, const double* 
             }
         }
     }
+    if (j0 == 0) {  // ||w||^2 over this row block (the same tree as k_gemvt's nrm)
+        double s2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < KR; ++k) s2 += xs[0][k].x * xs[0][k].x + xs[0][k].y * xs[0][k].y;
+        s2 = wave_sum(s2);
+        if ((t & 63) == 0) nred[t >> 6] = s2;
+    }
     // the reduce-scatter of k_gemvt, once per vector
     const int lane = t & 63;
 #pragma unroll
@@ -470,6 +479,7 @@ __global__ __launch_bounds__(256) void k_gemvt3(int ldv, int nrb, const double* 
             part[(size_t(m) * tot + size_t(j0 + c)) * nrb + rbk] =
                 (red[m][0][c] + red[m][1][c]) + (red[m][2][c] + red[m][3][c]);
     }
+    if (j0 == 0 && t == 3 * GT_COLS) part[size_t(3 * tot) * nrb + rbk] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
 }
 
 // The canonical order of a column sum over the projection partials: 8 lanes
@@ -768,7 +778,8 @@ __global__ __launch_bounds__(256) void k_update_mr(int ldv, const double* __rest
                                                    const double* __restrict__ vim1, const double* __restrict__ fn2_i,
                                                    const double* __restrict__ bov_i, double* __restrict__ dst,
                                                    double* __restrict__ npart, double* __restrict__ alpha,
-                                                   double* __restrict__ offd) {
+                                                   double* __restrict__ offd, double* __restrict__ cflag,
+                                                   double cancel) {
     constexpr int UB = EK_UPD_UB;
     __shared__ double hc[MAX_NCV + 2 * UB];
     __shared__ double hu0;
@@ -799,6 +810,15 @@ __global__ __launch_bounds__(256) void k_update_mr(int ldv, const double* __rest
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         alpha[i] = a + hc[i];
         if (i > 0) offd[i] = braw + hc[i - 1];
+        // ||f'||^2 from the same sums (v_i, v_{i-1} unit and orthogonal to
+        // rounding): a cancelled f' (||f'||^2 < cancel ||w||^2) leaves the
+        // projection of f' by linearity with an error eps ||w|| instead of
+        // eps ||f'||, so the host re-projects the next vector (Lanczos::repair)
+        const double w2 = hall[3 * tot];
+        const double vw = i > 0 ? hall[i - 1] : 0.0, vv = i > 0 ? hall[tot + i - 1] : 0.0;
+        const double vn = i > 0 ? hall[2 * tot + i - 1] : 0.0;
+        const double f2 = w2 - 2.0 * a * a - 2.0 * b * vw + a * a * hall[tot + i] + b * b * vn + 2.0 * a * b * vv;
+        cflag[i] = f2 < cancel * w2 ? 1.0 : 0.0;  // (NaN: 0 — a breakdown is the host's own test)
     }
     double2 x = xw;
     x.x -= a * xv.x;
@@ -1131,9 +1151,10 @@ void gemvt3(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has
 
 void update_mr(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
                const double* hall, const double* w, const double* vi, const double* vim1, const double* fn2_i,
-               const double* bov_i, double* dst, double* npart, double* alpha, double* offd) {
+               const double* bov_i, double* dst, double* npart, double* alpha, double* offd, double* cflag,
+               double cancel) {
     hipLaunchKernelGGL(k_update_mr, dim3(ldv / UPD_ROWS), dim3(256), 0, s, ldv, V, ncols, has_u0, u0val, nreal, hall,
-                       w, vi, vim1, fn2_i, bov_i, dst, npart, alpha, offd);
+                       w, vi, vim1, fn2_i, bov_i, dst, npart, alpha, offd, cflag, cancel);
 }
 
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h) {

@@ -241,6 +241,8 @@ typedef struct {
     int32_t update32_steps;     /* steps whose update was enqueued with the fp32 shadow */
     int32_t update32_fallbacks; /* ... of which took the fp64 basis (the accuracy test failed) */
     int32_t projected_steps;    /* steps that ran the Gram-Schmidt pass (= matvecs unless reorth 3) */
+    int32_t reprojected;        /* sharded steps whose f' cancelled (||f'||^2 < 2^-20 ||w||^2) and
+                                   whose next vector was projected again (a second CGS pass) */
     double ortho_max;           /* EK_LANCZOS_ORTHO=1: max |[V u0]^T [V u0] - I| at the restarts */
 } ek_lanczos_stats;
 

@@ -237,3 +237,66 @@ def test_two_rank_sharded_lanczos_syn10_config4():
     assert r0["nrows"] + r1["nrows"] == 2019200 and r1["row0"] == r0["nrows"]
     assert r0["lam"] == r1["lam"] and r0["v_sha"] == r1["v_sha"]
     assert abs(r0["lam"] - r0["lam1"]) <= 1e-10 and r0["residual1"] < 1e-8
+
+
+@pytest.mark.parametrize("name", ["ibm01", "industry2"])
+def test_rccl_one_rank_production_path(ek, monkeypatch, name):
+    """The RCCL production path on the 1-GPU pool: under
+    EK_COMM_FORCE a 1-rank context creates a real RCCL communicator
+    (ncclCommInitRank, nranks 1) and runs the sharded step (ctx.cpp
+    factorize_mr: the slot layout with the ||f||^2 tail, ncclAllGather of the
+    slots, ONE in-place ncclAllReduce of the projections, stream order).  The
+    Fiedler pair must meet the pre_saved_EIG tolerances, the same forced path
+    staged through the host (identity callbacks) must give the same bits, and
+    every Lanczos step must issue one all-gather (+ the final vector's)."""
+    monkeypatch.setenv("EK_COMM_FORCE", "1")
+    h = ek.Hypergraph.read(circuit_path(name))
+    L = h.laplacian()
+    out = {}
+    for mode in ("rccl", "host"):
+        c = ek.Context(0)
+        try:
+            if mode == "rccl":
+                c.comm_init(1, 0, ek.comm_unique_id())
+            else:
+                c.comm_init_host(1, 0, lambda x: x.copy(), lambda x: None)
+            c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+            out[mode] = c.lanczos_fiedler()
+        finally:
+            c.close()
+    (lam, v, st), (lam_h, v_h, st_h) = out["rccl"], out["host"]
+    print(name, {k: st[k] for k in ("matvecs", "restarts", "allgathers", "allreduces", "reprojected", "residual")})
+    r = _fiedler_ok(ek, name, lam, v)
+    assert st["converged"] and st["residual"] < 1e-9 and r["dlam"] <= 1e-10 and r["dv"] <= 1e-8 and r["bits_equal"], r
+    assert st["allgathers"] == st["matvecs"] + 1
+    assert st["matvecs"] <= st["allreduces"] <= st["matvecs"] + 3 + 2 * (st["restarts"] + 1)
+    assert lam_h == lam and v_h.tobytes() == v.tobytes()
+    assert (st_h["allgathers"], st_h["allreduces"]) == (st["allgathers"], st["allreduces"])
+
+
+@pytest.mark.parametrize("name", ["ibm01", "industry2"])
+def test_sharded_step_reprojection(ek, monkeypatch, name):
+    """the sharded step projects f' by linearity, exact to
+    eps ||w|| rather than eps ||f'||; where f' cancels (||f'||^2 <
+    2^-20 ||w||^2) the driver projects the next vector once more (ctx.cpp
+    Lanczos::repair).  The bar is raised (EK_MR_CANCEL=0.1) so the repair runs
+    on many steps: the run must still meet the golden's tolerances with the
+    basis orthonormal to 1e-12 at every restart (EK_LANCZOS_ORTHO), on the
+    forced 1-rank RCCL path."""
+    monkeypatch.setenv("EK_COMM_FORCE", "1")
+    monkeypatch.setenv("EK_MR_CANCEL", "0.1")
+    monkeypatch.setenv("EK_LANCZOS_ORTHO", "1")
+    h = ek.Hypergraph.read(circuit_path(name))
+    L = h.laplacian()
+    c = ek.Context(0)
+    try:
+        c.comm_init(1, 0, ek.comm_unique_id())
+        c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+        lam, v, st = c.lanczos_fiedler()
+    finally:
+        c.close()
+    print(name, {k: st[k] for k in ("matvecs", "restarts", "reprojected", "ortho_max", "residual")})
+    r = _fiedler_ok(ek, name, lam, v)
+    assert st["converged"] and st["residual"] < 1e-9 and r["dlam"] <= 1e-10 and r["dv"] <= 1e-8 and r["bits_equal"], r
+    assert st["reprojected"] > 0
+    assert st["ortho_max"] <= 1e-12
