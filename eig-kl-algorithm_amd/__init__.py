@@ -20,7 +20,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# EK_LIB_PATH: a design lab's A/B build of the same library (tools/ab_lab.sh)
+# EK_LIB_PATH: a design lab's A/B build of the same library (profiles/r03/scripts/ab_lab.sh)
 LIB_PATH = os.environ.get("EK_LIB_PATH") or os.path.join(HERE, "build", "libeigkl_hip.so")
 BIN_DIR = os.path.join(HERE, "build", "bin")
 

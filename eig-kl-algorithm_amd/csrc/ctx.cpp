@@ -126,6 +126,14 @@ struct ek_ctx {
     int64_t slot = 0;
     DBuf off_d, xexp;
     DBuf spx;  // ek_spmv's x in the all-gather layout (sharded), sized when the shard map is set
+    // the owned-slot part of a sharded rank's rows (plain CSR, local column
+    // ids), summed while the all-gather of the other slots runs on `gstream`
+    DBuf own_rowptr, own_col, own_val, own_rb, yown;
+    int own_nrb = 0;
+    int64_t own_nnz = 0;
+    bool own_ready = false;
+    hipStream_t gstream = nullptr;
+    hipEvent_t ag_ev[2] = {nullptr, nullptr};
     // the column-panel form of the SpMV (pn_G > 0; kernels_panel.hip)
     int pn_G = 0, pn_P = 0, pn_pb = 0, pn_max_rows = 0, pn_ndict = 0;
     DBuf pn_wrow, pn_start, pn_word, pn_rid;
@@ -235,6 +243,18 @@ ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
     return m;
 }
 
+// the owned-slot rows (c->own_*): plain CSR over local columns, x = the rank's f
+ek::dev::SpmvMat own_mat(const ek_ctx* c) {
+    ek::dev::SpmvMat m;
+    m.nblocks = c->own_nrb;
+    m.block_nnz = 512;
+    m.desc = c->own_rb.as<int32_t>();
+    m.rowptr = c->own_rowptr.as<int32_t>();
+    m.col = c->own_col.as<int32_t>();
+    m.val = c->own_val.as<double>();
+    return m;
+}
+
 double* stage_for(ek_ctx* c, size_t doubles) {
     if (c->stage_doubles < doubles) {
         if (c->stage) HIPCHK(hipHostFree(c->stage));
@@ -281,22 +301,24 @@ void allreduce(ek_ctx* c, double* p, size_t count) {
     HIPCHK(hipStreamSynchronize(c->stream));  // the staging buffer is reused by the next collective
 }
 
-// recv[r*count .. (r+1)*count) = rank r's send block (rank-major), on the stream.
-void allgather(ek_ctx* c, const double* send, size_t count, double* recv) {
+// recv[r*count .. (r+1)*count) = rank r's send block (rank-major), on the
+// stream (default: the context's).
+void allgather(ek_ctx* c, const double* send, size_t count, double* recv, hipStream_t st = nullptr) {
     ++c->n_ag;
+    if (!st) st = c->stream;
     if (c->comm) {
-        NCCLCHK(ncclAllGather(send, recv, count, ncclDouble, c->comm, c->stream));
+        NCCLCHK(ncclAllGather(send, recv, count, ncclDouble, c->comm, st));
         return;
     }
     CommTimer t{c};
     const size_t tot = count * size_t(c->nranks);
     double* h = stage_for(c, count + tot);
-    HIPCHK(hipMemcpyAsync(h, send, count * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpyAsync(h, send, count * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     if (c->host_ag(c->host_user, h, int64_t(count), h + count) != 0)
         ek::fail(EK_ECOMM, "host all-gather callback failed");
-    HIPCHK(hipMemcpyAsync(recv, h + count, tot * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpyAsync(recv, h + count, tot * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
 }
 
 void comm_reset(ek_ctx* c) {
@@ -369,6 +391,12 @@ void ek_destroy(ek_ctx* c) {
         if (c->chk_copied[i]) (void)hipEventDestroy(c->chk_copied[i]);
     }
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->gstream) {
+        (void)hipStreamSynchronize(c->gstream);
+        (void)hipStreamDestroy(c->gstream);
+    }
+    for (auto e : c->ag_ev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->kstream);
     (void)hipStreamDestroy(c->stream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
@@ -544,6 +572,66 @@ void remap_cols_host(const ek_ctx* c, const int32_t* col, int64_t nnz, std::vect
     });
 }
 
+// The owned-slot rows of a sharded context (factorize_mr overlaps their SpMV
+// with the all-gather): row blocks over the local CSR own_rowptr_h, the
+// stream and events of the overlapped step.
+void own_finish(ek_ctx* c, const std::vector<int32_t>& orp) {
+    auto rbv = ek::dev::spmv_row_blocks(orp.data(), c->nrows, 512);
+    c->own_nrb = int(rbv.size() / 4);
+    upload(c->own_rb, rbv.data(), rbv.size(), c->stream);
+    c->yown.ensure(size_t(std::max<int64_t>(c->nrows, 1)) * 8);
+    if (!c->gstream) HIPCHK(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+    for (auto& e : c->ag_ev)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->own_ready = true;
+}
+
+// ... from the host rows (columns already in the slot layout)
+void own_build_host(ek_ctx* c, const int32_t* rowptr, const int32_t* col, const double* val) {
+    c->own_ready = false;
+    const int64_t lo = c->rank * c->slot, hi = lo + c->nrows;
+    std::vector<int32_t> orp(size_t(c->nrows) + 1, 0), oc;
+    std::vector<double> ov;
+    for (int64_t r = 0; r < c->nrows; ++r) {
+        for (int32_t p = rowptr[r]; p < rowptr[r + 1]; ++p)
+            if (col[p] >= lo && col[p] < hi) {
+                oc.push_back(int32_t(col[p] - lo));
+                ov.push_back(val[p]);
+            }
+        orp[size_t(r) + 1] = int32_t(oc.size());
+    }
+    c->own_nnz = int64_t(oc.size());
+    upload(c->own_rowptr, orp.data(), orp.size(), c->stream);
+    upload(c->own_col, oc.data(), std::max<size_t>(oc.size(), 1), c->stream);
+    upload(c->own_val, ov.data(), std::max<size_t>(ov.size(), 1), c->stream);
+    own_finish(c, orp);
+}
+
+// ... from the device rows (ek_spmv_setup_pins: c->rowptr / col / val, columns remapped)
+void own_build_dev(ek_ctx* c, hipStream_t s, long long* tiles) {
+    c->own_ready = false;
+    const int lo = int(c->rank * c->slot), hi = int(lo + c->nrows);
+    const size_t nr = size_t(c->nrows);
+    DBuf cnt, offs;
+    cnt.ensure((nr + 1) * 4);
+    offs.ensure((nr + 1) * 8);
+    const long long tot = ek::dev::own_split(s, (long long)nr, c->rowptr.as<int>(), c->col.as<int>(),
+                                             c->val.as<double>(), lo, hi, cnt.as<int>(), offs.as<long long>(), tiles,
+                                             nullptr, nullptr, nullptr);
+    c->own_nnz = tot;
+    c->own_rowptr.ensure((nr + 1) * 4);
+    c->own_col.ensure(size_t(std::max<long long>(tot, 1)) * 4);
+    c->own_val.ensure(size_t(std::max<long long>(tot, 1)) * 8);
+    ek::dev::own_split(s, (long long)nr, c->rowptr.as<int>(), c->col.as<int>(), c->val.as<double>(), lo, hi,
+                       cnt.as<int>(), offs.as<long long>(), tiles, c->own_rowptr.as<int>(), c->own_col.as<int>(),
+                       c->own_val.as<double>());
+    std::vector<int32_t> orp(nr + 1);
+    HIPCHK(hipMemcpyAsync(orp.data(), c->own_rowptr.p, (nr + 1) * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    own_finish(c, orp);
+}
+
 // ek_spmv_setup's body, the shard map given (no collective: also the
 // device build's host fallback, which one rank may take alone)
 void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, const int32_t* rowptr, const int32_t* col,
@@ -558,9 +646,11 @@ void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, cons
     for (int64_t p = 0; p < nnz; ++p)
         if (col[p] < 0 || col[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup: column %d out of range", col[p]);
     std::vector<int32_t> colx;  // sharded: the columns in the all-gather layout
+    c->own_ready = false;
     if (c->mr) {
         remap_cols_host(c, col, nnz, colx);
         col = colx.data();
+        own_build_host(c, rowptr, col, val);
     }
     c->n = n;
     c->nnz = nnz;
@@ -796,9 +886,11 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
     c->n = n;
     c->nnz = nnz;
     const std::vector<long long> offll(off.begin(), off.end());  // (alive until the stream is drained below)
+    c->own_ready = false;
     if (c->mr) {  // global columns -> the all-gather layout (monotone: rows stay sorted)
         upload(c->off_d, offll.data(), offll.size(), s);
         ek::dev::remap_cols(s, nnz, c->col.as<int>(), c->off_d.as<long long>(), c->nranks, c->slot);
+        own_build_dev(c, s, tiles);
     }
     // the same greedy row blocks as the host path (ek_spmv_setup)
     int colbits = 1;
@@ -1121,6 +1213,9 @@ struct Lanczos {
     // few ulps x ||w||/||f||; it does not compound, because f' is still formed
     // by direct subtraction).  Not bit-identical to the single-GPU step; within
     // the Fiedler tolerances on every golden (tests).
+    // overlap (sharded): the owned-slot SpMV runs on the context stream while
+    // the all-gather runs on gstream; the halo SpMV then starts from its sums
+    bool overlap = false;
     void factorize_mr(int k, int kend) {
         double* fn2 = c->fn2.as<double>();
         double* f = c->f.as<double>();
@@ -1128,11 +1223,25 @@ struct Lanczos {
         for (int i = k; i < kend; ++i) {
             ek::dev::finalize_step(s, c->npart.as<double>(), nub, f + ldv, nullptr, nullptr, -1, nullptr, nullptr);
             const double* x = f;
-            if (sharded) {
+            ek::dev::StepFin fin;
+            if (sharded && overlap) {
+                // f (with this rank's ||f||^2 partial at f[ldv]) is final: the
+                // all-gather goes out on gstream, and the owned slot's rows are
+                // summed meanwhile (unscaled: ||f|| comes with the all-gather)
+                HIPCHK(hipEventRecord(c->ag_ev[0], s));
+                HIPCHK(hipStreamWaitEvent(c->gstream, c->ag_ev[0], 0));
+                ek::dev::spmv(s, own_mat(c), f, c->yown.as<double>(), nullptr, nullptr, nullptr, nullptr);
+                allgather(c, f, size_t(c->slot), c->xfull.as<double>(), c->gstream);
+                HIPCHK(hipEventRecord(c->ag_ev[1], c->gstream));
+                HIPCHK(hipStreamWaitEvent(s, c->ag_ev[1], 0));
+                x = c->xfull.as<double>();
+                fin.own_lo = int(c->rank * c->slot);
+                fin.own_hi = int(c->rank * c->slot + c->nrows);
+                fin.ybase = c->yown.as<double>();
+            } else if (sharded) {
                 allgather(c, f, size_t(c->slot), c->xfull.as<double>());
                 x = c->xfull.as<double>();
             }
-            ek::dev::StepFin fin;
             fin.npart = x + ldv;
             fin.nb = c->nranks;
             fin.nstride = int(c->slot);
@@ -1534,6 +1643,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     };
     // the sharded step's re-projection of a cancelled f' (Lanczos::repair)
     const bool mr_step = c->mr && L.reorth == 1;
+    // the owned-slot / halo split of the sharded SpMV (EK_MR_OVERLAP=0: one
+    // SpMV after the all-gather, the round-3 step; A/B and tests)
+    {
+        const char* e = std::getenv("EK_MR_OVERLAP");
+        L.overlap = c->mr && c->own_ready && !(e && e[0] == '0');
+    }
     if (mr_step) {
         c->cflag.ensure(size_t(m + 2) * 8);
         if (const char* e = std::getenv("EK_MR_CANCEL"); e && e[0]) L.mr_cancel = std::atof(e);  // (tests)

@@ -170,6 +170,12 @@ struct StepFin {
     // scaled product) beside its alpha partial, for k_pro's estimate of
     // beta_{i+1}.  Read whether or not npart is set.
     double* wpart = nullptr;
+    // the sharded step's halo SpMV (overlapped with the all-gather): entries
+    // whose column lies in [own_lo, own_hi) (the rank's own slot, summed by
+    // the owned-slot SpMV beforehand) contribute 0, and every row's sum starts
+    // from ybase[row] (that SpMV's unscaled partial); own_lo == own_hi: none
+    int own_lo = 0, own_hi = 0;
+    const double* ybase = nullptr;
 };
 
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
@@ -279,6 +285,23 @@ void encode_segments(hipStream_t s, int nblocks, const int32_t* desc, const int*
 // col[p] (global ids) -> r * slot + (col - off[r]) for the owner r of col
 // (off: nranks + 1 row offsets of the shard map): the all-gather slot layout
 void remap_cols(hipStream_t s, long long nnz, int* col, const long long* off, int nranks, long long slot);
+// the entries of each of nr local rows whose column lies in [lo, hi), with
+// columns rebased to col - lo: a first call with ocol == null counts them
+// (cnt: nr ints, off: nr + 1, tiles: scan scratch) and returns the total;
+// a second call with the output arrays (orp: nr + 1) fills them
+long long own_split(hipStream_t s, long long nr, const int* rowptr, const int* col, const double* val, int lo, int hi,
+                    int* cnt, long long* off, long long* tiles, int* orp, int* ocol, double* oval);
+
+// The memory order of the counter adds that pick the last workgroup of an
+// in-launch hand-off (kernels_spmv/lanczos/panel.hip): acquire-release at
+// agent scope (the partials' stores happen-before the add, the last block's
+// loads after it).  EK_HANDOFF_RELAXED: relaxed adds after an explicit
+// vmcnt(0) wait, the round-3 form (A/B builds only).
+#ifdef EK_HANDOFF_RELAXED
+#define EK_HANDOFF_ORDER __ATOMIC_RELAXED
+#else
+#define EK_HANDOFF_ORDER __ATOMIC_ACQ_REL
+#endif
 
 // kernels_lanczos.hip
 #ifndef EK_GT_ROWS

@@ -484,5 +484,50 @@ void remap_cols(hipStream_t s, long long nnz, int* col, const long long* off, in
         hipLaunchKernelGGL(k_remap_cols, dim3(grid_of(nnz)), dim3(BT), 0, s, nnz, col, off, nranks, slot);
 }
 
+// The owned-slot part of a sharded rank's rows (ctx.cpp factorize_mr: its
+// SpMV runs while the all-gather of the other slots is in flight): per local
+// row the entries whose slot-layout column lies in [lo, hi) — a contiguous
+// run, the columns are sorted — counted, then copied with LOCAL column ids
+// (col - lo: x is the rank's own f) after an exclusive scan of the counts.
+__global__ __launch_bounds__(BT) void k_own_count(long long nr, const int* __restrict__ rowptr,
+                                                  const int* __restrict__ col, int lo, int hi, int* __restrict__ cnt) {
+    const long long r = (long long)blockIdx.x * BT + threadIdx.x;
+    if (r >= nr) return;
+    int k = 0;
+    for (int p = rowptr[r]; p < rowptr[r + 1]; ++p) k += col[p] >= lo && col[p] < hi;
+    cnt[r] = k;
+}
+
+__global__ __launch_bounds__(BT) void k_own_fill(long long nr, const int* __restrict__ rowptr,
+                                                 const int* __restrict__ col, const double* __restrict__ val, int lo,
+                                                 int hi, const long long* __restrict__ off, int* __restrict__ orp,
+                                                 int* __restrict__ ocol, double* __restrict__ oval) {
+    const long long r = (long long)blockIdx.x * BT + threadIdx.x;
+    if (r > nr) return;
+    orp[r] = int(off[r]);
+    if (r == nr) return;
+    long long q = off[r];
+    for (int p = rowptr[r]; p < rowptr[r + 1]; ++p)
+        if (col[p] >= lo && col[p] < hi) {
+            ocol[q] = col[p] - lo;
+            oval[q] = val[p];
+            ++q;
+        }
+}
+
+long long own_split(hipStream_t s, long long nr, const int* rowptr, const int* col, const double* val, int lo, int hi,
+                    int* cnt, long long* off, long long* tiles, int* orp, int* ocol, double* oval) {
+    if (nr <= 0) return 0;
+    hipLaunchKernelGGL(k_own_count, dim3(grid_of(nr)), dim3(BT), 0, s, nr, rowptr, col, lo, hi, cnt);
+    exclusive_scan(s, cnt, nr, off, tiles);
+    long long tot = 0;
+    (void)hipMemcpyAsync(&tot, off + nr, 8, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    if (ocol)
+        hipLaunchKernelGGL(k_own_fill, dim3(grid_of(nr + 1)), dim3(BT), 0, s, nr, rowptr, col, val, lo, hi, off, orp,
+                           ocol, oval);
+    return tot;
+}
+
 }  // namespace dev
 }  // namespace ek

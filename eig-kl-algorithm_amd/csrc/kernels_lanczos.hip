@@ -64,7 +64,11 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 }
 
 // Agent-scope (sc1) stores / loads: the hand-off of partials between
-// workgroups of one launch (MI355X_MICROARCH.md, inter-workgroup visibility)
+// workgroups of one launch (MI355X_MICROARCH.md, inter-workgroup visibility).
+// The counter adds that pick the last workgroup are acquire-release at agent
+// scope: every block's partial stores happen-before its add (release), and the
+// last block's partial loads after its add (acquire) — the memory model's
+// guarantee, not only today's codegen (the explicit vmcnt waits stay).
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -153,8 +157,8 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
         const int g = rbk % GT_SUB;
         const unsigned gsize = unsigned((nrb - g + GT_SUB - 1) / GT_SUB), ngroups = unsigned(nrb < GT_SUB ? nrb : GT_SUB);
         int last = 0;
-        if (__hip_atomic_fetch_add(gctr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
-            last = __hip_atomic_fetch_add(gctr + GT_SUB * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        if (__hip_atomic_fetch_add(gctr + g * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
+            last = __hip_atomic_fetch_add(gctr + GT_SUB * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) ==
                    ngroups - 1u;
         s_last = last;
     }
@@ -350,8 +354,8 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
         const int g = rbk % GT_SUB;
         const unsigned gsize = unsigned((nrb - g + GT_SUB - 1) / GT_SUB), ngroups = unsigned(nrb < GT_SUB ? nrb : GT_SUB);
         int last = 0;
-        if (__hip_atomic_fetch_add(ctr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
-            last = __hip_atomic_fetch_add(ctr + GT_SUB * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        if (__hip_atomic_fetch_add(ctr + g * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
+            last = __hip_atomic_fetch_add(ctr + GT_SUB * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) ==
                    ngroups - 1u;
         s_last = last;
     }

@@ -208,12 +208,16 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
             rr[u] = i < cnt ? m.rid[cc + i] : uint16_t(0xffff);  // 0xffff: no entry
         }
     };
+    const int olo = fin.own_lo, ohi = fin.own_hi;  // (the halo SpMV: the own slot's entries are 0)
     auto gather = [&](int pp, const uint32_t* wd, double* xv, double* dv) {
         const double* xp = x + (size_t(pp < P ? pp : 0) << pb);
+        const int cbase = (pp < P ? pp : 0) << pb;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            xv[u] = xp[wd[u] & pmask];  // word 0 past cnt: a valid address
-            dv[u] = LDICT ? sdict[wd[u] >> pb] : dict[wd[u] >> pb];
+            const int cg = cbase + int(wd[u] & pmask);
+            const bool own = cg >= olo && cg < ohi;
+            xv[u] = own ? 0.0 : xp[wd[u] & pmask];  // word 0 past cnt: a valid address
+            dv[u] = own ? 0.0 : (LDICT ? sdict[wd[u] >> pb] : dict[wd[u] >> pb]);
         }
     };
     // chunk k (p, c0), k+1 (p1, c1), k+2 (p2, c2)
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     const double scale = (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0;
     double av = 0.0, wv = 0.0;
     for (int r = t; r < nr; r += PT) {
-        const double yr = acc[r] * scale;
+        const double yr = (fin.ybase ? fin.ybase[r0 + r] + acc[r] : acc[r]) * scale;
         y[r0 + r] = yr;
         if (vcol) {
             const double v = f[r0 + r] * scale;
@@ -342,8 +346,8 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
             const unsigned nb = gridDim.x, g = blockIdx.x % ALPHA_SUB;
             const unsigned gsize = (nb - g + ALPHA_SUB - 1) / ALPHA_SUB, ngroups = nb < ALPHA_SUB ? nb : ALPHA_SUB;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            s_last = __hip_atomic_fetch_add(actr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u &&
-                             __hip_atomic_fetch_add(actr + ALPHA_SUB * 64, 1u, __ATOMIC_RELAXED,
+            s_last = __hip_atomic_fetch_add(actr + g * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u &&
+                             __hip_atomic_fetch_add(actr + ALPHA_SUB * 64, 1u, EK_HANDOFF_ORDER,
                                                     __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1u
                          ? 1
                          : 0;

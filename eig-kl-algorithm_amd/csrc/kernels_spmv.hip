@@ -97,8 +97,8 @@ __device__ __forceinline__ bool alpha_last_block(unsigned* ctr) {
     const unsigned nb = gridDim.x, g = blockIdx.x % ALPHA_SUB;
     const unsigned gsize = (nb - g + ALPHA_SUB - 1) / ALPHA_SUB, ngroups = nb < ALPHA_SUB ? nb : ALPHA_SUB;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (__hip_atomic_fetch_add(ctr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gsize - 1u) return false;
-    return __hip_atomic_fetch_add(ctr + ALPHA_SUB * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1u;
+    if (__hip_atomic_fetch_add(ctr + g * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) != gsize - 1u) return false;
+    return __hip_atomic_fetch_add(ctr + ALPHA_SUB * 64, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1u;
 }
 __device__ __forceinline__ void alpha_handoff(const double* apart, double* alpha_out, unsigned* ctr, double* wsum,
                                               int* s_last) {
@@ -188,12 +188,15 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         const double scale = scale_of(norm2());
         double s = 0.0;
         const uint32_t cmask = (1u << colbits) - 1u;
+        const int olo = fin.own_lo, ohi = fin.own_hi;  // (the halo SpMV: the own slot's entries are 0)
         for (int i = t; i < cnt; i += SPMV_THREADS) {
             if constexpr (PK) {
                 const uint32_t wd = uint32_t(col[p0 + i]);
-                s += val[wd >> colbits] * x[wd & cmask];
+                const int c = int(wd & cmask);
+                s += c >= olo && c < ohi ? 0.0 : val[wd >> colbits] * x[c];
             } else {
-                s += val[p0 + i] * x[col[p0 + i]];
+                const int c = col[p0 + i];
+                s += c >= olo && c < ohi ? 0.0 : val[p0 + i] * x[c];
             }
         }
 #pragma unroll
@@ -201,7 +204,8 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         if ((t & 63) == 0) wsum[t >> 6] = s;
         __syncthreads();
         if (t == 0) {
-            const double a = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+            const double a0 = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+            const double a = fin.ybase ? fin.ybase[r0] + a0 : a0;
             y[r0] = a * scale;
             if (vcol) {
                 const double v = f[r0] * scale;
@@ -238,8 +242,17 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     }
     const double fr = (vcol && t < nr) ? f[r0 + t] : 0.0;  // prefetched for the epilogue
     double xv[PER];
+    if (fin.own_hi > fin.own_lo) {  // the halo SpMV: the own slot's entries are summed by the owned-slot SpMV
 #pragma unroll
-    for (int u = 0; u < PER; ++u) xv[u] = ci[u] >= 0 ? x[ci[u]] : 0.0;
+        for (int u = 0; u < PER; ++u) {
+            const bool own = ci[u] >= fin.own_lo && ci[u] < fin.own_hi;
+            xv[u] = ci[u] >= 0 && !own ? x[ci[u]] : 0.0;
+            vv[u] = own ? 0.0 : vv[u];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) xv[u] = ci[u] >= 0 ? x[ci[u]] : 0.0;
+    }
     const double scale = scale_of(norm2());  // overlaps the gathers in flight
     if (t <= nr) rbeg[t] = rb0;
     if (t == 0 && nr == SPMV_THREADS) rbeg[SPMV_THREADS] = rb1;
@@ -258,7 +271,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         for (int i = rbeg[g] + lane; i < rbeg[g + 1]; i += L) s += prod[i];
     for (int o = L >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, L);
     if (g < nr && lane == 0) {
-        const double yr = s * scale;
+        const double yr = (fin.ybase ? fin.ybase[r0 + g] + s : s) * scale;
         y[r0 + g] = yr;
         if (apart) yrow[g] = yr;
     }

@@ -8,6 +8,8 @@ pieces (generator, Laplacian rows, the nnz-balanced shard map):
   doubles, with the rank's ||f||^2 partial in the slot's tail, so the matrix
   reads x through columns remapped to r*S + (c - off[r]) and every rank sums
   the ranks' partials in rank order (the same bits everywhere);
+* the SpMV split around that all-gather: the owned slot's entries summed from
+  the rank's own f while the gather is in flight, the halo's after it;
 * ONE all-reduce per step: [V^T w | V^T v_i | V^T v_{i-1}], from which
   alpha = (V^T w)_i and the projection of f' = w - alpha v_i - beta v_{i-1}
   come by linearity.
@@ -79,6 +81,7 @@ def _worker(rank, port, out):
         S_rows = h.laplacian_rows(row0, row0 + nrows)
         owner = np.searchsorted(off[1:-1], S_rows.col, side="right")
         colx = owner * S + (S_rows.col - off[owner])  # k_remap_cols
+        own = owner == rank  # the owned slot's entries (k_own_count)
         real = np.zeros(ldv)
         real[:nrows] = 1.0
         u0 = real / np.sqrt(n)
@@ -111,8 +114,15 @@ def _worker(rank, port, out):
             fn2 = sum(x[r * S + ldv] for r in range(WORLD))  # rank order: same bits on every rank
             b_prev = np.sqrt(fn2)
             v = f / b_prev
+            # the overlapped SpMV (ctx.cpp factorize_mr): the owned slot's
+            # entries summed from f itself (while the all-gather is in flight),
+            # the halo's from the gathered x, the row sum starting from the
+            # owned part, then scaled by 1/||f||
+            rp64 = S_rows.rowptr.astype(np.int64)
+            y_own = _local_spmv(rp64, np.where(own, colx - rank * S, 0), np.where(own, S_rows.val, 0.0), f)
+            y_halo = _local_spmv(rp64, colx, np.where(own, 0.0, S_rows.val), x)
             w = np.zeros(ldv)
-            w[:nrows] = _local_spmv(S_rows.rowptr.astype(np.int64), colx, S_rows.val, x) / b_prev
+            w[:nrows] = (y_own + y_halo) / b_prev
             V.append(v)
             if i > 0:
                 beta.append(b_prev)

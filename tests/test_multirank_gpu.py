@@ -264,8 +264,20 @@ def test_rccl_one_rank_production_path(ek, monkeypatch, name):
             out[mode] = c.lanczos_fiedler()
         finally:
             c.close()
+    # the same path without the owned-slot / halo split of the SpMV (one SpMV
+    # after the all-gather): other rounding, the same pair within tolerance
+    monkeypatch.setenv("EK_MR_OVERLAP", "0")
+    c = ek.Context(0)
+    try:
+        c.comm_init(1, 0, ek.comm_unique_id())
+        c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+        lam_n, v_n, st_n = c.lanczos_fiedler()
+    finally:
+        c.close()
     (lam, v, st), (lam_h, v_h, st_h) = out["rccl"], out["host"]
     print(name, {k: st[k] for k in ("matvecs", "restarts", "allgathers", "allreduces", "reprojected", "residual")})
+    assert abs(lam_n - lam) <= 1e-10 and st_n["residual"] < 1e-9
+    assert _fiedler_ok(ek, name, lam_n, v_n)["bits_equal"]
     r = _fiedler_ok(ek, name, lam, v)
     assert st["converged"] and st["residual"] < 1e-9 and r["dlam"] <= 1e-10 and r["dv"] <= 1e-8 and r["bits_equal"], r
     assert st["allgathers"] == st["matvecs"] + 1
