@@ -253,6 +253,15 @@ def main():
     prof = {}
     lcc = args.workload == "lcc"
     wl = f"{args.mult:g}lcc" if lcc else f"{args.mult:g}"  # tools/spmv_probe.py's workload argument
+    if world > 1 and rank == 0 and not args.no_extras and not args.no_pmc:
+        # the sharded SpMV (syn10 at this N): rank 0's rows, one process with
+        # no collective, while the other ranks wait in the rendezvous below
+        t = time.time()
+        shard = ["shard", 10.0, 10, world]
+        prof["trace10"] = rocprof_pass("trace", shard, work, f"10x_shard{world}")
+        prof["fetch10"] = rocprof_pass("FETCH_SIZE", shard, work, f"10x_shard{world}")
+        prof["write10"] = rocprof_pass("WRITE_SIZE", shard, work, f"10x_shard{world}")
+        log(f"rocprofv3 shard passes {time.time() - t:.1f} s")
     if extras and not args.no_pmc:
         t = time.time()
         prof["trace"] = rocprof_pass("trace", ["file", wl, args.seed, 1, 3], work, "1x")
@@ -434,11 +443,18 @@ def main():
                  "collectives_per_solve": {"allgather": st10["allgathers"], "allreduce": st10["allreduces"]},
                  "comm_ms_per_solve": round(max_over_ranks(st10["comm_ms"]), 3), "comm": comm if world > 1 else None}
         calls10, us10_rp = kernel_avg_us(prof.get("trace10"), "k_spmv")
-        if us10_rp:  # 1 rank: the rocprofv3 kernel trace of the same solve (a child pass before this process)
+        if us10_rp:  # the rocprofv3 kernel trace (a child pass before this process touched the GPU)
             syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,
                                 "achieved_GBps": round(b10 / us10_rp / 1e3, 1),
-                                "frac": round(b10 / us10_rp / 1e3 / HBM_PEAK_GBS, 4)}
-        if extras and not args.no_pmc:
+                                "frac": round(b10 / us10_rp / 1e3 / HBM_PEAK_GBS, 4),
+                                "what": ("the resident 1-rank solve" if world == 1 else
+                                         f"rank 0's shard of the {world}-rank map, 200 back-to-back fused launches "
+                                         "(tools/spmv_probe.py shard)")}
+        if world > 1:  # every rank's shard back to back (events), the max over ranks
+            us_bb = max_over_ranks(c10.spmv_bench(200, fused=True))
+            syn10["spmv_back_to_back_us_max_rank"] = round(us_bb, 3)
+            syn10["spmv_back_to_back_frac_per_gpu"] = round(b10 / us_bb / 1e3 / HBM_PEAK_GBS, 4)
+        if (extras or world > 1) and not args.no_pmc and rank == 0:
             t10 = traffic_of(prof.get("fetch10"), prof.get("write10"))
             if "error" not in t10:
                 t10["per_algorithmic_byte"] = round(t10["traffic"] / b10, 3)

@@ -1016,24 +1016,26 @@ int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_bench before ek_spmv_setup");
     if (iters <= 0 || !avg_us) ek::fail(EK_EINVAL, "ek_spmv_bench: bad argument");
-    if (c->mr) ek::fail(EK_EINVAL, "ek_spmv_bench: single-context measurement");
+    // (a sharded context: this rank's rows over the padded all-gather layout,
+    // x synthetic in every slot; no collective — bench.py's per-shard leg)
     hipStream_t s = c->stream;
-    const size_t n = size_t(c->n);
+    const size_t X = size_t(x_extent(c)), R = size_t(std::max<int64_t>(c->nrows, 1));
     DBuf x, y, vcol, apart, fn2;
-    x.ensure(n * 8);
-    y.ensure(n * 8);
-    vcol.ensure(n * 8);
+    x.ensure(X * 8);
+    y.ensure(R * 8);
+    vcol.ensure(R * 8);
     apart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
     fn2.ensure(8);
-    std::vector<double> h(n);
-    for (size_t i = 0; i < n; ++i) h[i] = double((i * 2654435761u) % 1000u) / 1000.0 - 0.5;
+    std::vector<double> h(X);
+    for (size_t i = 0; i < X; ++i) h[i] = double((i * 2654435761u) % 1000u) / 1000.0 - 0.5;
     double nrm = 0.0;
     for (double v : h) nrm += v * v;
-    HIPCHK(hipMemcpyAsync(x.p, h.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(x.p, h.data(), X * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(fn2.p, &nrm, 8, hipMemcpyHostToDevice, s));
+    const double* fsrc = x.as<double>() + (c->mr ? size_t(c->rank * c->slot) : 0);  // this rank's rows of x
     auto launch = [&] {
         if (fused)
-            ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), fn2.as<double>(), x.as<double>(),
+            ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), fn2.as<double>(), fsrc,
                           vcol.as<double>(), apart.as<double>());
         else
             ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), nullptr, nullptr, nullptr, nullptr);

@@ -293,14 +293,20 @@ long long own_split(hipStream_t s, long long nr, const int* rowptr, const int* c
                     int* cnt, long long* off, long long* tiles, int* orp, int* ocol, double* oval);
 
 // The memory order of the counter adds that pick the last workgroup of an
-// in-launch hand-off (kernels_spmv/lanczos/panel.hip): acquire-release at
-// agent scope (the partials' stores happen-before the add, the last block's
-// loads after it).  EK_HANDOFF_RELAXED: relaxed adds after an explicit
-// vmcnt(0) wait, the round-3 form (A/B builds only).
-#ifdef EK_HANDOFF_RELAXED
-#define EK_HANDOFF_ORDER __ATOMIC_RELAXED
-#else
+// in-launch hand-off (kernels_spmv/lanczos/panel.hip).  The partials travel
+// as agent-scope atomic stores and loads (sc1: performed at the memory side,
+// past the per-XCD L2s, so coherent across XCDs by themselves); each block's
+// thread 0 waits for its own partial stores (s_waitcnt vmcnt(0)) before its
+// relaxed counter add, and the last block issues its partial loads after the
+// add returned.  EK_HANDOFF_ACQREL: acquire-release adds, the memory model's
+// formal guarantee — on gfx950 an agent-scope release is a buffer_wbl2 (a
+// write-back of the XCD's whole L2) in every workgroup: measured 27.6 ->
+// 54.3 ms per resident Lanczos solve at the headline (tools/pro_ab.py,
+// reorth 1), so it stays an A/B build.
+#ifdef EK_HANDOFF_ACQREL
 #define EK_HANDOFF_ORDER __ATOMIC_ACQ_REL
+#else
+#define EK_HANDOFF_ORDER __ATOMIC_RELAXED
 #endif
 
 // kernels_lanczos.hip

@@ -65,10 +65,9 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
 
 // Agent-scope (sc1) stores / loads: the hand-off of partials between
 // workgroups of one launch (MI355X_MICROARCH.md, inter-workgroup visibility).
-// The counter adds that pick the last workgroup are acquire-release at agent
-// scope: every block's partial stores happen-before its add (release), and the
-// last block's partial loads after its add (acquire) — the memory model's
-// guarantee, not only today's codegen (the explicit vmcnt waits stay).
+// The counter adds that pick the last workgroup: EK_HANDOFF_ORDER
+// (ek_internal.hpp; relaxed after an explicit vmcnt(0) wait, the partials
+// themselves agent-scope atomics).
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -12,7 +12,13 @@ the GPU itself, each pass a process of its own):
                            pass whose average SpMV duration the line's
                            roofline uses.
 
-usage: python tools/spmv_probe.py MODE MULT SEED [W K]
+  shard MULT SEED N        rank 0's rows of the N-rank nnz-balanced shard map
+                           (ek_spmv_setup_pins computes it without a
+                           collective), 200 back-to-back fused SpMV launches
+                           over the padded all-gather layout (ek_spmv_bench):
+                           bench.py's per-GPU SpMV leg at N > 1, one process.
+
+usage: python tools/spmv_probe.py MODE MULT SEED [W K | N]
        python tools/spmv_probe.py MULT SEED          (= resident)
 MULT with the suffix "lcc" (e.g. 1.15lcc): the largest connected component of
 that synthetic (bench.py's headline workload).
@@ -28,7 +34,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     args = sys.argv[1:]
-    mode = args.pop(0) if args and args[0] in ("resident", "file") else "resident"
+    mode = args.pop(0) if args and args[0] in ("resident", "file", "shard") else "resident"
     lcc = args[0].endswith("lcc")
     mult, seed = float(args[0][:-3] if lcc else args[0]), int(args[1])
     spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
@@ -38,7 +44,18 @@ def main():
     if lcc:
         h, _ = h.largest_component()
     ctx = ek.Context(0)
-    if mode == "resident":
+    if mode == "shard":
+        nranks = int(args[2])
+
+        def no_collective(*_):
+            raise RuntimeError("the shard probe runs no collective")
+
+        ctx.comm_init_host(nranks, 0, no_collective, no_collective)
+        ctx.spmv_setup_pins(h)
+        us = ctx.spmv_bench(200, fused=True)
+        _, r0, nr = ctx.spmv_dims()
+        print(f"probe: rank 0 of {nranks}: rows {r0}..{r0 + nr}, {us:.2f} us per SpMV", flush=True)
+    elif mode == "resident":
         ctx.spmv_setup_pins(h)
         lam, _, st = ctx.lanczos_fiedler()
         print(f"probe: {h.nodes} nodes, {st['matvecs']} matvecs, lambda1 {lam:.3e}", flush=True)
