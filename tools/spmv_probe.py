@@ -57,7 +57,8 @@ def main():
         print(f"probe: rank 0 of {nranks}: rows {r0}..{r0 + nr}, {us:.2f} us per SpMV", flush=True)
     elif mode == "resident":
         ctx.spmv_setup_pins(h)
-        lam, _, st = ctx.lanczos_fiedler()
+        for _ in range(int(args[2]) if len(args) > 2 else 1):  # (optional: solves in a row)
+            lam, _, st = ctx.lanczos_fiedler()
         print(f"probe: {h.nodes} nodes, {st['matvecs']} matvecs, lambda1 {lam:.3e}", flush=True)
     else:
         warm, steps = int(args[2]), int(args[3])
