@@ -447,7 +447,7 @@ class Context:
     def spmv_bench(self, iters=200, fused=True):
         """Average microseconds per back-to-back SpMV launch on resident buffers."""
         us = ctypes.c_double()
-        _chk(_lib.ek_spmv_bench(self._c, int(iters), 1 if fused else 0, ctypes.byref(us)), "spmv_bench")
+        _chk(_lib.ek_spmv_bench(self._c, int(iters), int(fused), ctypes.byref(us)), "spmv_bench")
         return us.value
 
     def lanczos_fiedler(self, ncv=0, tol=1e-10, maxit=1000, deflate=True, time_spmv=False, reorth=3, check_every=8,

@@ -9,7 +9,9 @@
 #include <cstring>
 #include <atomic>
 #include <limits>
+#include <map>
 #include <memory>
+#include <tuple>
 
 #include "ek_internal.hpp"
 
@@ -151,6 +153,13 @@ struct ek_ctx {
     // omega ring (3 x OMEGA_LD), k_pro's state and its per-step decisions
     DBuf wpart, omega, prost, pflags;
     DBuf cflag;  // the sharded step's cancellation flags (update_mr), one double per step
+    // HIP graphs of the single-context Lanczos step chunks (factorize_fused),
+    // keyed by (first step, end, run start, V, V32): captured on a chunk's
+    // second launch, replayed from its third; dropped when any buffer or
+    // parameter the launches carry changes (lz_sig)
+    std::map<std::tuple<int, int, int, const void*, const void*>, hipGraphExec_t> lz_graphs;
+    std::map<std::tuple<int, int, int, const void*, const void*>, int> lz_seen;
+    std::vector<uint64_t> lz_sig;
     // KL state
     int64_t kl_n = 0, kl_n0 = 0, kl_n1 = 0, kl_nets = 0;
     DBuf kl_rowptr, kl_col, kl_w, kl_side, kl_side_init, kl_locked, kl_gp0, kl_gp1, kl_order0, kl_order1, kl_plist, kl_pinfo0, kl_pinfo1, kl_nd, kl_cinfo0, kl_cinfo1,
@@ -397,6 +406,7 @@ void ek_destroy(ek_ctx* c) {
     }
     for (auto e : c->ag_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& g : c->lz_graphs) (void)hipGraphExecDestroy(g.second);
     (void)hipStreamDestroy(c->kstream);
     (void)hipStreamDestroy(c->stream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
@@ -1033,10 +1043,39 @@ int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
     HIPCHK(hipMemcpyAsync(x.p, h.data(), X * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(fn2.p, &nrm, 8, hipMemcpyHostToDevice, s));
     const double* fsrc = x.as<double>() + (c->mr ? size_t(c->rank * c->slot) : 0);  // this rank's rows of x
+    // fused == 2: also the Lanczos step's finalize folded into the prologue
+    // (||f||^2 from the update's one value, block 0 publishing alpha / offd)
+    // and the ||w||^2 partials of partial reorthogonalisation: the SpMV exactly
+    // as the solve launches it
+    DBuf scratch, wp;
+    ek::dev::StepFin fin;
+    if (fused == 2) {
+        scratch.ensure(64 * 8);
+        wp.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
+        std::vector<double> sv(64, 0.0);
+        sv[0] = nrm;   // fast: ||f||^2
+        sv[1] = nrm;   // fn2_i
+        sv[2] = 0.5;   // a3
+        sv[3] = std::nan("");  // bov (no override)
+        HIPCHK(hipMemcpyAsync(scratch.p, sv.data(), 64 * 8, hipMemcpyHostToDevice, s));
+        double* sc = scratch.as<double>();
+        fin.npart = sc + 40;
+        fin.nb = 1;
+        fin.fast = sc;
+        fin.fn2_out = sc + 8;
+        fin.h2 = sc + 16;
+        fin.step = 1;
+        fin.alpha = sc + 24;
+        fin.offd = sc + 32;
+        fin.a3 = sc + 2;
+        fin.fn2_i = sc + 1;
+        fin.bov_i = sc + 3;
+        fin.wpart = wp.as<double>();
+    }
     auto launch = [&] {
         if (fused)
             ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), fn2.as<double>(), fsrc,
-                          vcol.as<double>(), apart.as<double>());
+                          vcol.as<double>(), apart.as<double>(), fused == 2 ? &fin : nullptr);
         else
             ek::dev::spmv(s, spmv_mat(c), x.as<double>(), y.as<double>(), nullptr, nullptr, nullptr, nullptr);
     };
@@ -1170,7 +1209,7 @@ struct Lanczos {
         // EK_LANCZOS_UNFUSED: run the sharded step sequence on one GPU (tests)
         static const bool unfused = std::getenv("EK_LANCZOS_UNFUSED") != nullptr;
         if (reorth == 1) {
-            if (!c->mr && !unfused) return factorize_fused(k, kend);
+            if (!c->mr && !unfused) return graphs && !time_spmv ? factorize_graph(k, kend) : factorize_fused(k, kend);
             return factorize_mr(k, kend);
         }
         double* fn2 = c->fn2.as<double>();
@@ -1340,7 +1379,7 @@ struct Lanczos {
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
                                   i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
                                   col32(i), (alpha_last || pro) ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff,
-                                  nt, flag);
+                                  nt, flag, pro ? fast : nullptr);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
                                     i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), col32(i));
@@ -1417,6 +1456,43 @@ struct Lanczos {
     }
     int repairs = 0;
     double mr_cancel = 0x1p-20;
+
+    // The single-context step chunk as a HIP graph.  Eager, the host spends
+    // ~10 us per kernel launch, so a partially reorthogonalised step (four
+    // launches, ~26 us of kernels when it skips the basis passes) waited for
+    // its launches (tools/trace_gaps.py: the GPU idle between kernels).  A
+    // chunk's launches depend only on (k, kend, seg0) and the context's
+    // buffers, so its graph is captured the second time the chunk is run and
+    // replayed from then on: the restart cycles repeat the same chunks, and a
+    // service's solves all of them.  (The first time it runs eagerly: a
+    // one-shot process does not pay for captures it never replays.)
+    bool graphs = false;
+    void factorize_graph(int k, int kend) {
+        const auto key = std::make_tuple(k, kend, seg0, static_cast<const void*>(V()), static_cast<const void*>(V32()));
+        auto it = c->lz_graphs.find(key);
+        if (it == c->lz_graphs.end()) {
+            if (++c->lz_seen[key] < 2) return factorize_fused(k, kend);
+            hipGraph_t g = nullptr;
+            HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+            try {
+                factorize_fused(k, kend);  // (recorded, not run; its host counters advance here)
+            } catch (...) {
+                (void)hipStreamEndCapture(s, &g);
+                if (g) (void)hipGraphDestroy(g);
+                throw;
+            }
+            HIPCHK(hipStreamEndCapture(s, &g));
+            hipGraphExec_t ex = nullptr;
+            const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            HIPCHK(e);
+            it = c->lz_graphs.emplace(key, ex).first;
+        } else {
+            matvecs += kend - k;
+            if (b32) u32_steps += kend - k;
+        }
+        HIPCHK(hipGraphLaunch(it->second, s));
+    }
 
     // Invariant subspace found at step j1-1 (||f|| collapsed, as on a graph
     // with several components): continue the sequence from a fresh random
@@ -1580,6 +1656,38 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         c->pflags.ensure(size_t(m + 2) * 4);
         HIPCHK(hipMemsetAsync(c->prost.p, 0, sizeof(ek::dev::ProState), s));
     }
+    // the step chunks' graphs (EK_LANCZOS_GRAPH=0: eager launches, A/B), kept
+    // while every buffer and parameter their launches carry is unchanged
+    L.graphs = env_or("EK_LANCZOS_GRAPH", true) && !c->mr && L.reorth == 1;
+    if (L.graphs) {
+        const int tt_env = std::getenv("EK_LANCZOS_TT") ? 1 : 0;
+        auto pv = [](const void* p) { return uint64_t(reinterpret_cast<uintptr_t>(p)); };
+        auto db = [](double x) {
+            uint64_t u;
+            std::memcpy(&u, &x, 8);
+            return u;
+        };
+        // (V / Vn and V32 / Vn32 swap at every restart: the pairs, not their order)
+        std::vector<uint64_t> sig{std::min(pv(c->V.p), pv(c->Vn.p)), std::max(pv(c->V.p), pv(c->Vn.p)),
+                                  std::min(pv(c->V32.p), pv(c->Vn32.p)), std::max(pv(c->V32.p), pv(c->Vn32.p)),
+                                  pv(c->f.p), pv(c->w.p),
+                                  pv(c->part.p), pv(c->h1.p), pv(c->h2.p), pv(c->alpha.p), pv(c->offd.p), pv(c->fn2.p),
+                                  pv(c->bov.p), pv(c->npart.p), pv(c->apart.p), pv(c->scal.p), pv(c->fbk.p),
+                                  pv(c->actr.p), pv(c->gctr.p), pv(c->wpart.p), pv(c->omega.p), pv(c->prost.p),
+                                  pv(c->pflags.p), pv(c->rb.p), pv(c->pk.p), pv(c->rel.p), pv(c->dict.p), pv(c->col.p),
+                                  pv(c->val.p), pv(c->rowptr.p), pv(c->pn_wrow.p), pv(c->pn_start.p), pv(c->pn_word.p),
+                                  pv(c->pn_rid.p), uint64_t(m), uint64_t(L.ldv), uint64_t(L.nreal), uint64_t(c->n),
+                                  uint64_t(c->nrb_spmv), uint64_t(c->pn_G), uint64_t(c->colbits), uint64_t(L.has_u0),
+                                  uint64_t(L.b32), uint64_t(L.pro), uint64_t(L.nt), uint64_t(L.alpha_last),
+                                  uint64_t(tt_env), db(L.pro_thresh),
+                                  db(L.pro_eps1), db(L.u0val)};
+        if (sig != c->lz_sig) {
+            for (auto& g : c->lz_graphs) HIPCHK(hipGraphExecDestroy(g.second));
+            c->lz_graphs.clear();
+            c->lz_seen.clear();
+            c->lz_sig = std::move(sig);
+        }
+    }
     // padded rows must be exactly 0 (only those: every kernel writes real
     // rows before it reads them, and no kernel writes a padded row nonzero)
     ek::dev::zero_pad_rows(s, c->V.as<double>(), L.ldv, L.nreal, m + 1);
@@ -1726,7 +1834,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                             beta_r = std::sqrt(std::max(0.0, pa[2 * m + jr]));
                         }
                     if (j1 >= 0 || jr >= 0) break;
-                    if (!ek::tridiag_eig(j, d.data(), e.data(), theta.data(), zl.data(), nullptr))
+                    // only the nev smallest Ritz values and their last components
+                    // (bisection + inverse iteration: ~70 us at j = 100 against
+                    // ~370 us for all j by QL; with partial reorthogonalisation a
+                    // chunk of steps is shorter than the QL took, and the GPU
+                    // waited for the check before the next chunk's launches)
+                    if (!ek::tridiag_smallest(j, d.data(), e.data(), std::min(nev, j), theta.data(), zl.data()))
                         ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
                     const double fj = std::sqrt(std::max(0.0, pa[2 * m + j]));
                     int nc = 0;

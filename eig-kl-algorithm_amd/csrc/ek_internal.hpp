@@ -110,6 +110,12 @@ uint64_t hashtable_next_buckets(uint64_t cur);  // bucket count after the rehash
 // eigenvalues (ascending) of the symmetric tridiagonal (d, e), e[i] = T(i+1,i);
 // zlast[j] = last component of eigenvector j; full Z (m x m col-major) if Z != null.
 bool tridiag_eig(int m, const double* d, const double* e, double* evals, double* zlast, double* Z);
+// The k smallest eigenvalues (ascending, bisection on Sturm counts to full
+// precision) and the last component of each unit eigenvector (inverse
+// iteration): what the Lanczos driver's mid-cycle convergence test reads, in
+// O(k m log) instead of tridiag_eig's O(m^2) QL sweeps.  False if the
+// iteration did not settle.
+bool tridiag_smallest(int m, const double* d, const double* e, int k, double* evals, double* zlast);
 // one implicit symmetric QR step with shift mu on (d, e); the rotations of
 // its Q factor appended to rots in order: {p, c, s} is Q <- Q G_p, i.e.
 // Q[i][p], Q[i][p+1] <- c a + s b, -s a + c b (a, b their old values)
@@ -354,7 +360,7 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col = nullptr, const double* apart = nullptr,
               int nparts = 0, unsigned* gctr = nullptr, double* h_out = nullptr, bool nt = false,
-              const int* flag = nullptr);
+              const int* flag = nullptr, double* fn2_fast = nullptr);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 

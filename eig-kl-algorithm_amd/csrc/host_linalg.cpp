@@ -95,6 +95,105 @@ bool tridiag_eig(int m, const double* d_in, const double* e_in, double* evals, d
     return true;
 }
 
+// Sturm count: the eigenvalues of T below x (LDL^T pivots of T - xI; a zero
+// pivot is nudged, the standard guard of dstebz)
+static int sturm_below(int m, const double* d, const double* e2, double x, double pivmin) {
+    int c = 0;
+    double q = d[0] - x;
+    if (std::fabs(q) < pivmin) q = -pivmin;
+    if (q < 0.0) ++c;
+    for (int i = 1; i < m; ++i) {
+        q = d[i] - x - e2[i - 1] / q;
+        if (std::fabs(q) < pivmin) q = -pivmin;
+        if (q < 0.0) ++c;
+    }
+    return c;
+}
+
+bool tridiag_smallest(int m, const double* d, const double* e, int k, double* evals, double* zlast) {
+    if (m <= 0 || k <= 0 || k > m) return false;
+    std::vector<double> e2(size_t(std::max(m - 1, 1)), 0.0);
+    double lo = d[0], hi = d[0], tnorm = 0.0, emax2 = 0.0;
+    for (int i = 0; i < m; ++i) {
+        const double r = (i > 0 ? std::fabs(e[i - 1]) : 0.0) + (i + 1 < m ? std::fabs(e[i]) : 0.0);
+        lo = std::min(lo, d[i] - r);
+        hi = std::max(hi, d[i] + r);
+        tnorm = std::max(tnorm, std::fabs(d[i]) + r);
+        if (i + 1 < m) {
+            e2[size_t(i)] = e[i] * e[i];
+            emax2 = std::max(emax2, e2[size_t(i)]);
+        }
+    }
+    const double pivmin = std::max(DBL_MIN, DBL_MIN * emax2);
+    std::vector<double> a(static_cast<size_t>(m)), b(static_cast<size_t>(m)), x(static_cast<size_t>(m)),
+        y(static_cast<size_t>(m));
+    for (int j = 0; j < k; ++j) {
+        // the (j+1)-th smallest: count(x) > j  <=>  x above it
+        double l = lo, h = hi;
+        // (to 1e-12 relative: the convergence test reads lambda through
+        // tol * max(eps^(2/3), |lambda|) only, and inverse iteration from it
+        // converges at the rate 1e-12 |lambda| / gap)
+        for (int it = 0; it < 200 && h - l > 1e-12 * std::max(std::fabs(l), std::fabs(h)) + pivmin; ++it) {
+            const double mid = 0.5 * (l + h);
+            if (mid <= l || mid >= h) break;
+            if (sturm_below(m, d, e2.data(), mid, pivmin) > j) h = mid;
+            else l = mid;
+        }
+        const double lam = 0.5 * (l + h);
+        evals[j] = lam;
+        // inverse iteration on T - (lam - delta) I, three solves by Gaussian
+        // elimination with partial pivoting of the tridiagonal (LAPACK dgtsv's
+        // scheme; a zero pivot is replaced by eps ||T||)
+        const double shift = lam - 1e-12 * std::fabs(lam) - DBL_EPSILON * tnorm, tiny = DBL_EPSILON * tnorm + DBL_MIN;
+        for (int i = 0; i < m; ++i) x[size_t(i)] = 1.0;
+        for (int pass = 0; pass < 3; ++pass) {
+            for (int i = 0; i < m; ++i) {
+                a[size_t(i)] = d[i] - shift;                  // D
+                b[size_t(i)] = i + 1 < m ? e[i] : 0.0;       // DL (sub), then DU2 after an interchange
+                y[size_t(i)] = i + 1 < m ? e[i] : 0.0;       // DU (super)
+            }
+            for (int i = 0; i + 1 < m; ++i) {
+                if (std::fabs(a[size_t(i)]) >= std::fabs(b[size_t(i)])) {
+                    if (a[size_t(i)] == 0.0) a[size_t(i)] = tiny;
+                    const double f = b[size_t(i)] / a[size_t(i)];
+                    a[size_t(i) + 1] -= f * y[size_t(i)];
+                    x[size_t(i) + 1] -= f * x[size_t(i)];
+                    b[size_t(i)] = 0.0;
+                } else {  // interchange rows i and i+1
+                    const double f = a[size_t(i)] / b[size_t(i)];
+                    a[size_t(i)] = b[size_t(i)];
+                    const double t = a[size_t(i) + 1];
+                    a[size_t(i) + 1] = y[size_t(i)] - f * t;
+                    if (i + 2 < m) {
+                        b[size_t(i)] = y[size_t(i) + 1];
+                        y[size_t(i) + 1] = -f * b[size_t(i)];
+                    } else {
+                        b[size_t(i)] = 0.0;
+                    }
+                    y[size_t(i)] = t;
+                    const double r = x[size_t(i)];
+                    x[size_t(i)] = x[size_t(i) + 1];
+                    x[size_t(i) + 1] = r - f * x[size_t(i) + 1];
+                }
+            }
+            if (a[size_t(m) - 1] == 0.0) a[size_t(m) - 1] = tiny;
+            for (int i = m - 1; i >= 0; --i) {
+                double v = x[size_t(i)];
+                if (i + 1 < m) v -= y[size_t(i)] * x[size_t(i) + 1];
+                if (i + 2 < m) v -= b[size_t(i)] * x[size_t(i) + 2];
+                x[size_t(i)] = v / a[size_t(i)];
+            }
+            double nrm = 0.0;
+            for (int i = 0; i < m; ++i) nrm += x[size_t(i)] * x[size_t(i)];
+            nrm = std::sqrt(nrm);
+            if (!(nrm > 0.0) || !std::isfinite(nrm)) return false;
+            for (int i = 0; i < m; ++i) x[size_t(i)] /= nrm;
+        }
+        zlast[j] = x[size_t(m) - 1];
+    }
+    return true;
+}
+
 // One implicitly shifted symmetric QR step (bulge chase) with shift mu:
 // T <- G^T T G, where G = G_0 ... G_{m-2} is the orthogonal factor of the QR
 // decomposition of T - mu I (implicit-Q theorem); G's rotations are appended

@@ -139,7 +139,8 @@ constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (co
 // i-1, the two the finalize reads, are zeroed.
 __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, int rbk, int t,
                                                 double* __restrict__ part, const double* nred,
-                                                unsigned* __restrict__ gctr, double* __restrict__ h_out) {
+                                                unsigned* __restrict__ gctr, double* __restrict__ h_out,
+                                                double* __restrict__ fn2_fast) {
     const int tot = ncols + has_u0, i = ncols - 1;
     __syncthreads();  // nred complete
     const double nb = (nred[0] + nred[1]) + (nred[2] + nred[3]);
@@ -178,7 +179,10 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
         }
 #pragma unroll
         for (int o = 1; o < CS_LANES; o <<= 1) a += __shfl_xor(a, o, 64);
-        if (t == 0) h_out[tot] = a;
+        if (t == 0) {
+            h_out[tot] = a;
+            if (fn2_fast) *fn2_fast = a;  // ||f||^2 = ||f'||^2 for the next SpMV (the update has nothing to do)
+        }
     }
     if (t < GT_SUB + 1) gctr[t * 64] = 0u;  // re-armed (column group 0's counters)
 }
@@ -192,7 +196,8 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
                                                double* __restrict__ fp, int nrm, float* __restrict__ v32col,
                                                const double* __restrict__ apart, int nparts,
                                                double* __restrict__ alpha_pub, unsigned* __restrict__ gctr,
-                                               double* __restrict__ h_out, const int* __restrict__ flag) {
+                                               double* __restrict__ h_out, const int* __restrict__ flag,
+                                               double* __restrict__ fn2_fast) {
     __shared__ double red[4][GT_COLS];
     __shared__ double nred[4];
     __shared__ double lds4[4];
@@ -200,13 +205,15 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     const int t = threadIdx.x;
     const int ncg = (ncols + has_u0 + GT_COLS - 1) / GT_COLS;
     const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-    const int v = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-    const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
     // partial reorthogonalisation (k_pro's decision for this step, uniform
     // over the launch): a step that does not project only forms f' and its
-    // ||f'||^2 partials (column group 0); the other column groups have no work
+    // ||f'||^2 partials (column group 0); the other column groups have no
+    // work.  Then the first nrb workgroups — the first dispatched — take the
+    // row blocks in order, and the rest return at once
     const bool skip = flag && *flag == 0;
-    if (skip && j0 != 0) return;
+    if (skip && orig >= nrb) return;
+    const int v = skip ? orig * ncg : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+    const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
     double acc[GT_COLS];
 #pragma unroll
     for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
         if ((t & 63) == 0) nred[t >> 6] = s;
     }
     if (skip) {
-        gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr, h_out);
+        gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr, h_out, fn2_fast);
         return;
     }
 #pragma unroll
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     // partial reorthogonalisation: a step k_pro left unprojected keeps f = f'
     // (the projection kernel stored it); ||f||^2 = ||f'||^2 (h[tot]) for the
     // next SpMV
-    if (flag && *flag == 0) {
+    if (flag && *flag == 0) {  // (the projection's hand-off already wrote it; with k_reduce_cols, here)
         if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = h[ncols + has_u0];
         return;
     }
@@ -908,19 +915,49 @@ __global__ __launch_bounds__(256) void k_pro(const double* __restrict__ apart, c
     double* onew = omega + size_t((i + 1) % 3) * OMEGA_LD;       // omega_{i+1}
     double* ocur = omega + size_t(i % 3) * OMEGA_LD;             // omega_i
     const double* oprev = omega + size_t((i + 2) % 3) * OMEGA_LD;  // omega_{i-1}
-    // alpha in k_three_term's order (the bits of every other alpha path), ||w||^2 alike
-    const double sa = block_sum256(strided_sum256(apart, nparts), lds4);
-    const double sw = block_sum256(strided_sum256(wpart, nparts), lds4);
+    // the recurrence's operands do not depend on the sums: their loads go out
+    // first, so they return while the partials are reduced
+    double r_al = 0.0, r_o0 = 0.0, r_o1 = 0.0, c_m1 = 0.0, c_0 = 0.0, c_p1 = 0.0, p_0 = 0.0;
+    if (t < i) {
+        r_al = alpha[t];
+        r_o1 = t + 1 < i ? offd[t + 1] : 0.0;
+        r_o0 = t > 0 ? offd[t] : 0.0;
+        c_m1 = t > 0 ? ocur[t - 1] : 0.0;
+        c_0 = ocur[t];
+        c_p1 = t + 1 < i ? ocur[t + 1] : 1.0;  // (omega_{i,i} = 1)
+        p_0 = t < i - 1 ? oprev[t] : 1.0;      // (omega_{i-1,i-1} = 1)
+    } else if (t == 255) {
+        c_0 = ocur[MAX_NCV];
+        p_0 = oprev[MAX_NCV];
+    }
+    double s_an = 0.0, s_f2 = 0.0, s_bo = 0.0;
+    int s_fo = 0;
     if (t == 0) {
+        s_an = st->anorm;
+        s_fo = st->force;
+        s_f2 = *fn2_i;
+        s_bo = *bov_i;
+    }
+    // alpha in k_three_term's order (the bits of every other alpha path), ||w||^2 alike
+    // (both trees in one pass: wave sums, then one barrier for the cross-wave adds)
+    double sa = wave_sum(strided_sum256(apart, nparts)), sw = wave_sum(strided_sum256(wpart, nparts));
+    if ((t & 63) == 0) {
+        lds4[t >> 6] = sa;
+        mx4[t >> 6] = sw;
+    }
+    __syncthreads();
+    if (t == 0) {
+        sa = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+        sw = (mx4[0] + mx4[1]) + (mx4[2] + mx4[3]);
         const double a = sa;
         *a3 = a;
-        const double b = i > 0 ? (isnan(*bov_i) ? sqrt(*fn2_i) : *bov_i) : 0.0;
+        const double b = i > 0 ? (isnan(s_bo) ? sqrt(s_f2) : s_bo) : 0.0;
         const double b2 = sw - a * a - b * b;
         const bool valid = b2 > 0x1p-20 * sw;  // false for NaN
         const double bn = valid ? sqrt(b2) : 0.0;
-        const double an = fmax(st->anorm, fabs(a) + b + bn);
+        const double an = fmax(s_an, fabs(a) + b + bn);
         st->anorm = an;
-        const int pair = st->force || i == seg0;  // the first step of a run starts a pair like a triggered one
+        const int pair = s_fo || i == seg0;  // the first step of a run starts a pair like a triggered one
         sh[0] = a;
         sh[1] = b;
         sh[2] = bn;
@@ -935,16 +972,17 @@ __global__ __launch_bounds__(256) void k_pro(const double* __restrict__ apart, c
     if (!forced) {
         if (t < i) {
             const int j = t;
-            double x = j + 1 < i ? offd[j + 1] * ocur[j + 1] : b;  // (omega_{i,i} = 1)
-            x += (alpha[j] - a) * ocur[j];
-            if (j > 0) x += offd[j] * ocur[j - 1];
-            x -= b * (j < i - 1 ? oprev[j] : 1.0);  // (omega_{i-1,i-1} = 1)
+            double x = j + 1 < i ? r_o1 * c_p1 : b;  // (omega_{i,i} = 1)
+            x += (r_al - a) * c_0;
+            if (j > 0) x += r_o0 * c_m1;
+            x -= b * p_0;
             nv = (x + copysign(eps1 * an, x)) / bn;
         } else if (t == 255) {
-            const double x = -a * ocur[U] - b * oprev[U];
+            const double x = -a * c_0 - b * p_0;
             nv = (x + copysign(eps1 * an, x)) / bn;
         }
     }
+    __syncthreads();  // (mx4 held ||w||^2's wave sums)
     double mx = fabs(nv);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
@@ -1115,23 +1153,23 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
     if (nt)
         hipLaunchKernelGGL((k_gemvt<false, true>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
-                           h_out, nullptr);
+                           h_out, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_gemvt<false, false>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
-                           h_out, nullptr);
+                           h_out, nullptr, nullptr);
 }
 
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
-              unsigned* gctr, double* h_out, bool nt, const int* flag) {
+              unsigned* gctr, double* h_out, bool nt, const int* flag, double* fn2_fast) {
     const int cols = ncols + has_u0;
     const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS));
 #define EK_GEMVT_TT(NT_, APE_)                                                                                    \
     hipLaunchKernelGGL((k_gemvt<true, NT_, APE_>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, \
                        part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, (v32col || flag) ? 1 : 0, v32col, \
-                       apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out, flag)
+                       apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out, flag, fn2_fast)
     const bool wide = apart && nparts > 12 * 256;  // 24 partials a thread (up to 6,144; beyond: strided_sum256)
     if (nt) {
         if (wide) EK_GEMVT_TT(true, 24);

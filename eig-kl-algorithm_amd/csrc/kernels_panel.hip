@@ -384,12 +384,22 @@ void spmv_panel(hipStream_t s, const SpmvPanel& m, const double* dict, const dou
                 const double* f, double* vcol, double* apart, const StepFin* fin, hipEvent_t ev_start,
                 hipEvent_t ev_stop, double* alpha_out, unsigned* actr) {
     const StepFin fv = fin ? *fin : StepFin{};
+    const size_t lds = panel_lds_bytes(m.max_rows, m.ndict);
+    if (!ev_start && !ev_stop) {  // a plain launch: the one a captured HIP graph records
+        if (m.ndict <= PANEL_LDS_DICT)
+            hipLaunchKernelGGL((k_spmv_panel<true>), dim3(m.G), dim3(PT), lds, s, m, dict, x, y, fn2, f, vcol, apart, fv,
+                               alpha_out, actr);
+        else
+            hipLaunchKernelGGL((k_spmv_panel<false>), dim3(m.G), dim3(PT), lds, s, m, dict, x, y, fn2, f, vcol, apart,
+                               fv, alpha_out, actr);
+        return;
+    }
     if (m.ndict <= PANEL_LDS_DICT)
-        hipExtLaunchKernelGGL(k_spmv_panel<true>, dim3(m.G), dim3(PT), panel_lds_bytes(m.max_rows, m.ndict), s, ev_start,
-                              ev_stop, 0, m, dict, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);
+        hipExtLaunchKernelGGL(k_spmv_panel<true>, dim3(m.G), dim3(PT), lds, s, ev_start, ev_stop, 0, m, dict, x, y, fn2,
+                              f, vcol, apart, fv, alpha_out, actr);
     else
-        hipExtLaunchKernelGGL(k_spmv_panel<false>, dim3(m.G), dim3(PT), panel_lds_bytes(m.max_rows, m.ndict), s,
-                              ev_start, ev_stop, 0, m, dict, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);
+        hipExtLaunchKernelGGL(k_spmv_panel<false>, dim3(m.G), dim3(PT), lds, s, ev_start, ev_stop, 0, m, dict, x, y,
+                              fn2, f, vcol, apart, fv, alpha_out, actr);
 }
 
 }  // namespace dev

@@ -318,9 +318,17 @@ void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const dou
     const double* v = m.pk ? m.dict : m.val;
     // with events: HIP records the kernel's own start/end timestamps (what
     // rocprofv3 reports), not event packets around it
-#define EK_SPMV_LAUNCH(BN, PK)                                                                                 \
-    hipExtLaunchKernelGGL(k_spmv_adaptive<BN, PK>, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, ev_start, ev_stop, 0, \
-                          d, m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv, alpha_out, actr)
+    // (without events a plain launch: the one a captured HIP graph records)
+#define EK_SPMV_LAUNCH(BN, PK)                                                                                     \
+    do {                                                                                                           \
+        if (ev_start || ev_stop)                                                                                   \
+            hipExtLaunchKernelGGL(k_spmv_adaptive<BN, PK>, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, ev_start,    \
+                                  ev_stop, 0, d, m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv,  \
+                                  alpha_out, actr);                                                                \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_spmv_adaptive<BN, PK>), dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, d, m.rowptr, c, \
+                               v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);               \
+    } while (0)
     if (m.pk) {
         EK_SPMV_LAUNCH(SPMV_SEG_NNZ, true);
     } else {

@@ -183,7 +183,9 @@ int64_t ek_spmv_bytes(ek_ctx* ctx);
 int ek_spmv_format(ek_ctx* ctx, int32_t* packed, int64_t* stored_bytes);
 /* Back-to-back SpMV launches on context-owned buffers, timed with HIP events
  * around the batch: *avg_us = average per launch (a sharded context: this
- * rank's rows over the all-gather layout, no collective).  fused = 1 times the
+ * rank's rows over the all-gather layout, no collective).  fused = 2: also the
+ * solve's folded finalize and ||w||^2 partials (the SpMV as the Lanczos step
+ * launches it).  fused = 1 times the
  * Lanczos form (y scaled by 1/||x||, basis column + alpha partials written:
  * + 16*nrows bytes over ek_spmv_bytes).  Measurement helper for bench.py's
  * size sweep; no reference counterpart. */

@@ -12,6 +12,8 @@ the GPU itself, each pass a process of its own):
                            pass whose average SpMV duration the line's
                            roofline uses.
 
+  b2b MULT SEED [fused]    200 back-to-back launches on resident buffers
+                           (ek_spmv_bench; fused: the Lanczos epilogue)
   shard MULT SEED N        rank 0's rows of the N-rank nnz-balanced shard map
                            (ek_spmv_setup_pins computes it without a
                            collective), 200 back-to-back fused SpMV launches
@@ -34,7 +36,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     args = sys.argv[1:]
-    mode = args.pop(0) if args and args[0] in ("resident", "file", "shard") else "resident"
+    mode = args.pop(0) if args and args[0] in ("resident", "file", "shard", "b2b") else "resident"
     lcc = args[0].endswith("lcc")
     mult, seed = float(args[0][:-3] if lcc else args[0]), int(args[1])
     spec = importlib.util.spec_from_file_location("eigkl_amd", os.path.join(REPO, "eig-kl-algorithm_amd", "__init__.py"))
@@ -55,6 +57,11 @@ def main():
         us = ctx.spmv_bench(200, fused=True)
         _, r0, nr = ctx.spmv_dims()
         print(f"probe: rank 0 of {nranks}: rows {r0}..{r0 + nr}, {us:.2f} us per SpMV", flush=True)
+    elif mode == "b2b":  # 200 back-to-back SpMV launches (fused: the Lanczos epilogue), resident matrix and x
+        ctx.spmv_setup_pins(h)
+        fused = {"fused": 1, "solve": 2}.get(args[2] if len(args) > 2 else "", 0)
+        us = ctx.spmv_bench(200, fused=fused)
+        print(f"probe: back to back (fused={fused}) {us:.2f} us per SpMV", flush=True)
     elif mode == "resident":
         ctx.spmv_setup_pins(h)
         for _ in range(int(args[2]) if len(args) > 2 else 1):  # (optional: solves in a row)
