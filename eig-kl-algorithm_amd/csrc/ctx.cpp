@@ -1751,8 +1751,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         for (int i = 0; i < m; ++i) a = std::max(a, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
         return a;
     };
-    // the sharded step's re-projection of a cancelled f' (Lanczos::repair)
-    const bool mr_step = c->mr && L.reorth == 1;
+    // the sharded step's re-projection of a cancelled f' (Lanczos::repair);
+    // EK_LANCZOS_UNFUSED runs that step (and its flags) on a single context too
+    const bool mr_step = (c->mr || std::getenv("EK_LANCZOS_UNFUSED") != nullptr) && L.reorth == 1;
     // the owned-slot / halo split of the sharded SpMV (EK_MR_OVERLAP=0: one
     // SpMV after the all-gather, the round-3 step; A/B and tests)
     {
@@ -1760,7 +1761,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         L.overlap = c->mr && c->own_ready && !(e && e[0] == '0');
     }
     if (mr_step) {
-        c->cflag.ensure(size_t(m + 2) * 8);
+        c->cflag.ensure(size_t(m + 2) * 8);  // (update_mr writes one flag per step)
         if (const char* e = std::getenv("EK_MR_CANCEL"); e && e[0]) L.mr_cancel = std::atof(e);  // (tests)
     }
     for (;;) {
