@@ -9,7 +9,7 @@
 # Output: gpurun_out/kl_budget/.
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
-OUT="$ROOT/gpurun_out/kl_budget"
+OUT="$ROOT/gpurun_out/${KL_BUDGET_DIR:-kl_budget}"
 mkdir -p "$OUT"
 timeout -k 10 120 python3 "$ROOT/tools/kl_prof.py" > "$OUT/prof.txt" 2>&1
 cd /tmp
