@@ -4,6 +4,7 @@
 //     InitializeSparsMatrix (cKL.cpp:84-149) + the iteration order of its
 //     std::unordered_map<uint32_t,float> rows, emulated
 //     here so the product does not depend on the host's libstdc++.
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstring>
@@ -42,15 +43,24 @@ uint64_t hashtable_next_buckets(uint64_t cur) {
 //     whose new bucket is empty goes to the front (and the previous front's
 //     bucket is re-pointed at it); otherwise after its bucket's before node.
 void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch) {
+    std::vector<int32_t> b0, b1;
+    hashtable_order(keys, cnt, out, scratch, b0, b1);
+}
+// (bk0 / bk1: the bucket arrays, reused across calls: no allocation per row)
+void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch,
+                     std::vector<int32_t>& bk0, std::vector<int32_t>& bk1) {
     constexpr int32_t NIL = -1, BB = -2, EMPTY = -3;
     if (cnt == 0) return;
     scratch.resize(size_t(cnt));
     int32_t* next = scratch.data();
-    std::vector<int32_t> bucket(1, EMPTY);
+    std::vector<int32_t>* cur_b = &bk0;
+    std::vector<int32_t>* spare = &bk1;
+    cur_b->assign(1, EMPTY);
     uint64_t B = 1, next_resize = 0, count = 0;
     int32_t head = NIL;
     auto rehash = [&](uint64_t nb) {
-        std::vector<int32_t> nbk(nb, EMPTY);
+        std::vector<int32_t>& nbk = *spare;
+        nbk.assign(nb, EMPTY);
         int32_t p = head;
         head = NIL;
         uint64_t bbegin = 0;
@@ -72,7 +82,7 @@ void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vect
             }
             p = nx;
         }
-        bucket.swap(nbk);
+        std::swap(cur_b, spare);
         B = nb;
     };
     for (int64_t i = 0; i < cnt; ++i) {
@@ -97,17 +107,17 @@ void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vect
         }
         const int32_t node = int32_t(i);
         const uint64_t b = keys[i] % B;
-        if (bucket[b] == EMPTY) {
+        if ((*cur_b)[b] == EMPTY) {
             next[node] = head;
             head = node;
-            if (next[node] != NIL) bucket[keys[next[node]] % B] = node;
-            bucket[b] = BB;
-        } else if (bucket[b] == BB) {
+            if (next[node] != NIL) (*cur_b)[keys[next[node]] % B] = node;
+            (*cur_b)[b] = BB;
+        } else if ((*cur_b)[b] == BB) {
             next[node] = head;
             head = node;
         } else {
-            next[node] = next[bucket[b]];
-            next[bucket[b]] = node;
+            next[node] = next[(*cur_b)[b]];
+            next[(*cur_b)[b]] = node;
         }
         ++count;
     }
@@ -280,123 +290,205 @@ void build_laplacian(const ek_hgr& h, ek_csr& L) { build_laplacian_rows(h, 0, h.
 
 // ---------------------------------------------------------------------------
 // cKL.cpp:107-131 + connections() order (cKL.cpp:229-248).
+// Every phase parallel, no atomics, no per-row allocations (round 4; the
+// round-3 form counted and filled one global pair list net by net on one
+// thread and kept a std::vector per row: ~20 ms on the box's host, against a
+// ~22 ms Lanczos solve it has to hide behind).  Thread t owns the nets
+// [nets t/T, nets (t+1)/T) in phase A and the rows [n t/T, n (t+1)/T) in
+// phases B and C; per-thread counts (T x n, one array reused) give every
+// thread its own slots, in thread order:
+//   A. pairs (j < q) of every net, filed under their smaller endpoint: a row's
+//      slots from thread t precede thread t+1's, and each thread walks its
+//      nets in order, so every row's pairs lie in the reference's loop order;
+//   B. per row: its pairs stable-sorted by key (each key's pairs in loop
+//      order, summed in fp32 in that order); the keys in first-pair order
+//      (the map's insertion order) through the emulated map iteration, into
+//      the thread's own buffer;
+//   C. forward parts copied into place; backward parts (for node k, the rows
+//      i < k holding k) scattered to per-thread slots, which puts them in
+//      ascending row order without a sort.
+// The result is the round-3 form's, bit for bit (test_kl_graph_matches_oracle,
+// test_kl_row_order_*, test_kl_graph_repeated_pins).
 void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     PhaseTimer pt("kl_graph");
-    const int64_t n = h.nodes;
-    // 1. upper-triangle pairs per row (min endpoint), in net order
-    std::vector<int64_t> cnt(size_t(n) + 1, 0);
-    for (int64_t e = 0; e < h.nets; ++e) {
-        const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
-        for (int64_t j = 0; j + 1 < k; ++j)
-            for (int64_t q = j + 1; q < k; ++q) {
-                const int32_t a = h.pins[size_t(p0 + j)], b = h.pins[size_t(p0 + q)];
-                cnt[size_t(std::min(a, b)) + 1]++;
+    const int64_t n = h.nodes, nets = h.nets;
+    const int T = int(std::max<int64_t>(1, std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 4096))));
+    dvec<int32_t> loc(static_cast<size_t>(T) * static_cast<size_t>(n));  // per-thread counts, then slots (within a row)
+    auto zero_loc = [&](int t) {
+        std::memset(loc.data() + size_t(t) * size_t(n), 0, size_t(n) * sizeof(int32_t));
+    };
+    // A. pairs by smaller endpoint
+    run_threads(T, [&](int t) {
+        zero_loc(t);
+        int32_t* c = loc.data() + size_t(t) * size_t(n);
+        for (int64_t e = nets * t / T; e < nets * (t + 1) / T; ++e) {
+            const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
+            const int32_t* pe = h.pins.data() + p0;
+            for (int64_t j = 0; j + 1 < k; ++j)
+                for (int64_t q = j + 1; q < k; ++q) ++c[std::min(pe[j], pe[q])];
+        }
+    });
+    dvec<int64_t> cnt(static_cast<size_t>(n) + 1);
+    run_threads(T, [&](int t) {  // per row: the total, and each thread's slot base relative to the row
+        for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+            int64_t run = 0;
+            for (int u = 0; u < T; ++u) {
+                int32_t& x = loc[size_t(u) * size_t(n) + size_t(r)];
+                const int64_t v = x;
+                x = int32_t(run);
+                run += v;
             }
-    }
+            cnt[size_t(r) + 1] = run;
+        }
+    });
+    cnt[0] = 0;
     for (int64_t i = 0; i < n; ++i) cnt[size_t(i) + 1] += cnt[size_t(i)];
-    std::vector<uint32_t> pk(size_t(cnt[size_t(n)]));
-    std::vector<float> pw(size_t(cnt[size_t(n)]));
-    {
-        std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
-        for (int64_t e = 0; e < h.nets; ++e) {
+    const int64_t npairs = cnt[size_t(n)];
+    dvec<uint32_t> pk(static_cast<size_t>(npairs));
+    dvec<float> pw(static_cast<size_t>(npairs));
+    run_threads(T, [&](int t) {
+        int32_t* c = loc.data() + size_t(t) * size_t(n);
+        for (int64_t e = nets * t / T; e < nets * (t + 1) / T; ++e) {
             const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
             if (k < 2) continue;
             const float weight = 1.0f / float(k - 1);  // cKL.cpp:117
+            const int32_t* pe = h.pins.data() + p0;
             for (int64_t j = 0; j + 1 < k; ++j)
                 for (int64_t q = j + 1; q < k; ++q) {
-                    int32_t a = h.pins[size_t(p0 + j)], b = h.pins[size_t(p0 + q)];
-                    if (a > b) std::swap(a, b);
-                    pk[size_t(cur[size_t(a)])] = uint32_t(b);
-                    pw[size_t(cur[size_t(a)]++)] = weight;
+                    const int32_t a = std::min(pe[j], pe[q]), b = std::max(pe[j], pe[q]);
+                    const int64_t at = cnt[size_t(a)] + c[a]++;
+                    pk[size_t(at)] = uint32_t(b);
+                    pw[size_t(at)] = weight;
                 }
         }
-    }
-    // 2. per row: distinct keys in first-insertion order, fp32 sums in net order
-    //    (adjacencyList[a][b] += w), then the emulated map iteration order.
-    std::vector<int32_t> fcnt(size_t(n), 0);
-    std::vector<std::vector<std::pair<uint32_t, float>>> fwd(static_cast<size_t>(n));
+    });
+    pt.mark("pairs");
+    // B. rows: forward lists in map order, per thread, rows in order
+    struct Part {
+        std::vector<uint32_t> key;
+        std::vector<float> w;
+        std::vector<int64_t> off;  // row r's entries at [off[r - lo], off[r - lo + 1])
+    };
+    std::vector<Part> parts(static_cast<size_t>(T));
+    dvec<int32_t> fcnt(static_cast<size_t>(n));
     std::atomic<bool> too_big{false};
-    parallel_for(n, [&](int64_t lo, int64_t hi) {
+    run_threads(T, [&](int t) {
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        Part& P = parts[size_t(t)];
+        P.off.assign(size_t(hi - lo) + 1, 0);
+        P.key.clear();
+        P.w.clear();
+        P.key.reserve(size_t(cnt[size_t(hi)] - cnt[size_t(lo)]));
+        P.w.reserve(size_t(cnt[size_t(hi)] - cnt[size_t(lo)]));
+        zero_loc(t);  // (now: this thread's backward counts per node)
+        int32_t* bc = loc.data() + size_t(t) * size_t(n);
         std::vector<int64_t> idx;
-        std::vector<std::pair<int64_t, std::pair<uint32_t, float>>> first;  // (first seq, (key, sum))
+        std::vector<int32_t> scratch, bk0, bk1;
+        std::vector<std::pair<int64_t, std::pair<uint32_t, float>>> first;  // (first pair, (key, sum))
         std::vector<uint32_t> keys, order;
-        std::vector<int32_t> scratch;
-        for (int64_t r = lo; r < hi; ++r) {
-            const int64_t b = cnt[size_t(r)], e = cnt[size_t(r) + 1];
-            if (b == e) continue;
+        std::vector<std::pair<uint32_t, float>> bykey;
+        for (int64_t a = lo; a < hi; ++a) {
+            const int64_t b = cnt[size_t(a)], e = cnt[size_t(a) + 1];
+            if (b == e) {
+                P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
+                fcnt[size_t(a)] = 0;
+                continue;
+            }
             idx.resize(size_t(e - b));
             std::iota(idx.begin(), idx.end(), b);
-            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return pk[size_t(x)] < pk[size_t(y)]; });
+            // (std::stable_sort allocates a merge buffer per call: small rows
+            // take a stable insertion sort instead)
+            if (idx.size() <= 48) {
+                for (size_t u = 1; u < idx.size(); ++u) {
+                    const int64_t x = idx[u];
+                    const uint32_t kx = pk[size_t(x)];
+                    size_t v = u;
+                    for (; v > 0 && pk[size_t(idx[v - 1])] > kx; --v) idx[v] = idx[v - 1];
+                    idx[v] = x;
+                }
+            } else {
+                std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return pk[size_t(x)] < pk[size_t(y)]; });
+            }
             first.clear();
-            for (size_t t = 0; t < idx.size();) {
-                const uint32_t key = pk[size_t(idx[t])];
-                float s = 0.0f;  // operator[] value-initialises to 0.0f, then += in net order
-                const int64_t seq0 = idx[t];
-                for (; t < idx.size() && pk[size_t(idx[t])] == key; ++t) s += pw[size_t(idx[t])];
-                first.push_back({seq0, {key, s}});
+            bykey.clear();
+            for (size_t u = 0; u < idx.size();) {
+                const uint32_t key = pk[size_t(idx[u])];
+                float sum = 0.0f;  // operator[] value-initialises to 0.0f, then += in net order
+                const int64_t seq0 = idx[u];
+                for (; u < idx.size() && pk[size_t(idx[u])] == key; ++u) sum += pw[size_t(idx[u])];
+                first.push_back({seq0, {key, sum}});
+                bykey.push_back({key, sum});  // (ascending keys)
             }
             std::sort(first.begin(), first.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
             keys.resize(first.size());
-            for (size_t t = 0; t < first.size(); ++t) keys[t] = first[t].second.first;
+            for (size_t u = 0; u < first.size(); ++u) keys[u] = first[u].second.first;
             order.resize(keys.size());
             try {
-                hashtable_order(keys.data(), int64_t(keys.size()), order.data(), scratch);
+                hashtable_order(keys.data(), int64_t(keys.size()), order.data(), scratch, bk0, bk1);
             } catch (const Error&) {
                 too_big = true;
-                continue;
+                return;
             }
-            // map key -> summed weight (keys are distinct): sort a copy by key
-            std::vector<std::pair<uint32_t, float>> bykey(first.size());
-            for (size_t t = 0; t < first.size(); ++t) bykey[t] = first[t].second;
-            std::sort(bykey.begin(), bykey.end());
-            auto& out = fwd[size_t(r)];
-            out.resize(order.size());
-            for (size_t t = 0; t < order.size(); ++t) {
-                auto it = std::lower_bound(bykey.begin(), bykey.end(), std::make_pair(order[t], -INFINITY));
-                out[t] = *it;
+            for (uint32_t key : order) {
+                const auto it = std::lower_bound(bykey.begin(), bykey.end(), std::make_pair(key, -INFINITY));
+                P.key.push_back(key);
+                P.w.push_back(it->second);
+                if (int64_t(key) != a) ++bc[key];
             }
-            fcnt[size_t(r)] = int32_t(out.size());
+            fcnt[size_t(a)] = int32_t(order.size());
+            P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
         }
     });
     if (too_big) fail(EK_EINVAL, "hash-order emulation: a row exceeds the bucket table");
-    pt.mark("pairs + map order");
-    std::vector<float>().swap(pw);
-    std::vector<uint32_t>().swap(pk);
-    // 3. backward lists: for rows i ascending, (i, w) appended to key k's list
-    std::vector<int64_t> bcnt(size_t(n) + 1, 0);
-    for (int64_t i = 0; i < n; ++i)
-        for (auto& [k, w] : fwd[size_t(i)])
-            if (int64_t(k) != i) bcnt[size_t(k) + 1]++;
-    for (int64_t i = 0; i < n; ++i) bcnt[size_t(i) + 1] += bcnt[size_t(i)];
+    pt.mark("rows + map order");
+    // C. assemble
+    dvec<int64_t> bcnt(static_cast<size_t>(n));
+    run_threads(T, [&](int t) {  // per node: backward total, each thread's slot base relative to its list
+        for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
+            int64_t run = 0;
+            for (int u = 0; u < T; ++u) {
+                int32_t& x = loc[size_t(u) * size_t(n) + size_t(r)];
+                const int64_t v = x;
+                x = int32_t(run);
+                run += v;
+            }
+            bcnt[size_t(r)] = run;
+        }
+    });
     G.nrows = n;
     G.value_bytes = 4;
-    G.rowptr.assign(size_t(n) + 1, 0);
-    G.nfwd.assign(fcnt.begin(), fcnt.end());
+    G.rowptr.resize(size_t(n) + 1);
+    G.nfwd.resize(size_t(n));
+    G.rowptr[0] = 0;
     for (int64_t r = 0; r < n; ++r) {
-        const int64_t len = int64_t(fcnt[size_t(r)]) + (bcnt[size_t(r) + 1] - bcnt[size_t(r)]);
+        const int64_t len = int64_t(fcnt[size_t(r)]) + bcnt[size_t(r)];
         if (int64_t(G.rowptr[size_t(r)]) + len > INT32_MAX) fail(EK_EINVAL, "KL graph nnz exceeds int32");
         G.rowptr[size_t(r) + 1] = G.rowptr[size_t(r)] + int32_t(len);
     }
     G.col.resize(size_t(G.rowptr[size_t(n)]));
     G.val32.resize(size_t(G.rowptr[size_t(n)]));
-    parallel_for(n, [&](int64_t lo, int64_t hi) {
-        for (int64_t r = lo; r < hi; ++r) {
+    run_threads(T, [&](int t) {
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        const Part& P = parts[size_t(t)];
+        int32_t* bs = loc.data() + size_t(t) * size_t(n);
+        for (int64_t r = lo; r < hi; ++r) {  // forward part
+            G.nfwd[size_t(r)] = fcnt[size_t(r)];
             int64_t p = G.rowptr[size_t(r)];
-            for (auto& [k, w] : fwd[size_t(r)]) {
-                G.col[size_t(p)] = int32_t(k);
-                G.val32[size_t(p++)] = w;
+            for (int64_t q = P.off[size_t(r - lo)]; q < P.off[size_t(r - lo) + 1]; ++q) {
+                G.col[size_t(p)] = int32_t(P.key[size_t(q)]);
+                G.val32[size_t(p++)] = P.w[size_t(q)];
             }
         }
-    });
-    std::vector<int64_t> bcur(static_cast<size_t>(n));
-    for (int64_t r = 0; r < n; ++r) bcur[size_t(r)] = G.rowptr[size_t(r)] + fcnt[size_t(r)];
-    for (int64_t i = 0; i < n; ++i)
-        for (auto& [k, w] : fwd[size_t(i)])
-            if (int64_t(k) != i) {
-                G.col[size_t(bcur[k])] = int32_t(i);
-                G.val32[size_t(bcur[k]++)] = w;
+        for (int64_t r = lo; r < hi; ++r)  // backward parts: this thread's slots, rows ascending
+            for (int64_t q = P.off[size_t(r - lo)]; q < P.off[size_t(r - lo) + 1]; ++q) {
+                const int64_t k = P.key[size_t(q)];
+                if (k == r) continue;
+                const int64_t pos = G.rowptr[size_t(k)] + fcnt[size_t(k)] + bs[k]++;
+                G.col[size_t(pos)] = int32_t(r);
+                G.val32[size_t(pos)] = P.w[size_t(q)];
             }
-    pt.mark("backward + assemble");
+    });
+    pt.mark("assemble");
 }
 
 }  // namespace ek

@@ -78,6 +78,25 @@ def test_kl_graph_matches_oracle(ek, oracle, name):
     assert np.array_equal(G.val.view(np.uint32), w.view(np.uint32))  # fp32 bit-exact (cKL.cpp:117-128)
 
 
+def test_kl_graph_repeated_pins(ek, oracle, tmp_path):
+    """Nets that repeat a pin (self pairs, the (j < q) loop's order across the
+    repeats), nets of size 1 and a 1,500-pin net, against the oracle
+    restatement of InitializeSparsMatrix (cKL.cpp:84-149), bit for bit."""
+    rng = np.random.default_rng(11)
+    n = 2000
+    nets = [np.array([3, 7, 3]), np.array([5, 5]), np.array([1, 2, 3, 1, 9]), np.array([8]), np.array([9, 4, 9, 4, 9])]
+    nets += [rng.integers(0, n, size=int(k)) for k in rng.integers(2, 9, size=3000)]  # (unsorted, repeats possible)
+    nets.append(rng.choice(n, size=1500, replace=False))
+    net_ptr = np.concatenate([[0], np.cumsum([len(e) for e in nets])]).astype(np.int64)
+    pins = np.concatenate(nets).astype(np.int32)
+    path = str(tmp_path / "rep.hgr")
+    ek.Hypergraph.from_pins(n, net_ptr, pins).write(path)
+    G = ek.Hypergraph.read(path).kl_graph()
+    rp, col, w, nf = oracle.Graph.read(path).kl_csr()
+    assert np.array_equal(G.rowptr, rp) and np.array_equal(G.col, col) and np.array_equal(G.nfwd, nf)
+    assert np.array_equal(G.val.view(np.uint32), w.view(np.uint32))
+
+
 @pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
 def test_laplacian_matches_oracle(ek, oracle, name):
     L = ek.Hypergraph.read(circuit_path(name)).laplacian()
