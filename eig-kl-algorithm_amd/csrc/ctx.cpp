@@ -1200,6 +1200,11 @@ struct Lanczos {
     // recurrence against thresh; eps1 = eps sqrt(n), its rounding term)
     bool pro = false;
     double pro_thresh = 0.0, pro_eps1 = 0.0;
+    // the decision inside the projection launch (no k_pro launch; needs the
+    // projection's hand-off, upd_red 2).  EK_PRO_INLAUNCH=0: the k_pro launch
+    bool proi = false;
+    unsigned* pro_pub() { return reinterpret_cast<unsigned*>(c->pflags.as<char>() + pro_pub_off()); }
+    size_t pro_pub_off() const { return (size_t(m + 2) * 4 + 255) / 256 * 256; }
     float* V32() { return b32 ? c->V32.as<float>() : nullptr; }
     float* col32(int j) { return b32 ? c->V32.as<float>() + size_t(j) * ldv : nullptr; }
     int seg0 = 0;  // first step of the current run of steps (cycle start or injected vector)
@@ -1345,6 +1350,23 @@ struct Lanczos {
         const bool tt = tt_fused || pro;
         unsigned* gctr = upd_red == 2 ? c->gctr.as<unsigned>() : nullptr;
         double* hoff = upd_red == 2 ? c->h2.as<double>() : nullptr;
+        const bool inl = pro && proi && upd_red == 2;
+        static const bool pro_apart = std::getenv("EK_PRO_APART") != nullptr;  // (lab: k_pro + alpha re-reduced in the projection)
+        ek::dev::ProLaunch pl;
+        if (inl) {
+            pl.wpart = c->wpart.as<double>();
+            pl.alpha = c->alpha.as<double>();
+            pl.offd = c->offd.as<double>();
+            pl.omega = c->omega.as<double>();
+            pl.st = c->prost.as<ek::dev::ProState>();
+            pl.flags = c->pflags.as<int>();
+            pl.pub = pro_pub();
+            pl.a3 = a3;
+            pl.seg0 = seg0;
+            pl.m = m;
+            pl.thresh = pro_thresh;
+            pl.eps1 = pro_eps1;
+        }
         for (int i = k; i < kend; ++i) {
             ek::dev::StepFin fin;
             if (i > seg0) {
@@ -1371,15 +1393,15 @@ struct Lanczos {
             const int nc = i + 1;
             // partial reorthogonalisation: alpha, and whether this step projects
             const int* flag = pro ? c->pflags.as<int>() + i : nullptr;
-            if (pro)
+            if (pro && !inl)
                 ek::dev::pro_step(s, c->apart.as<double>(), c->wpart.as<double>(), c->nrb_spmv, a3, fn2 + i, bov + i,
                                   c->alpha.as<double>(), c->offd.as<double>(), c->omega.as<double>(),
                                   c->prost.as<ek::dev::ProState>(), c->pflags.as<int>(), i, seg0, m, pro_thresh, pro_eps1);
             if (tt) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
                                   i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
-                                  col32(i), (alpha_last || pro) ? nullptr : c->apart.as<double>(), c->nrb_spmv, gctr, hoff,
-                                  nt, flag, pro ? fast : nullptr);
+                                  col32(i), inl || pro_apart || !(alpha_last || pro) ? c->apart.as<double>() : nullptr, c->nrb_spmv,
+                                  gctr, hoff, nt, flag, pro ? fast : nullptr, inl ? &pl : nullptr);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
                                     i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), col32(i));
@@ -1391,7 +1413,8 @@ struct Lanczos {
             // (b32: the update also leaves ||f||^2 = ||f'||^2 - ||h||^2 for the next SpMV)
             if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
-                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt, flag);
+                                c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt, flag,
+                                inl ? pro_pub() : nullptr);
             } else if (upd_red == 1) {
                 ek::dev::update_r(s, ldv, V(), nc, has_u0, u0val, nreal, c->part.as<double>(), nrb, c->h2.as<double>(),
                                   c->f.as<double>(), c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt);
@@ -1601,6 +1624,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // 44 % of the steps projected; the headline LCC 32 %, residual unchanged
     L.pro_thresh = o.reorth_thresh > 0 ? o.reorth_thresh : 1e-10;
     L.pro_eps1 = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
+    if (const char* e = std::getenv("EK_PRO_INLAUNCH"); L.pro) L.proi = !(e && e[0] == '0');
 
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);
@@ -1653,8 +1677,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         c->wpart.ensure(size_t(std::max(c->nrb_spmv, 1)) * 8);
         c->omega.ensure(3 * size_t(ek::dev::OMEGA_LD) * 8);
         c->prost.ensure(sizeof(ek::dev::ProState));
-        c->pflags.ensure(size_t(m + 2) * 4);
+        // + the in-launch decision's words (PRO_PUB lines of 256 B), zero between launches
+        c->pflags.ensure(L.pro_pub_off() + size_t(ek::dev::PRO_PUB) * 256);
         HIPCHK(hipMemsetAsync(c->prost.p, 0, sizeof(ek::dev::ProState), s));
+        HIPCHK(hipMemsetAsync(L.pro_pub(), 0, size_t(ek::dev::PRO_PUB) * 256, s));
     }
     // the step chunks' graphs (EK_LANCZOS_GRAPH=0: eager launches, A/B), kept
     // while every buffer and parameter their launches carry is unchanged
@@ -1678,7 +1704,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                                   pv(c->val.p), pv(c->rowptr.p), pv(c->pn_wrow.p), pv(c->pn_start.p), pv(c->pn_word.p),
                                   pv(c->pn_rid.p), uint64_t(m), uint64_t(L.ldv), uint64_t(L.nreal), uint64_t(c->n),
                                   uint64_t(c->nrb_spmv), uint64_t(c->pn_G), uint64_t(c->colbits), uint64_t(L.has_u0),
-                                  uint64_t(L.b32), uint64_t(L.pro), uint64_t(L.nt), uint64_t(L.alpha_last),
+                                  uint64_t(L.b32), uint64_t(L.pro), uint64_t(L.proi), uint64_t(L.nt), uint64_t(L.alpha_last),
                                   uint64_t(tt_env), db(L.pro_thresh),
                                   db(L.pro_eps1), db(L.u0val)};
         if (sig != c->lz_sig) {
@@ -2008,6 +2034,15 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                                       hipMemcpyHostToDevice, s));
         }
         HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read (and k_pro's staging)
+        if (L.pro && std::getenv("EK_PRO_TRACE")) {  // (lab: the cycle's per-step decisions)
+            std::vector<int> fl(static_cast<size_t>(m));
+            HIPCHK(hipMemcpy(fl.data(), c->pflags.p, size_t(m) * 4, hipMemcpyDeviceToHost));
+            std::string row;
+            for (int i = k; i < m; ++i) row += fl[size_t(i)] ? '1' : '0';
+            std::fprintf(stderr, "[pro] cycle from %d: %s\n", k, row.c_str());
+            for (int i = k; i < m; ++i)
+                std::fprintf(stderr, "[pro] %d d %a e %a\n", i, d[size_t(i)], i + 1 < m ? e[size_t(i)] : 0.0);
+        }
         for (int i = 0; i < knew; ++i) d[size_t(i)] = dd[size_t(i)];
         for (int i = 0; i + 1 < knew; ++i) e[size_t(i)] = ee[size_t(i)];
         k = knew;

@@ -332,8 +332,10 @@ constexpr int MAX_NCV = 128;
 // nt: the basis is read non-temporally (a basis larger than the MALL)
 // gctr / h_out (nrb <= 256): the column sums are also reduced in the launch
 // (the last workgroup of each column group; col_sum2's order) into h_out;
-// gctr: GT_HANDOFF_UINTS zeroed uints, re-armed by each launch
-constexpr int GT_HANDOFF_UINTS = ((MAX_NCV + 2 + GT_COLS - 1) / GT_COLS) * 9 * 64;
+// gctr: GT_HANDOFF_UINTS zeroed uints, re-armed by each launch (the last
+// 9 x 64: the in-launch decision form's own hand-off of the ||f'||^2 column)
+constexpr int GT_NORM_CTR = ((MAX_NCV + 2 + GT_COLS - 1) / GT_COLS) * 9 * 64;
+constexpr int GT_HANDOFF_UINTS = GT_NORM_CTR + 9 * 64;
 void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val,
            int nreal, const double* w, double* part, int nrm = 0, unsigned* gctr = nullptr, double* h_out = nullptr,
            bool nt = false);
@@ -362,7 +364,7 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col = nullptr, const double* apart = nullptr,
               int nparts = 0, unsigned* gctr = nullptr, double* h_out = nullptr, bool nt = false,
-              const int* flag = nullptr, double* fn2_fast = nullptr);
+              const int* flag = nullptr, double* fn2_fast = nullptr, const struct ProLaunch* pl = nullptr);
 // h[j] = sum_b part[j*nrb + b]  for j < ncols_total
 void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, double* h);
 
@@ -378,7 +380,8 @@ void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, do
 // dst = src - V[:, :ncols] h[:ncols] - u0 h[ncols]; optional per-block sum of dst^2 -> npart
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32 = nullptr,
-            unsigned* fb = nullptr, double* fn2_fast = nullptr, bool nt = false, const int* flag = nullptr);
+            unsigned* fb = nullptr, double* fn2_fast = nullptr, bool nt = false, const int* flag = nullptr,
+            unsigned* pub_rearm = nullptr);
 // Partial reorthogonalisation (Lanczos reorth 3; one workgroup per step,
 // between the SpMV and the projection): alpha = sum(apart) (k_three_term's
 // order: the bits every other alpha path gives) -> *a3; beta_{i+1} estimated
@@ -399,6 +402,26 @@ struct ProState {
 void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,
               const double* bov_i, const double* alpha, const double* offd, double* omega, ProState* st, int* flags,
               int i, int seg0, int m, double thresh, double eps1);
+// The decision inside the projection launch (PROI, no k_pro launch): its
+// first workgroup runs k_pro's body and publishes 1 + decision to PRO_PUB
+// words (one 256-B line each; workgroup b polls word b % 8, its XCD's); the
+// other column groups wait for it before their basis loads, column group 0
+// after forming f'.  The step's update re-arms the words (zero) for the next
+// launch.  i = ncols - 1; alpha / a3 as k_pro.
+constexpr int PRO_PUB = 8;
+constexpr int PRO_PUB_STRIDE = 64;  // uints between two words (256 B)
+struct ProLaunch {
+    const double* wpart = nullptr;
+    const double* alpha = nullptr;
+    const double* offd = nullptr;
+    double* omega = nullptr;
+    ProState* st = nullptr;
+    int* flags = nullptr;
+    unsigned* pub = nullptr;  // PRO_PUB words, zero before the launch
+    double* a3 = nullptr;
+    int seg0 = 0, m = 0;
+    double thresh = 0.0, eps1 = 0.0;
+};
 // fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
 // alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
 // alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]

@@ -60,10 +60,15 @@ void slurp(const char* path, ek::dvec<char>& buf) {
 // calls (a service re-reading circuits of similar size): fresh ones cost a
 // page fault per 4 KB on first touch, ~1 ms a read of the ibm18-shape file.
 // One caller at a time uses them; a concurrent read gets its own.
+// The result arrays (net_ptr, pins) of a freed ek_hgr come back here too
+// (ek_hgr_free) and are handed to the next read: in a solve loop the heap
+// churn between reads otherwise gave them fresh pages every time.
 struct ReadCache {
     std::mutex mu;
     ek::dvec<char> buf;
     std::vector<ek::dvec<int32_t>> part;
+    ek::dvec<int64_t> net_ptr;
+    ek::dvec<int32_t> pins;
 };
 ReadCache& read_cache() {
     static ReadCache c;
@@ -137,6 +142,10 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     });
     if (nh < 2) ek::fail(EK_EINVAL, "%s: header must be '<nets> <nodes>'", path);
     auto h = std::make_unique<ek_hgr>();
+    if (cache_lk.owns_lock()) {  // a freed result's arrays (capacity kept)
+        h->net_ptr.swap(read_cache().net_ptr);
+        h->pins.swap(read_cache().pins);
+    }
     h->nets = int64_t(hv[0]);
     h->nodes = int64_t(hv[1]);
     if (h->nodes > INT32_MAX || h->nets > INT32_MAX) ek::fail(EK_EINVAL, "%s: sizes exceed int32", path);
@@ -374,6 +383,19 @@ int ek_hgr_copy_pins(const ek_hgr* h, int64_t* net_ptr, int32_t* pins) {
     return EK_OK;
 }
 
-void ek_hgr_free(ek_hgr* h) { delete h; }
+void ek_hgr_free(ek_hgr* h) {
+    if (!h) return;
+    {
+        ReadCache& c = read_cache();
+        std::unique_lock<std::mutex> lk(c.mu, std::try_to_lock);
+        if (lk.owns_lock()) {  // keep the larger arrays for the next read
+            if (h->net_ptr.capacity() > c.net_ptr.capacity()) c.net_ptr.swap(h->net_ptr);
+            if (h->pins.capacity() > c.pins.capacity()) c.pins.swap(h->pins);
+            c.net_ptr.clear();
+            c.pins.clear();
+        }
+    }
+    delete h;
+}
 
 }  // extern "C"

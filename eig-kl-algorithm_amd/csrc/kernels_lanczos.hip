@@ -11,6 +11,9 @@
 // whose float atomicAdd norm is replaced by deterministic fp64 trees.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "ek_internal.hpp"
 
 #ifndef EK_UPD_UB
@@ -44,6 +47,29 @@ __device__ __forceinline__ double strided_sum256(const double* __restrict__ x, i
         for (int u = 0; u < SB; ++u) s += i0 + u * 256 < n ? v[u] : 0.0;
     }
     return s;
+}
+
+// strided_sum256 of two arrays at once: both arrays' loads in flight together
+// (one round trip instead of two); each sum in strided_sum256's order
+__device__ __forceinline__ void strided_sum256x2(const double* __restrict__ x, const double* __restrict__ y, int n,
+                                                 double& sx, double& sy) {
+    constexpr int SB = 16;
+    sx = 0.0;
+    sy = 0.0;
+    if (n <= 0) return;
+    for (int i0 = threadIdx.x; i0 < n; i0 += SB * 256) {
+        double vx[SB], vy[SB];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            vx[u] = x[min(i0 + u * 256, n - 1)];
+            vy[u] = y[min(i0 + u * 256, n - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            sx += i0 + u * 256 < n ? vx[u] : 0.0;
+            sy += i0 + u * 256 < n ? vy[u] : 0.0;
+        }
+    }
 }
 
 #ifndef EK_TT_ROWS
@@ -130,6 +156,133 @@ constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (co
 // each row block also writes ||rhs||^2 over its rows to part column
 // ncols + has_u0 (the update's accuracy test reads the sum), and with TT
 // the fp32 copy of v_i to v32col (vi rows are loaded here anyway).
+// Partial reorthogonalisation: the decision for step i (ek_internal.hpp
+// pro_step).  Simon's omega recurrence (Simon 1984; PROPACK's update_mu) for
+// omega_{i+1,j} ~ v_{i+1}^T v_j:
+//   beta_{i+1} omega_{i+1,j} = beta_{j+1} omega_{i,j+1} + (alpha_j - alpha_i) omega_{i,j}
+//                              + beta_j omega_{i,j-1} - beta_i omega_{i-1,j}  (+- eps1 ||L||)
+// with omega_{k,k} = 1; against u0 (L u0 = 0) the same with alpha_j = 0 and no
+// neighbours.  beta_{i+1} is not known before the projection kernel forms f',
+// so it is estimated from ||w||^2 - alpha^2 - beta_i^2 (w = L v_i, v_i and
+// v_{i-1} orthonormal to far better than the threshold); a step whose
+// estimate cancels below 2^-20 ||w||^2 projects.  One workgroup; thread j < i
+// owns omega_{i+1,j}, thread 255 the u0 entry.
+// (the body of k_pro and of the projection's decider workgroup, PROI; 256
+// threads; returns the decision to every thread)
+__device__ __forceinline__ bool pro_decide(const double* __restrict__ apart, const double* __restrict__ wpart,
+                                           int nparts, double* __restrict__ a3, const double* __restrict__ fn2_i,
+                                           const double* __restrict__ bov_i, const double* __restrict__ alpha,
+                                           const double* __restrict__ offd, double* __restrict__ omega,
+                                           ProState* __restrict__ st, int* __restrict__ flags, int i, int seg0, int m,
+                                           double thresh, double eps1) {
+    // no contraction into FMAs: the decision must come out the same in every
+    // kernel this is inlined into (k_pro, the projection's decider) — with
+    // contraction on, the two copies fused different products, so omega and
+    // a decision near the threshold differed
+#pragma clang fp contract(off)
+    __shared__ double lds4[4];
+    __shared__ double sh[4];
+    __shared__ double mx4[4];
+    __shared__ int s_pair, s_forced;
+    const int t = int(threadIdx.x);
+    constexpr int U = MAX_NCV;  // the u0 entry of a ring row
+    double* onew = omega + size_t((i + 1) % 3) * OMEGA_LD;       // omega_{i+1}
+    double* ocur = omega + size_t(i % 3) * OMEGA_LD;             // omega_i
+    const double* oprev = omega + size_t((i + 2) % 3) * OMEGA_LD;  // omega_{i-1}
+    // the recurrence's operands do not depend on the sums: their loads go out
+    // first, so they return while the partials are reduced
+    double r_al = 0.0, r_o0 = 0.0, r_o1 = 0.0, c_m1 = 0.0, c_0 = 0.0, c_p1 = 0.0, p_0 = 0.0;
+    if (t < i) {
+        r_al = alpha[t];
+        r_o1 = t + 1 < i ? offd[t + 1] : 0.0;
+        r_o0 = t > 0 ? offd[t] : 0.0;
+        c_m1 = t > 0 ? ocur[t - 1] : 0.0;
+        c_0 = ocur[t];
+        c_p1 = t + 1 < i ? ocur[t + 1] : 1.0;  // (omega_{i,i} = 1)
+        p_0 = t < i - 1 ? oprev[t] : 1.0;      // (omega_{i-1,i-1} = 1)
+    } else if (t == 255) {
+        c_0 = ocur[MAX_NCV];
+        p_0 = oprev[MAX_NCV];
+    }
+    double s_an = 0.0, s_f2 = 0.0, s_bo = 0.0;
+    int s_fo = 0;
+    if (t == 0) {
+        s_an = st->anorm;
+        s_fo = st->force;
+        s_f2 = *fn2_i;
+        s_bo = *bov_i;
+    }
+    // alpha in k_three_term's order (the bits of every other alpha path), ||w||^2 alike
+    // (both trees in one pass: wave sums, then one barrier for the cross-wave adds)
+    double sa, sw;
+    strided_sum256x2(apart, wpart, nparts, sa, sw);
+    sa = wave_sum(sa);
+    sw = wave_sum(sw);
+    if ((t & 63) == 0) {
+        lds4[t >> 6] = sa;
+        mx4[t >> 6] = sw;
+    }
+    __syncthreads();
+    if (t == 0) {
+        sa = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+        sw = (mx4[0] + mx4[1]) + (mx4[2] + mx4[3]);
+        const double a = sa;
+        *a3 = a;
+        const double b = i > 0 ? (isnan(s_bo) ? sqrt(s_f2) : s_bo) : 0.0;
+        const double b2 = sw - a * a - b * b;
+        const bool valid = b2 > 0x1p-20 * sw;  // false for NaN
+        const double bn = valid ? sqrt(b2) : 0.0;
+        const double an = fmax(s_an, fabs(a) + b + bn);
+        st->anorm = an;
+        const int pair = s_fo || i == seg0;  // the first step of a run starts a pair like a triggered one
+        sh[0] = a;
+        sh[1] = b;
+        sh[2] = bn;
+        sh[3] = an;
+        s_pair = pair;
+        s_forced = pair || i == m - 1 || !valid;  // (the cycle's last step: f_m orthogonal for the restart)
+    }
+    __syncthreads();
+    const double a = sh[0], b = sh[1], bn = sh[2], an = sh[3];
+    const bool forced = s_forced != 0;
+    double nv = 0.0;
+    if (!forced) {
+        if (t < i) {
+            const int j = t;
+            double x = j + 1 < i ? r_o1 * c_p1 : b;  // (omega_{i,i} = 1)
+            x += (r_al - a) * c_0;
+            if (j > 0) x += r_o0 * c_m1;
+            x -= b * p_0;
+            nv = (x + copysign(eps1 * an, x)) / bn;
+        } else if (t == 255) {
+            const double x = -a * c_0 - b * p_0;
+            nv = (x + copysign(eps1 * an, x)) / bn;
+        }
+    }
+    __syncthreads();  // (mx4 held ||w||^2's wave sums)
+    double mx = fabs(nv);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if ((t & 63) == 0) mx4[t >> 6] = mx;
+    __syncthreads();
+    const double mxa = fmax(fmax(mx4[0], mx4[1]), fmax(mx4[2], mx4[3]));
+    const bool d = forced || !(mxa <= thresh);  // (NaN: project)
+    // after a projection the next vector is orthogonal to rounding: omega = eps1
+    if (t < i) onew[t] = d ? eps1 : nv;
+    if (t == i) onew[i] = eps1;
+    if (t == 255) onew[U] = d ? eps1 : nv;
+    if (i == seg0) {  // omega_i of a run's first vector (a restart's kept basis, an injected vector)
+        if (t < i) ocur[t] = eps1;
+        if (t == 255) ocur[U] = eps1;
+    }
+    if (t == 0) {
+        flags[i] = d ? 1 : 0;
+        st->force = (d && !s_pair) ? 1 : 0;
+        if (d) st->projected += 1;
+    }
+    return d;
+}
+
 // The end of a projection launch for a step that does not project (k_pro):
 // column group 0 only.  The block's ||f'||^2 partial goes to column tot (the
 // update's accuracy test and the next SpMV's ||f||^2 read its sum); the
@@ -137,10 +290,14 @@ constexpr int CS_LANES = 8;  // lanes per column of the canonical column sum (co
 // With the hand-off the workgroup completing column group 0 writes them; else
 // (k_reduce_cols sums the partials) this block's partials of columns i and
 // i-1, the two the finalize reads, are zeroed.
+// zero_h false (PROI: the norm's own hand-off, run before the decision by
+// every column-group-0 workgroup, on counters of its own): h is left alone
+// (a projecting step's column groups write it; a skipped step's update
+// zeroes the two entries the finalize reads)
 __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, int rbk, int t,
                                                 double* __restrict__ part, const double* nred,
                                                 unsigned* __restrict__ gctr, double* __restrict__ h_out,
-                                                double* __restrict__ fn2_fast) {
+                                                double* __restrict__ fn2_fast, bool zero_h = true) {
     const int tot = ncols + has_u0, i = ncols - 1;
     __syncthreads();  // nred complete
     const double nb = (nred[0] + nred[1]) + (nred[2] + nred[3]);
@@ -164,7 +321,8 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
     }
     __syncthreads();
     if (!s_last) return;
-    for (int j = t; j < tot; j += 256) h_out[j] = 0.0;
+    if (zero_h)
+        for (int j = t; j < tot; j += 256) h_out[j] = 0.0;
     // the norm column in col_sum2's order (8 lanes, every 8th block, xor tree)
     if (t < CS_LANES) {
         const double* pc = part + size_t(tot) * nrb;
@@ -187,8 +345,22 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
     if (t < GT_SUB + 1) gctr[t * 64] = 0u;  // re-armed (column group 0's counters)
 }
 
-template <bool TT, bool NT, int APE = 12>
-__global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* __restrict__ V, int ncols,
+// PROI: the step's decision is taken in this launch (ek_internal.hpp
+// ProLaunch); a poller's word, 1 + decision (thread 0)
+__device__ __forceinline__ int pro_poll(const unsigned* pub) {
+    unsigned v = 0u;
+    // (bounded: the decider waits on nothing, so this ends in a few us; the
+    // bound only keeps a broken hand-off from hanging the GPU)
+    for (int it = 0; it < (1 << 22); ++it) {
+        v = __hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v != 0u) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    return v != 0u ? int(v) : 2;
+}
+
+template <bool TT, bool NT, int APE, bool PROI>
+__device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part, const double* __restrict__ alpha,
                                                const double* __restrict__ vi, const double* __restrict__ vim1,
@@ -197,23 +369,61 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
                                                const double* __restrict__ apart, int nparts,
                                                double* __restrict__ alpha_pub, unsigned* __restrict__ gctr,
                                                double* __restrict__ h_out, const int* __restrict__ flag,
-                                               double* __restrict__ fn2_fast) {
+                                               double* __restrict__ fn2_fast, ProLaunch pl) {
+    // every product-sum below is written with explicit FMAs and nothing else
+    // is contracted: with contraction left to the compiler, two
+    // instantiations of this body (k_gemvt, k_gemvt_pro) fused different
+    // products of the same expression, so the paths differed in the last bit
+#pragma clang fp contract(off)
     __shared__ double red[4][GT_COLS];
     __shared__ double nred[4];
     __shared__ double lds4[4];
     __shared__ double s_alpha;
     const int t = threadIdx.x;
     const int ncg = (ncols + has_u0 + GT_COLS - 1) / GT_COLS;
-    const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+    int nwg = int(gridDim.x), orig = int(blockIdx.x);
+    if constexpr (PROI) {
+        // the decider: the first of 8 extra workgroups ahead of the map (the
+        // other seven return; the offset keeps every workgroup's XCD) runs
+        // k_pro's body and publishes at once to every XCD's word
+        if (orig < 8) {
+            if (orig == 0) {
+                const bool d = pro_decide(apart, pl.wpart, nparts, pl.a3, fn2_i, bov_i, pl.alpha, pl.offd, pl.omega,
+                                          pl.st, pl.flags, ncols - 1, pl.seg0, pl.m, pl.thresh, pl.eps1);
+                if (t < PRO_PUB)
+                    __hip_atomic_store(pl.pub + PRO_PUB_STRIDE * t, d ? 2u : 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
+        orig -= 8;
+        nwg -= 8;
+    }
+    const int xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
     // partial reorthogonalisation (k_pro's decision for this step, uniform
     // over the launch): a step that does not project only forms f' and its
     // ||f'||^2 partials (column group 0); the other column groups have no
     // work.  Then the first nrb workgroups — the first dispatched — take the
     // row blocks in order, and the rest return at once
-    const bool skip = flag && *flag == 0;
+    // PROI: the decision comes from the decider workgroup, so the
+    // projecting map is used either way; a column group > 0 waits for it
+    // before anything (nothing to do unless the step projects), group 0 forms
+    // f' first.  skip is uniform over the workgroup in every form
+    bool skip = !PROI && flag && *flag == 0;
     if (skip && orig >= nrb) return;
     const int v = skip ? orig * ncg : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
     const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
+    __shared__ int s_dec;
+    if constexpr (PROI) {
+        if (j0 != 0) {
+            if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd);
+            __syncthreads();
+            if (s_dec == 1) return;
+        }
+    }
+    // (PROI: the basis tile is loaded after f' is formed, at one place for
+    // every column group: two load sites cost the kernel a spill)
+    const bool v_first = !PROI && !skip;
     double acc[GT_COLS];
 #pragma unroll
     for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
@@ -243,7 +453,7 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
             tv[k] = *reinterpret_cast<const double2*>(vi + r);
             tu[k] = vim1 ? *reinterpret_cast<const double2*>(vim1 + r) : make_double2(0.0, 0.0);
         }
-        if (!skip) {
+        if (v_first) {
 #pragma unroll
             for (int jj = 0; jj < GT_COLS; ++jj)
                 vs[k][jj] = ld_basis<NT>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
@@ -277,11 +487,11 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
 #pragma unroll
         for (int k = 0; k < KR; ++k) {
             double2 y = xs[k];
-            y.x -= a * tv[k].x;
-            y.y -= a * tv[k].y;
+            y.x = __builtin_fma(-a, tv[k].x, y.x);
+            y.y = __builtin_fma(-a, tv[k].y, y.y);
             if (vim1) {
-                y.x -= b * tu[k].x;
-                y.y -= b * tu[k].y;
+                y.x = __builtin_fma(-b, tu[k].x, y.x);
+                y.y = __builtin_fma(-b, tu[k].y, y.y);
             }
             xs[k] = y;
             if (j0 == 0) {
@@ -294,9 +504,30 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     if (nrm && j0 == 0) {  // ||rhs||^2 over this row block: a fixed tree (the same in TT and plain forms)
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < KR; ++k) s += xs[k].x * xs[k].x + xs[k].y * xs[k].y;
+        for (int k = 0; k < KR; ++k) s += __builtin_fma(xs[k].x, xs[k].x, xs[k].y * xs[k].y);
         s = wave_sum(s);
         if ((t & 63) == 0) nred[t >> 6] = s;
+    }
+    if constexpr (PROI) {
+        if (j0 == 0) {
+            // ||f'||^2 (both outcomes need it): its hand-off before the decision
+            gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out, fn2_fast, false);
+            if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd);
+            __syncthreads();
+            skip = s_dec == 1;
+            if (skip) return;
+        }
+        if (!skip) {
+            {
+#pragma unroll
+                for (int k = 0; k < KR; ++k) {
+                    const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+#pragma unroll
+                    for (int jj = 0; jj < GT_COLS; ++jj)
+                        vs[k][jj] = ld_basis<NT>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
+                }
+            }
+        }
     }
     if (skip) {
         gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr, h_out, fn2_fast);
@@ -311,9 +542,9 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
             const int j = j0 + jj;
             if (j < ncols) {
                 const double2 v = vs[k][jj];
-                acc[jj] += v.x * x.x + v.y * x.y;
+                acc[jj] += __builtin_fma(v.x, x.x, v.y * x.y);
             } else if (has_u0 && j == ncols) {
-                acc[jj] += u0val * ((r < nr ? x.x : 0.0) + (r + 1 < nr ? x.y : 0.0));
+                acc[jj] = __builtin_fma(u0val, (r < nr ? x.x : 0.0) + (r + 1 < nr ? x.y : 0.0), acc[jj]);
             }
         }
     }
@@ -352,7 +583,7 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     // hand-off: every store below is made by wave 0
     __shared__ int s_last;
     if (t < GT_COLS && j0 + t < tot) st_sc1(part + size_t(j0 + t) * nrb + rbk, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]));
-    if (nrm && j0 == 0 && t == 0) st_sc1(part + size_t(tot) * nrb + rbk, (nred[0] + nred[1]) + (nred[2] + nred[3]));
+    if (!PROI && nrm && j0 == 0 && t == 0) st_sc1(part + size_t(tot) * nrb + rbk, (nred[0] + nred[1]) + (nred[2] + nred[3]));
     const int cg = j0 / GT_COLS;
     unsigned* ctr = gctr + size_t(cg) * (GT_SUB + 1) * 64;
     if (t == 0) {
@@ -371,7 +602,7 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     // l summing blocks l, l + 8, ... in order (col_sum2's loads and adds), then
     // the xor tree
     const int gq = t / CS_LANES, l = t % CS_LANES;
-    const int ncol = min(GT_COLS, tot - j0) + ((nrm && j0 == 0) ? 1 : 0);
+    const int ncol = min(GT_COLS, tot - j0) + ((nrm && j0 == 0 && !PROI) ? 1 : 0);  // (PROI: the norm went before)
     if (gq < ncol) {
         const int j = gq < GT_COLS && j0 + gq < tot ? j0 + gq : tot;  // (the last group member: the norm column)
         const double* pc = part + size_t(j) * nrb;
@@ -390,6 +621,28 @@ __global__ __launch_bounds__(256) void k_gemvt(int ldv, int nrb, const double* _
     }
     if (t < GT_SUB + 1) ctr[t * 64] = 0u;  // re-armed for the next launch (visible at the kernel boundary)
 }
+
+#define EK_GEMVT_PARAMS                                                                                               \
+    int ldv, int nrb, const double *__restrict__ V, int ncols, int has_u0, double u0val, int nreal,                  \
+        const double *__restrict__ w, double *__restrict__ part, const double *__restrict__ alpha,                   \
+        const double *__restrict__ vi, const double *__restrict__ vim1, const double *__restrict__ fn2_i,            \
+        const double *__restrict__ bov_i, double *__restrict__ fp, int nrm, float *__restrict__ v32col,              \
+        const double *__restrict__ apart, int nparts, double *__restrict__ alpha_pub, unsigned *__restrict__ gctr,   \
+        double *__restrict__ h_out, const int *__restrict__ flag, double *__restrict__ fn2_fast, ProLaunch pl
+#define EK_GEMVT_ARGS                                                                                                \
+    ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part, alpha, vi, vim1, fn2_i, bov_i, fp, nrm, v32col, apart, nparts,  \
+        alpha_pub, gctr, h_out, flag, fn2_fast, pl
+template <bool TT, bool NT, int APE = 12>
+__global__ __launch_bounds__(256) void k_gemvt(EK_GEMVT_PARAMS) {
+    gemvt_body<TT, NT, APE, false>(EK_GEMVT_ARGS);
+}
+// the projection with the in-launch decision (PROI)
+template <bool NT, int APE>
+__global__ __launch_bounds__(256) void k_gemvt_pro(EK_GEMVT_PARAMS) {
+    gemvt_body<true, NT, APE, true>(EK_GEMVT_ARGS);
+}
+#undef EK_GEMVT_PARAMS
+#undef EK_GEMVT_ARGS
 
 // The sharded step's projection (ctx.cpp Lanczos::factorize_mr): the partial
 // dot products of THREE vectors with the same basis columns in one sweep of
@@ -604,12 +857,18 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
                                                 double* __restrict__ npart, const double* __restrict__ part, int nrb,
                                                 double* __restrict__ h_out, const float* __restrict__ V32,
                                                 unsigned* __restrict__ fb, double* __restrict__ fn2_fast,
-                                                const int* __restrict__ flag) {
+                                                const int* __restrict__ flag, unsigned* __restrict__ pub_rearm) {
+    // PROI: the projection's decision words, zero again for the next launch
+    // (every reader of them has finished: the previous launch)
+    if (pub_rearm && blockIdx.x == 0 && threadIdx.x < PRO_PUB) pub_rearm[PRO_PUB_STRIDE * threadIdx.x] = 0u;
     // partial reorthogonalisation: a step k_pro left unprojected keeps f = f'
     // (the projection kernel stored it); ||f||^2 = ||f'||^2 (h[tot]) for the
     // next SpMV
     if (flag && *flag == 0) {  // (the projection's hand-off already wrote it; with k_reduce_cols, here)
         if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = h[ncols + has_u0];
+        // PROI: the projection left h alone; the finalize reads h[i], h[i-1]
+        if (pub_rearm && blockIdx.x == 0 && threadIdx.x < 2 && ncols - 1 - int(threadIdx.x) >= 0)
+            const_cast<double*>(h)[ncols - 1 - int(threadIdx.x)] = 0.0;
         return;
     }
     if constexpr (!B32) {  // the next SpMV sums this launch's ||f||^2 partials
@@ -889,120 +1148,13 @@ __global__ __launch_bounds__(256) void k_finalize_step(const double* __restrict_
     }
 }
 
-// Partial reorthogonalisation: the decision for step i (ek_internal.hpp
-// pro_step).  Simon's omega recurrence (Simon 1984; PROPACK's update_mu) for
-// omega_{i+1,j} ~ v_{i+1}^T v_j:
-//   beta_{i+1} omega_{i+1,j} = beta_{j+1} omega_{i,j+1} + (alpha_j - alpha_i) omega_{i,j}
-//                              + beta_j omega_{i,j-1} - beta_i omega_{i-1,j}  (+- eps1 ||L||)
-// with omega_{k,k} = 1; against u0 (L u0 = 0) the same with alpha_j = 0 and no
-// neighbours.  beta_{i+1} is not known before the projection kernel forms f',
-// so it is estimated from ||w||^2 - alpha^2 - beta_i^2 (w = L v_i, v_i and
-// v_{i-1} orthonormal to far better than the threshold); a step whose
-// estimate cancels below 2^-20 ||w||^2 projects.  One workgroup; thread j < i
-// owns omega_{i+1,j}, thread 255 the u0 entry.
 __global__ __launch_bounds__(256) void k_pro(const double* __restrict__ apart, const double* __restrict__ wpart,
                                              int nparts, double* __restrict__ a3, const double* __restrict__ fn2_i,
                                              const double* __restrict__ bov_i, const double* __restrict__ alpha,
                                              const double* __restrict__ offd, double* __restrict__ omega,
                                              ProState* __restrict__ st, int* __restrict__ flags, int i, int seg0, int m,
                                              double thresh, double eps1) {
-    __shared__ double lds4[4];
-    __shared__ double sh[4];
-    __shared__ double mx4[4];
-    __shared__ int s_pair, s_forced;
-    const int t = int(threadIdx.x);
-    constexpr int U = MAX_NCV;  // the u0 entry of a ring row
-    double* onew = omega + size_t((i + 1) % 3) * OMEGA_LD;       // omega_{i+1}
-    double* ocur = omega + size_t(i % 3) * OMEGA_LD;             // omega_i
-    const double* oprev = omega + size_t((i + 2) % 3) * OMEGA_LD;  // omega_{i-1}
-    // the recurrence's operands do not depend on the sums: their loads go out
-    // first, so they return while the partials are reduced
-    double r_al = 0.0, r_o0 = 0.0, r_o1 = 0.0, c_m1 = 0.0, c_0 = 0.0, c_p1 = 0.0, p_0 = 0.0;
-    if (t < i) {
-        r_al = alpha[t];
-        r_o1 = t + 1 < i ? offd[t + 1] : 0.0;
-        r_o0 = t > 0 ? offd[t] : 0.0;
-        c_m1 = t > 0 ? ocur[t - 1] : 0.0;
-        c_0 = ocur[t];
-        c_p1 = t + 1 < i ? ocur[t + 1] : 1.0;  // (omega_{i,i} = 1)
-        p_0 = t < i - 1 ? oprev[t] : 1.0;      // (omega_{i-1,i-1} = 1)
-    } else if (t == 255) {
-        c_0 = ocur[MAX_NCV];
-        p_0 = oprev[MAX_NCV];
-    }
-    double s_an = 0.0, s_f2 = 0.0, s_bo = 0.0;
-    int s_fo = 0;
-    if (t == 0) {
-        s_an = st->anorm;
-        s_fo = st->force;
-        s_f2 = *fn2_i;
-        s_bo = *bov_i;
-    }
-    // alpha in k_three_term's order (the bits of every other alpha path), ||w||^2 alike
-    // (both trees in one pass: wave sums, then one barrier for the cross-wave adds)
-    double sa = wave_sum(strided_sum256(apart, nparts)), sw = wave_sum(strided_sum256(wpart, nparts));
-    if ((t & 63) == 0) {
-        lds4[t >> 6] = sa;
-        mx4[t >> 6] = sw;
-    }
-    __syncthreads();
-    if (t == 0) {
-        sa = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
-        sw = (mx4[0] + mx4[1]) + (mx4[2] + mx4[3]);
-        const double a = sa;
-        *a3 = a;
-        const double b = i > 0 ? (isnan(s_bo) ? sqrt(s_f2) : s_bo) : 0.0;
-        const double b2 = sw - a * a - b * b;
-        const bool valid = b2 > 0x1p-20 * sw;  // false for NaN
-        const double bn = valid ? sqrt(b2) : 0.0;
-        const double an = fmax(s_an, fabs(a) + b + bn);
-        st->anorm = an;
-        const int pair = s_fo || i == seg0;  // the first step of a run starts a pair like a triggered one
-        sh[0] = a;
-        sh[1] = b;
-        sh[2] = bn;
-        sh[3] = an;
-        s_pair = pair;
-        s_forced = pair || i == m - 1 || !valid;  // (the cycle's last step: f_m orthogonal for the restart)
-    }
-    __syncthreads();
-    const double a = sh[0], b = sh[1], bn = sh[2], an = sh[3];
-    const bool forced = s_forced != 0;
-    double nv = 0.0;
-    if (!forced) {
-        if (t < i) {
-            const int j = t;
-            double x = j + 1 < i ? r_o1 * c_p1 : b;  // (omega_{i,i} = 1)
-            x += (r_al - a) * c_0;
-            if (j > 0) x += r_o0 * c_m1;
-            x -= b * p_0;
-            nv = (x + copysign(eps1 * an, x)) / bn;
-        } else if (t == 255) {
-            const double x = -a * c_0 - b * p_0;
-            nv = (x + copysign(eps1 * an, x)) / bn;
-        }
-    }
-    __syncthreads();  // (mx4 held ||w||^2's wave sums)
-    double mx = fabs(nv);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    if ((t & 63) == 0) mx4[t >> 6] = mx;
-    __syncthreads();
-    const double mxa = fmax(fmax(mx4[0], mx4[1]), fmax(mx4[2], mx4[3]));
-    const bool d = forced || !(mxa <= thresh);  // (NaN: project)
-    // after a projection the next vector is orthogonal to rounding: omega = eps1
-    if (t < i) onew[t] = d ? eps1 : nv;
-    if (t == i) onew[i] = eps1;
-    if (t == 255) onew[U] = d ? eps1 : nv;
-    if (i == seg0) {  // omega_i of a run's first vector (a restart's kept basis, an injected vector)
-        if (t < i) ocur[t] = eps1;
-        if (t == 255) ocur[U] = eps1;
-    }
-    if (t == 0) {
-        flags[i] = d ? 1 : 0;
-        st->force = (d && !s_pair) ? 1 : 0;
-        if (d) st->projected += 1;
-    }
+    (void)pro_decide(apart, wpart, nparts, a3, fn2_i, bov_i, alpha, offd, omega, st, flags, i, seg0, m, thresh, eps1);
 }
 
 // Three-term recurrence f' = w - alpha v_i - beta_i v_{i-1}, alpha = sum of the
@@ -1014,6 +1166,7 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
                                                     const double* __restrict__ vi, const double* __restrict__ vim1,
                                                     const double* __restrict__ fn2_i, const double* __restrict__ bov_i,
                                                     double* __restrict__ fp, float* __restrict__ v32col) {
+#pragma clang fp contract(off)  // (gemvt_body's f', the same FMAs)
     __shared__ double lds4[4];
     __shared__ double s_alpha;
     // TT_ROWS rows per block (2 double2 per thread): fewer blocks re-reduce the
@@ -1046,11 +1199,11 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
     for (int k = 0; k < KR; ++k) {
         const size_t r = size_t(blockIdx.x) * TT_ROWS + size_t(k) * 512 + 2 * size_t(threadIdx.x);
         double2 y = x[k];
-        y.x -= a * v[k].x;
-        y.y -= a * v[k].y;
+        y.x = __builtin_fma(-a, v[k].x, y.x);
+        y.y = __builtin_fma(-a, v[k].y, y.y);
         if (vim1) {
-            y.x -= b * u[k].x;
-            y.y -= b * u[k].y;
+            y.x = __builtin_fma(-b, u[k].x, y.x);
+            y.y = __builtin_fma(-b, u[k].y, y.y);
         }
         *reinterpret_cast<double2*>(fp + r) = y;
         if (v32col) *reinterpret_cast<float2*>(v32col + r) = make_float2(float(v[k].x), float(v[k].y));
@@ -1153,30 +1306,46 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
     if (nt)
         hipLaunchKernelGGL((k_gemvt<false, true>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
-                           h_out, nullptr, nullptr);
+                           h_out, nullptr, nullptr, ProLaunch{});
     else
         hipLaunchKernelGGL((k_gemvt<false, false>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, part,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nrm, nullptr, nullptr, 0, nullptr, gctr,
-                           h_out, nullptr, nullptr);
+                           h_out, nullptr, nullptr, ProLaunch{});
 }
 
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
-              unsigned* gctr, double* h_out, bool nt, const int* flag, double* fn2_fast) {
+              unsigned* gctr, double* h_out, bool nt, const int* flag, double* fn2_fast, const ProLaunch* pl) {
     const int cols = ncols + has_u0;
-    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS));
-#define EK_GEMVT_TT(NT_, APE_)                                                                                    \
-    hipLaunchKernelGGL((k_gemvt<true, NT_, APE_>), g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal, w, \
-                       part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, (v32col || flag) ? 1 : 0, v32col, \
-                       apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out, flag, fn2_fast)
+    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS) + (pl ? 8 : 0));
+    // pl (PROI): the decision in this launch (8 more workgroups); alpha reduced by every
+    // workgroup from apart (required) and published to pl->a3
+    const ProLaunch pv = pl ? *pl : ProLaunch{};
+#define EK_GEMVT_TT(KERNEL_)                                                                                           \
+    hipLaunchKernelGGL(KERNEL_, g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal,                         \
+                       w, part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, (v32col || flag || pl) ? 1 : 0,   \
+                       v32col, apart, nparts, apart ? const_cast<double*>(alpha) : nullptr, gctr, h_out, flag,       \
+                       fn2_fast, pv)
     const bool wide = apart && nparts > 12 * 256;  // 24 partials a thread (up to 6,144; beyond: strided_sum256)
-    if (nt) {
-        if (wide) EK_GEMVT_TT(true, 24);
-        else EK_GEMVT_TT(true, 12);
+    if (pl) {
+        if (!apart || !pl->pub || !gctr || !h_out) {
+            std::fprintf(stderr, "gemvt_tt: the in-launch decision needs the alpha partials and the hand-off\n");
+            std::abort();
+        }
+        if (nt) {
+            if (wide) EK_GEMVT_TT((k_gemvt_pro<true, 24>));
+            else EK_GEMVT_TT((k_gemvt_pro<true, 12>));
+        } else {
+            if (wide) EK_GEMVT_TT((k_gemvt_pro<false, 24>));
+            else EK_GEMVT_TT((k_gemvt_pro<false, 12>));
+        }
+    } else if (nt) {
+        if (wide) EK_GEMVT_TT((k_gemvt<true, true, 24>));
+        else EK_GEMVT_TT((k_gemvt<true, true, 12>));
     } else {
-        if (wide) EK_GEMVT_TT(false, 24);
-        else EK_GEMVT_TT(false, 12);
+        if (wide) EK_GEMVT_TT((k_gemvt<true, false, 24>));
+        else EK_GEMVT_TT((k_gemvt<true, false, 12>));
     }
 #undef EK_GEMVT_TT
 }
@@ -1208,19 +1377,19 @@ void reduce_cols(hipStream_t s, const double* part, int nrb, int ncols_total, do
     hipLaunchKernelGGL((k_update<RED, B32, NT>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, __VA_ARGS__)
 void update(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
             const double* h, const double* src, double* dst, double* npart, const float* V32, unsigned* fb,
-            double* fn2_fast, bool nt, const int* flag) {
+            double* fn2_fast, bool nt, const int* flag, unsigned* pub_rearm) {
     if (V32 && nt)
         EK_UPDATE_LAUNCH(false, true, true, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0, nullptr,
-                         V32, fb, fn2_fast, flag);
+                         V32, fb, fn2_fast, flag, pub_rearm);
     else if (V32)
         EK_UPDATE_LAUNCH(false, true, false, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
-                         nullptr, V32, fb, fn2_fast, flag);
+                         nullptr, V32, fb, fn2_fast, flag, pub_rearm);
     else if (nt)
         EK_UPDATE_LAUNCH(false, false, true, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
-                         nullptr, nullptr, nullptr, flag ? fn2_fast : nullptr, flag);
+                         nullptr, nullptr, nullptr, flag ? fn2_fast : nullptr, flag, pub_rearm);
     else
         EK_UPDATE_LAUNCH(false, false, false, ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, nullptr, 0,
-                         nullptr, nullptr, nullptr, flag ? fn2_fast : nullptr, flag);
+                         nullptr, nullptr, nullptr, flag ? fn2_fast : nullptr, flag, pub_rearm);
 }
 
 void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, double u0val, int nreal,
@@ -1228,16 +1397,16 @@ void update_r(hipStream_t s, int ldv, const double* V, int ncols, int has_u0, do
               const float* V32, unsigned* fb, double* fn2_fast, bool nt) {
     if (V32 && nt)
         EK_UPDATE_LAUNCH(true, true, true, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, V32, fb, fn2_fast, nullptr);
+                         h_out, V32, fb, fn2_fast, nullptr, nullptr);
     else if (V32)
         EK_UPDATE_LAUNCH(true, true, false, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, V32, fb, fn2_fast, nullptr);
+                         h_out, V32, fb, fn2_fast, nullptr, nullptr);
     else if (nt)
         EK_UPDATE_LAUNCH(true, false, true, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, nullptr, nullptr, nullptr, nullptr);
+                         h_out, nullptr, nullptr, nullptr, nullptr, nullptr);
     else
         EK_UPDATE_LAUNCH(true, false, false, ldv, V, ncols, has_u0, u0val, nreal, nullptr, src, dst, npart, part, nrb,
-                         h_out, nullptr, nullptr, nullptr, nullptr);
+                         h_out, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 #undef EK_UPDATE_LAUNCH
 

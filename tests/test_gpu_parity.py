@@ -399,7 +399,7 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
 @pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_ALPHA_LAST=1", "EK_UPD_RED=0", "EK_UPD_RED=1",
                                     "EK_UPD_RED=2", "EK_V_NT=1", "pro:EK_UPD_RED=0", "pro:EK_UPD_RED=2",
-                                    "pro:EK_V_NT=1"])
+                                    "pro:EK_V_NT=1", "pro:EK_PRO_INLAUNCH=0"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
@@ -410,7 +410,10 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
       group (EK_UPD_RED=2, the default up to 256 row blocks), by every update
       workgroup (1) or by a k_reduce_cols launch (0, the default above);
     * the basis passes' non-temporal loads (EK_V_NT=1; the default above 768
-      MB of basis) against plain ones.
+      MB of basis) against plain ones;
+    * the partial reorthogonalisation's decision taken inside the projection
+      launch (the default with the projection's hand-off) against the k_pro
+      launch (EK_PRO_INLAUNCH=0).
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses.  These run the full
     reorthogonalisation (EK_REORTH=1); "pro:" switches hold the partial one
@@ -440,6 +443,35 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     x, y = np.load(a), np.load(b)
     assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
     assert x[2] < 1e-8
+
+
+@pytest.mark.parametrize("which", ["ibm01", "syn0.25"])
+def test_lanczos_pro_inlaunch_graph_replays(ek, tmp_path, which):
+    """The in-launch decision (the projection's decider workgroup publishes
+    to words the step's update re-arms) under the step-chunk graphs: three
+    solves in one process (eager, captured, replayed) give the same bits, and
+    the bits of eager launches with the k_pro launch (EK_PRO_INLAUNCH=0,
+    EK_LANCZOS_GRAPH=0)."""
+    import subprocess
+    import sys
+    gen = {"ibm01": "ek.Hypergraph.read(circuit_path('ibm01'))", "syn0.25": "ek.Hypergraph.generate(0.25, 3)"}[which]
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); from conftest import load_package, circuit_path; "
+        "ek = load_package(); h = %s; c = ek.Context(0); c.spmv_setup_pins(h); out = []\n"
+        "for _ in range(3):\n"
+        "    lam, v, st = c.lanczos_fiedler(); out.append(np.concatenate([[lam, st['matvecs'], st['residual']], v]))\n"
+        "np.save(sys.argv[1], np.stack(out))"
+    ) % (os.path.dirname(os.path.abspath(__file__)), gen)
+    env = dict(os.environ, EK_REORTH="3")
+    a, b = str(tmp_path / "inl.npy"), str(tmp_path / "kpro.npy")
+    subprocess.run([sys.executable, "-c", code, a], check=True, timeout=180, env=env)
+    subprocess.run([sys.executable, "-c", code, b], check=True, timeout=180,
+                   env=dict(env, EK_PRO_INLAUNCH="0", EK_LANCZOS_GRAPH="0"))
+    x, y = np.load(a), np.load(b)
+    for r in range(3):
+        assert np.array_equal(x[r].view(np.uint64), y[0].view(np.uint64)), r
+        assert np.array_equal(y[r].view(np.uint64), y[0].view(np.uint64)), r
+    assert x[0][2] < 1e-8
 
 
 @pytest.mark.parametrize("name", ["ibm01", "industry2", "fract"])
