@@ -1203,6 +1203,9 @@ struct Lanczos {
     // the decision inside the projection launch (no k_pro launch; needs the
     // projection's hand-off, upd_red 2).  EK_PRO_INLAUNCH=0: the k_pro launch
     bool proi = false;
+    // ... and the update's workgroups in the projection launch (no update
+    // launch: a skipped step is two launches).  EK_PRO_MERGE=0: its own launch
+    bool pro_merge = false;
     unsigned* pro_pub() { return reinterpret_cast<unsigned*>(c->pflags.as<char>() + pro_pub_off()); }
     size_t pro_pub_off() const { return (size_t(m + 2) * 4 + 255) / 256 * 256; }
     float* V32() { return b32 ? c->V32.as<float>() : nullptr; }
@@ -1366,7 +1369,14 @@ struct Lanczos {
             pl.m = m;
             pl.thresh = pro_thresh;
             pl.eps1 = pro_eps1;
+            if (pro_merge) {
+                pl.merged = 1;
+                pl.npart = c->npart.as<double>();
+                pl.V32 = V32();
+                pl.fb = b32 ? c->fbk.as<unsigned>() : nullptr;
+            }
         }
+        const bool mrg = inl && pro_merge;
         for (int i = k; i < kend; ++i) {
             ek::dev::StepFin fin;
             if (i > seg0) {
@@ -1383,6 +1393,7 @@ struct Lanczos {
                 fin.fast = fast;  // the update's ||f||^2 (or NaN)
             }
             if (pro) fin.wpart = c->wpart.as<double>();  // ||w||^2 partials for k_pro (also at i == seg0)
+            if (mrg) fin.pub_rearm = pro_pub();  // (the merged update's words and done counter)
             const bool timed = spmv_timed_step(i);
             // the SpMV's last block also reduces alpha into a3 (k_three_term's bits)
             ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
@@ -1400,7 +1411,8 @@ struct Lanczos {
             if (tt) {  // the projection of f' = w - alpha v_i - beta v_{i-1}, formed per row (and stored to f)
                 ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
                                   i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, c->f.as<double>(), c->part.as<double>(),
-                                  col32(i), inl || pro_apart || !(alpha_last || pro) ? c->apart.as<double>() : nullptr, c->nrb_spmv,
+                                  col32(i),
+                                  inl || pro_apart || !(alpha_last || pro) ? c->apart.as<double>() : nullptr, c->nrb_spmv,
                                   gctr, hoff, nt, flag, pro ? fast : nullptr, inl ? &pl : nullptr);
             } else {
                 ek::dev::three_term(s, ldv, c->apart.as<double>(), c->nrb_spmv, a3, c->w.as<double>(), col(i),
@@ -1411,7 +1423,9 @@ struct Lanczos {
             // (b32: ||f'||^2 rides along as one more column of the partials)
             unsigned* fb = b32 ? c->fbk.as<unsigned>() : nullptr;
             // (b32: the update also leaves ||f||^2 = ||f'||^2 - ||h||^2 for the next SpMV)
-            if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
+            if (mrg) {
+                // (the update ran inside the projection launch)
+            } else if (upd_red == 2) {  // h (and ||f'||^2) reduced by the projection
                 ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, c->h2.as<double>(), c->f.as<double>(),
                                 c->f.as<double>(), c->npart.as<double>(), V32(), fb, fast, nt, flag,
                                 inl ? pro_pub() : nullptr);
@@ -1625,6 +1639,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.pro_thresh = o.reorth_thresh > 0 ? o.reorth_thresh : 1e-10;
     L.pro_eps1 = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     if (const char* e = std::getenv("EK_PRO_INLAUNCH"); L.pro) L.proi = !(e && e[0] == '0');
+    if (const char* e = std::getenv("EK_PRO_MERGE"); L.proi) L.pro_merge = !(e && e[0] == '0');
 
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);
@@ -1678,9 +1693,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         c->omega.ensure(3 * size_t(ek::dev::OMEGA_LD) * 8);
         c->prost.ensure(sizeof(ek::dev::ProState));
         // + the in-launch decision's words (PRO_PUB lines of 256 B), zero between launches
-        c->pflags.ensure(L.pro_pub_off() + size_t(ek::dev::PRO_PUB) * 256);
+        c->pflags.ensure(L.pro_pub_off() + size_t(ek::dev::PRO_PUB_WORDS) * 256);
         HIPCHK(hipMemsetAsync(c->prost.p, 0, sizeof(ek::dev::ProState), s));
-        HIPCHK(hipMemsetAsync(L.pro_pub(), 0, size_t(ek::dev::PRO_PUB) * 256, s));
+        HIPCHK(hipMemsetAsync(L.pro_pub(), 0, size_t(ek::dev::PRO_PUB_WORDS) * 256, s));
     }
     // the step chunks' graphs (EK_LANCZOS_GRAPH=0: eager launches, A/B), kept
     // while every buffer and parameter their launches carry is unchanged
@@ -1704,7 +1719,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                                   pv(c->val.p), pv(c->rowptr.p), pv(c->pn_wrow.p), pv(c->pn_start.p), pv(c->pn_word.p),
                                   pv(c->pn_rid.p), uint64_t(m), uint64_t(L.ldv), uint64_t(L.nreal), uint64_t(c->n),
                                   uint64_t(c->nrb_spmv), uint64_t(c->pn_G), uint64_t(c->colbits), uint64_t(L.has_u0),
-                                  uint64_t(L.b32), uint64_t(L.pro), uint64_t(L.proi), uint64_t(L.nt), uint64_t(L.alpha_last),
+                                  uint64_t(L.b32), uint64_t(L.pro), uint64_t(L.proi), uint64_t(L.pro_merge), uint64_t(L.nt), uint64_t(L.alpha_last),
                                   uint64_t(tt_env), db(L.pro_thresh),
                                   db(L.pro_eps1), db(L.u0val)};
         if (sig != c->lz_sig) {

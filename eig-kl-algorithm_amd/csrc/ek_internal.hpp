@@ -184,6 +184,11 @@ struct StepFin {
     // from ybase[row] (that SpMV's unscaled partial); own_lo == own_hi: none
     int own_lo = 0, own_hi = 0;
     const double* ybase = nullptr;
+    // the update inside the projection launch (ctx.cpp, PROI merged): the
+    // fp32 shadow of the basis column (fl32(v), written with v) and the
+    // projection's decision words + done counter, zeroed by block 0
+    float* v32col = nullptr;
+    unsigned* pub_rearm = nullptr;
 };
 
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)
@@ -410,6 +415,9 @@ void pro_step(hipStream_t s, const double* apart, const double* wpart, int npart
 // launch.  i = ncols - 1; alpha / a3 as k_pro.
 constexpr int PRO_PUB = 8;
 constexpr int PRO_PUB_STRIDE = 64;  // uints between two words (256 B)
+// (merged update: word PRO_PUB is the launch's done counter — the column
+// groups' and the norm's last workgroups, once their h entries are stored)
+constexpr int PRO_PUB_WORDS = PRO_PUB + 1;
 struct ProLaunch {
     const double* wpart = nullptr;
     const double* alpha = nullptr;
@@ -417,8 +425,13 @@ struct ProLaunch {
     double* omega = nullptr;
     ProState* st = nullptr;
     int* flags = nullptr;
-    unsigned* pub = nullptr;  // PRO_PUB words, zero before the launch
+    unsigned* pub = nullptr;  // PRO_PUB_WORDS words, zero before the launch
     double* a3 = nullptr;
+    // merged (the update's workgroups follow the projection's in the launch):
+    double* npart = nullptr;      // the update's ||f||^2 partials
+    const float* V32 = nullptr;   // the fp32 shadow (B32 update), column i from the SpMV
+    unsigned* fb = nullptr;       // B32 fp64-fallback count
+    int merged = 0;               // the update's workgroups in this launch (no update launch)
     int seg0 = 0, m = 0;
     double thresh = 0.0, eps1 = 0.0;
 };

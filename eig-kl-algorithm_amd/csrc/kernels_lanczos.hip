@@ -297,7 +297,8 @@ __device__ __forceinline__ bool pro_decide(const double* __restrict__ apart, con
 __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, int rbk, int t,
                                                 double* __restrict__ part, const double* nred,
                                                 unsigned* __restrict__ gctr, double* __restrict__ h_out,
-                                                double* __restrict__ fn2_fast, bool zero_h = true) {
+                                                double* __restrict__ fn2_fast, bool zero_h = true,
+                                                unsigned* __restrict__ done = nullptr) {
     const int tot = ncols + has_u0, i = ncols - 1;
     __syncthreads();  // nred complete
     const double nb = (nred[0] + nred[1]) + (nred[2] + nred[3]);
@@ -338,8 +339,14 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
 #pragma unroll
         for (int o = 1; o < CS_LANES; o <<= 1) a += __shfl_xor(a, o, 64);
         if (t == 0) {
-            h_out[tot] = a;
-            if (fn2_fast) *fn2_fast = a;  // ||f||^2 = ||f'||^2 for the next SpMV (the update has nothing to do)
+            if (done) {  // (merged: the update in this launch reads it; write-through, then the signal)
+                st_sc1(h_out + tot, a);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                h_out[tot] = a;
+                if (fn2_fast) *fn2_fast = a;  // ||f||^2 = ||f'||^2 for the next SpMV (the update has nothing to do)
+            }
         }
     }
     if (t < GT_SUB + 1) gctr[t * 64] = 0u;  // re-armed (column group 0's counters)
@@ -358,8 +365,37 @@ __device__ __forceinline__ int pro_poll(const unsigned* pub) {
     }
     return v != 0u ? int(v) : 2;
 }
+// thread 0: wait until the counter reaches target (bounded like pro_poll);
+// 1 when it did
+__device__ __forceinline__ int pro_wait(const unsigned* ctr, unsigned target) {
+    for (int it = 0; it < (1 << 22); ++it) {
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return 1;
+        __builtin_amdgcn_s_sleep(4);
+    }
+    return 0;
+}
 
-template <bool TT, bool NT, int APE, bool PROI>
+// the merged update's own f' (the projection's formula and operands: it
+// does not read the f' the projection stores in the same launch)
+struct UpdTT {
+    const double* w = nullptr;
+    const double* vi = nullptr;
+    const double* vim1 = nullptr;
+    const double* fn2_i = nullptr;
+    const double* bov_i = nullptr;
+    const double* apart = nullptr;
+    int nparts = 0;
+};
+template <bool RED, bool B32, bool NT, bool MRG>
+__device__ __forceinline__ void update_body(int blk, int ldv, const double* __restrict__ V, int ncols, int has_u0,
+                                            double u0val, int nreal, const double* __restrict__ h,
+                                            const double* __restrict__ src, double* __restrict__ dst,
+                                            double* __restrict__ npart, const double* __restrict__ part, int nrb,
+                                            double* __restrict__ h_out, const float* __restrict__ V32,
+                                            unsigned* __restrict__ fb, double* __restrict__ fn2_fast,
+                                            const unsigned* __restrict__ done, unsigned done_target, UpdTT tt);
+
+template <bool TT, bool NT, int APE, bool PROI, bool MRG = false, bool B32U = false>
 __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __restrict__ V, int ncols,
                                                int has_u0, double u0val, int nreal, const double* __restrict__ w,
                                                double* __restrict__ part, const double* __restrict__ alpha,
@@ -398,6 +434,41 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         }
         orig -= 8;
         nwg -= 8;
+        if constexpr (MRG) {
+            // the update's workgroups, after every projection workgroup (so
+            // they wait only on workgroups dispatched before them)
+            const int nproj = nrb * ncg;
+            if (orig >= nproj) {
+                const int blk = orig - nproj, tot = ncols + has_u0;
+                unsigned* done = pl.pub + PRO_PUB_STRIDE * PRO_PUB;
+                __shared__ int s_ud;
+                if (t == 0) s_ud = pro_poll(pl.pub + PRO_PUB_STRIDE * (orig % 8));
+                __syncthreads();
+                if (s_ud == 1) {  // a skipped step: f = f'; ||f||^2 = ||f'||^2 once the norm is in
+                    if (blk == 0) {
+                        if (t == 0) {
+                            (void)pro_wait(done, 1u);
+                            if (fn2_fast) *fn2_fast = ld_sc1(h_out + tot);
+                        }
+                        if (t < 2 && ncols - 1 - t >= 0) h_out[ncols - 1 - t] = 0.0;  // (the finalize's h[i], h[i-1])
+                    }
+                    return;
+                }
+                UpdTT tt;
+                tt.w = w;
+                tt.vi = vi;
+                tt.vim1 = vim1;
+                tt.fn2_i = fn2_i;
+                tt.bov_i = bov_i;
+                tt.apart = apart;
+                tt.nparts = nparts;
+                update_body<false, B32U, NT, true>(blk, ldv, V, ncols, has_u0, u0val, nreal, h_out, fp, fp, pl.npart,
+                                                   nullptr, nrb, nullptr, pl.V32, pl.fb, fn2_fast, done,
+                                                   unsigned(ncg + 1), tt);
+                return;
+            }
+            nwg = nproj;
+        }
     }
     const int xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
     // partial reorthogonalisation (k_pro's decision for this step, uniform
@@ -496,7 +567,9 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
             xs[k] = y;
             if (j0 == 0) {
                 const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
-                *reinterpret_cast<double2*>(fp + r) = y;
+                // (merged: stored only once the step is known to skip — a
+                // projecting step's f is written by the update in this launch)
+                if constexpr (!MRG) *reinterpret_cast<double2*>(fp + r) = y;
                 if (v32col) *reinterpret_cast<float2*>(v32col + r) = make_float2(float(tv[k].x), float(tv[k].y));
             }
         }
@@ -511,10 +584,18 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     if constexpr (PROI) {
         if (j0 == 0) {
             // ||f'||^2 (both outcomes need it): its hand-off before the decision
-            gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out, fn2_fast, false);
+            gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out, MRG ? nullptr : fn2_fast,
+                            false, MRG ? pl.pub + PRO_PUB_STRIDE * PRO_PUB : nullptr);
             if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd);
             __syncthreads();
             skip = s_dec == 1;
+            if constexpr (MRG) {
+                if (skip) {  // f = f'
+#pragma unroll
+                    for (int k = 0; k < KR; ++k)
+                        *reinterpret_cast<double2*>(fp + size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t)) = xs[k];
+                }
+            }
             if (skip) return;
         }
         if (!skip) {
@@ -617,7 +698,16 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         }
 #pragma unroll
         for (int o = 1; o < CS_LANES; o <<= 1) a += __shfl_xor(a, o, 64);
-        if (l == 0) h_out[j] = a;
+        if (l == 0) {
+            if constexpr (MRG) st_sc1(h_out + j, a);
+            else h_out[j] = a;
+        }
+    }
+    if constexpr (MRG) {  // this column group's h is in: signal the update (every storing wave drained)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0)
+            __hip_atomic_fetch_add(pl.pub + PRO_PUB_STRIDE * PRO_PUB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t < GT_SUB + 1) ctr[t * 64] = 0u;  // re-armed for the next launch (visible at the kernel boundary)
 }
@@ -636,10 +726,11 @@ template <bool TT, bool NT, int APE = 12>
 __global__ __launch_bounds__(256) void k_gemvt(EK_GEMVT_PARAMS) {
     gemvt_body<TT, NT, APE, false>(EK_GEMVT_ARGS);
 }
-// the projection with the in-launch decision (PROI)
-template <bool NT, int APE>
+// the projection with the in-launch decision (PROI); MRG: + the update's
+// workgroups (B32U: its fp32-shadow form)
+template <bool NT, int APE, bool MRG, bool B32U>
 __global__ __launch_bounds__(256) void k_gemvt_pro(EK_GEMVT_PARAMS) {
-    gemvt_body<true, NT, APE, true>(EK_GEMVT_ARGS);
+    gemvt_body<true, NT, APE, true, MRG, B32U>(EK_GEMVT_ARGS);
 }
 #undef EK_GEMVT_PARAMS
 #undef EK_GEMVT_ARGS
@@ -850,29 +941,24 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
 // zero) every workgroup takes the same decision (the same h and norm, the
 // same sums) and runs the fp64 loop (*fb counts those launches).
 // ||src||^2 comes as one more column of the partials (k_gemvt's nrm) or h.
-template <bool RED, bool B32, bool NT>
-__global__ __launch_bounds__(256) void k_update(int ldv, const double* __restrict__ V, int ncols, int has_u0,
-                                                double u0val, int nreal, const double* __restrict__ h,
-                                                const double* __restrict__ src, double* __restrict__ dst,
-                                                double* __restrict__ npart, const double* __restrict__ part, int nrb,
-                                                double* __restrict__ h_out, const float* __restrict__ V32,
-                                                unsigned* __restrict__ fb, double* __restrict__ fn2_fast,
-                                                const int* __restrict__ flag, unsigned* __restrict__ pub_rearm) {
-    // PROI: the projection's decision words, zero again for the next launch
-    // (every reader of them has finished: the previous launch)
-    if (pub_rearm && blockIdx.x == 0 && threadIdx.x < PRO_PUB) pub_rearm[PRO_PUB_STRIDE * threadIdx.x] = 0u;
-    // partial reorthogonalisation: a step k_pro left unprojected keeps f = f'
-    // (the projection kernel stored it); ||f||^2 = ||f'||^2 (h[tot]) for the
-    // next SpMV
-    if (flag && *flag == 0) {  // (the projection's hand-off already wrote it; with k_reduce_cols, here)
-        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = h[ncols + has_u0];
-        // PROI: the projection left h alone; the finalize reads h[i], h[i-1]
-        if (pub_rearm && blockIdx.x == 0 && threadIdx.x < 2 && ncols - 1 - int(threadIdx.x) >= 0)
-            const_cast<double*>(h)[ncols - 1 - int(threadIdx.x)] = 0.0;
-        return;
-    }
+// MRG: the update inside the projection launch (k_gemvt_pro's last ldv/512
+// workgroups, blk = this one's index among them): h and f' come from the
+// same launch, so the first basis batches go out, then thread 0 waits for
+// *done to reach done_target (every h entry stored write-through), and f'
+// and h are read with agent-scope (sc1) loads
+template <bool RED, bool B32, bool NT, bool MRG>
+__device__ __forceinline__ void update_body(int blk, int ldv, const double* __restrict__ V, int ncols, int has_u0,
+                                            double u0val, int nreal, const double* __restrict__ h,
+                                            const double* __restrict__ src, double* __restrict__ dst,
+                                            double* __restrict__ npart, const double* __restrict__ part, int nrb,
+                                            double* __restrict__ h_out, const float* __restrict__ V32,
+                                            unsigned* __restrict__ fb, double* __restrict__ fn2_fast,
+                                            const unsigned* __restrict__ done, unsigned done_target, UpdTT tt) {
+    // explicit FMAs, no contraction: the same bits in every instantiation
+    // (the k_update launch and the update inside the projection launch)
+#pragma clang fp contract(off)
     if constexpr (!B32) {  // the next SpMV sums this launch's ||f||^2 partials
-        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = __builtin_nan("");
+        if (fn2_fast && blk == 0 && threadIdx.x == 0) *fn2_fast = __builtin_nan("");
     }
     constexpr int UB = EK_UPD_UB;
     constexpr int UB32 = 2 * EK_UPD_UB;  // fp32 columns per batch: the same bytes in flight
@@ -901,18 +987,41 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     // (One row per thread with 8-B loads in 512-thread blocks, twice the
     // waves: 28 vs 20 us per step.)
     const int jmax = ncols > 0 ? ncols - 1 : 0;
-    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    const size_t r = (size_t(blk) * 256 + threadIdx.x) * 2;
     auto load_batch = [&](double2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB; ++u) vb[u] = ld_basis<NT>(V + size_t(min(j0 + u, jmax)) * ldv + r);
     };
-    double2 x = *reinterpret_cast<const double2*>(src + r);
+    double2 x = make_double2(0.0, 0.0);
+    if constexpr (!MRG) {
+        x = *reinterpret_cast<const double2*>(src + r);
+    } else {
+        // f' = w - alpha v_i - beta v_{i-1} from operands of earlier launches,
+        // alpha in the projection's order (strided partials, block tree): the
+        // projection's bits.  Before the basis batches go out (registers)
+        const double2 ttw = *reinterpret_cast<const double2*>(tt.w + r);
+        const double2 ttv = *reinterpret_cast<const double2*>(tt.vi + r);
+        const double2 ttu = tt.vim1 ? *reinterpret_cast<const double2*>(tt.vim1 + r) : make_double2(0.0, 0.0);
+        __shared__ double s_al;
+        const double sa = block_sum256(strided_sum256(tt.apart, tt.nparts), lds4);
+        if (threadIdx.x == 0) s_al = sa;
+        __syncthreads();
+        const double a = s_al;
+        const double b = tt.vim1 ? (isnan(*tt.bov_i) ? sqrt(*tt.fn2_i) : *tt.bov_i) : 0.0;
+        x = ttw;
+        x.x = __builtin_fma(-a, ttv.x, x.x);
+        x.y = __builtin_fma(-a, ttv.y, x.y);
+        if (tt.vim1) {
+            x.x = __builtin_fma(-b, ttu.x, x.x);
+            x.y = __builtin_fma(-b, ttu.y, x.y);
+        }
+    }
     auto consume = [&](const double2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
             const double hj = hc[j0 + u];
-            x.x -= vb[u].x * hj;
-            x.y -= vb[u].y * hj;
+            x.x = __builtin_fma(-vb[u].x, hj, x.x);
+            x.y = __builtin_fma(-vb[u].y, hj, x.y);
         }
     };
     // past the end: clamped re-reads of column jmax (cache hits), coefficient 0
@@ -934,17 +1043,31 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     // (B32: the shadow's; the fp64 fallback issues its own afterwards)
     double2 ba[UB], bb[UB];
     float2 fa[UB32], fbb[UB32];
+    // MRG: the shadow's column i is being written in this launch (the
+    // projection's column-group-0 workgroups): the shadow loop stops before
+    // it (clamped to column i-1, its coefficient taken as 0 there) and column
+    // i is subtracted last as fl32 of the fp64 column — the same value and
+    // the same order of operations as the shadow loop over all columns
+    constexpr bool COLI = MRG && B32;
+    const int jmax32 = COLI ? (ncols > 1 ? ncols - 2 : 0) : jmax;
     auto load32 = [&](float2* vb, int j0) {
 #pragma unroll
         for (int u = 0; u < UB32; ++u)
-            vb[u] = ld_basis32<NT>(V32 + size_t(min(j0 + u, jmax)) * ldv + r);
+            vb[u] = ld_basis32<NT>(V32 + size_t(min(j0 + u, jmax32)) * ldv + r);
     };
+    double2 vi64 = make_double2(0.0, 0.0);
+    if constexpr (COLI) vi64 = ld_basis<NT>(V + size_t(jmax) * ldv + r);
     if constexpr (B32) {
         load32(fa, 0);
         load32(fbb, UB32);
     } else {
         load_batch(ba, 0);
         load_batch(bb, UB);
+    }
+    if constexpr (MRG) {
+        __shared__ int s_ok;
+        if (threadIdx.x == 0) s_ok = pro_wait(done, done_target);
+        __syncthreads();
     }
     auto put = [&](int j, double v) {
         if (j < ncols) hc[j] = v;
@@ -959,13 +1082,15 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
             col_sum2(part + size_t(ja) * nrb, part + size_t(min(jb, totr - 1)) * nrb, nrb, l, &sa, &sb);
             if (l == 0) {
                 put(ja, sa);
-                if (blockIdx.x == 0) h_out[ja] = sa;
+                if (blk == 0) h_out[ja] = sa;
                 if (jb < totr) {
                     put(jb, sb);
-                    if (blockIdx.x == 0) h_out[jb] = sb;
+                    if (blk == 0) h_out[jb] = sb;
                 }
             }
         }
+    } else if constexpr (MRG) {
+        for (int j = threadIdx.x; j < totr; j += 256) put(j, ld_sc1(h + j));
     } else {
         for (int j = threadIdx.x; j < totr; j += 256) put(j, h[j]);
     }
@@ -985,10 +1110,10 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
         // to O(eps ||f'||^2) like the direct sum while ||h||^2 <= 2^-20
         // ||f'||^2 (no cancellation); otherwise (a breakdown) NaN: the SpMV
         // sums the partials
-        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) {
+        if (fn2_fast && blk == 0 && threadIdx.x == 0) {
             double q = 0.0;
-            for (int j = 0; j < ncols; ++j) q += hc[j] * hc[j];
-            if (has_u0) q += hu0 * hu0;
+            for (int j = 0; j < ncols; ++j) q = __builtin_fma(hc[j], hc[j], q);
+            if (has_u0) q = __builtin_fma(hu0, hu0, q);
             *fn2_fast = q <= 0x1p-20 * snrm ? snrm - q : __builtin_nan("");
         }
         if (ok) {
@@ -996,11 +1121,19 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
 #pragma unroll
                 for (int u = 0; u < UB32; ++u) {
                     const double hj = hc[j0 + u];
-                    x.x -= double(vb[u].x) * hj;
-                    x.y -= double(vb[u].y) * hj;
+                    x.x = __builtin_fma(-double(vb[u].x), hj, x.x);
+                    x.y = __builtin_fma(-double(vb[u].y), hj, x.y);
                 }
             };
-            for (int j0 = 0; j0 < ncols; j0 += 2 * UB32) {
+            double hi = 0.0;
+            if constexpr (COLI) {  // (column i's coefficient: 0 inside the loop)
+                hi = hc[jmax];
+                __syncthreads();
+                if (threadIdx.x == 0) hc[jmax] = 0.0;
+                __syncthreads();
+            }
+            const int nloop = COLI ? ncols - 1 : ncols;
+            for (int j0 = 0; j0 < nloop; j0 += 2 * UB32) {
                 consume32(fa, j0);
                 __builtin_amdgcn_sched_barrier(0);
                 load32(fa, j0 + 2 * UB32);
@@ -1010,8 +1143,14 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
                 load32(fbb, j0 + 3 * UB32);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            if constexpr (COLI) {
+                if (ncols > 0) {
+                    x.x = __builtin_fma(-double(float(vi64.x)), hi, x.x);
+                    x.y = __builtin_fma(-double(float(vi64.y)), hi, x.y);
+                }
+            }
         } else {
-            if (fb && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(fb, 1u);
+            if (fb && blk == 0 && threadIdx.x == 0) atomicAdd(fb, 1u);
             load_batch(ba, 0);
             load_batch(bb, UB);
             run64(ba, bb);
@@ -1026,9 +1165,34 @@ __global__ __launch_bounds__(256) void k_update(int ldv, const double* __restric
     }
     *reinterpret_cast<double2*>(dst + r) = x;
     if (npart) {
-        const double s = block_sum256(x.x * x.x + x.y * x.y, lds4);
-        if (threadIdx.x == 0) npart[blockIdx.x] = s;
+        const double s = block_sum256(__builtin_fma(x.x, x.x, x.y * x.y), lds4);
+        if (threadIdx.x == 0) npart[blk] = s;
     }
+}
+
+template <bool RED, bool B32, bool NT>
+__global__ __launch_bounds__(256) void k_update(int ldv, const double* __restrict__ V, int ncols, int has_u0,
+                                                double u0val, int nreal, const double* __restrict__ h,
+                                                const double* __restrict__ src, double* __restrict__ dst,
+                                                double* __restrict__ npart, const double* __restrict__ part, int nrb,
+                                                double* __restrict__ h_out, const float* __restrict__ V32,
+                                                unsigned* __restrict__ fb, double* __restrict__ fn2_fast,
+                                                const int* __restrict__ flag, unsigned* __restrict__ pub_rearm) {
+    // PROI: the projection's decision words, zero again for the next launch
+    // (every reader of them has finished: the previous launch)
+    if (pub_rearm && blockIdx.x == 0 && threadIdx.x < PRO_PUB) pub_rearm[PRO_PUB_STRIDE * threadIdx.x] = 0u;
+    // partial reorthogonalisation: a step k_pro left unprojected keeps f = f'
+    // (the projection kernel stored it); ||f||^2 = ||f'||^2 (h[tot]) for the
+    // next SpMV
+    if (flag && *flag == 0) {  // (the projection's hand-off already wrote it; with k_reduce_cols, here)
+        if (fn2_fast && blockIdx.x == 0 && threadIdx.x == 0) *fn2_fast = h[ncols + has_u0];
+        // PROI: the projection left h alone; the finalize reads h[i], h[i-1]
+        if (pub_rearm && blockIdx.x == 0 && threadIdx.x < 2 && ncols - 1 - int(threadIdx.x) >= 0)
+            const_cast<double*>(h)[ncols - 1 - int(threadIdx.x)] = 0.0;
+        return;
+    }
+    update_body<RED, B32, NT, false>(int(blockIdx.x), ldv, V, ncols, has_u0, u0val, nreal, h, src, dst, npart, part,
+                                     nrb, h_out, V32, fb, fn2_fast, nullptr, 0u, UpdTT{});
 }
 
 // The sharded step's update (after the one all-reduce of k_gemvt3's column
@@ -1318,7 +1482,8 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
               const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
               unsigned* gctr, double* h_out, bool nt, const int* flag, double* fn2_fast, const ProLaunch* pl) {
     const int cols = ncols + has_u0;
-    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS) + (pl ? 8 : 0));
+    const bool mrg = pl && pl->merged;
+    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS) + (pl ? 8 : 0) + (mrg ? ldv / UPD_ROWS : 0));
     // pl (PROI): the decision in this launch (8 more workgroups); alpha reduced by every
     // workgroup from apart (required) and published to pl->a3
     const ProLaunch pv = pl ? *pl : ProLaunch{};
@@ -1333,13 +1498,20 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
             std::fprintf(stderr, "gemvt_tt: the in-launch decision needs the alpha partials and the hand-off\n");
             std::abort();
         }
+#define EK_GEMVT_PRO(NT_, APE_)                                                      \
+    do {                                                                            \
+        if (!mrg) EK_GEMVT_TT((k_gemvt_pro<NT_, APE_, false, false>));              \
+        else if (pl->V32) EK_GEMVT_TT((k_gemvt_pro<NT_, APE_, true, true>));        \
+        else EK_GEMVT_TT((k_gemvt_pro<NT_, APE_, true, false>));                    \
+    } while (0)
         if (nt) {
-            if (wide) EK_GEMVT_TT((k_gemvt_pro<true, 24>));
-            else EK_GEMVT_TT((k_gemvt_pro<true, 12>));
+            if (wide) EK_GEMVT_PRO(true, 24);
+            else EK_GEMVT_PRO(true, 12);
         } else {
-            if (wide) EK_GEMVT_TT((k_gemvt_pro<false, 24>));
-            else EK_GEMVT_TT((k_gemvt_pro<false, 12>));
+            if (wide) EK_GEMVT_PRO(false, 24);
+            else EK_GEMVT_PRO(false, 12);
         }
+#undef EK_GEMVT_PRO
     } else if (nt) {
         if (wide) EK_GEMVT_TT((k_gemvt<true, true, 24>));
         else EK_GEMVT_TT((k_gemvt<true, true, 12>));

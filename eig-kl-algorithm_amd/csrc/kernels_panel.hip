@@ -166,6 +166,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     __shared__ long long bst[MAX_PANELS + 1];
     __shared__ int s_last;
     const int w = blockIdx.x, t = threadIdx.x;
+    if (fin.pub_rearm && w == 0 && t < PRO_PUB_WORDS) fin.pub_rearm[PRO_PUB_STRIDE * t] = 0u;
     const int r0 = m.wrow[w], nr = m.wrow[w + 1] - r0;
     // the value table in LDS when it fits (PANEL_LDS_DICT entries): the
     // per-entry lookup is then an LDS read instead of a second global gather
@@ -329,6 +330,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
         if (vcol) {
             const double v = f[r0 + r] * scale;
             vcol[r0 + r] = v;
+            if (fin.v32col) fin.v32col[r0 + r] = float(v);
             av += v * yr;
             wv += yr * yr;
         }

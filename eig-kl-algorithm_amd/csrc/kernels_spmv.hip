@@ -149,6 +149,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     __shared__ double wsum2[SPMV_THREADS / 64];
     __shared__ int s_last;
     const int t = threadIdx.x;
+    if (fin.pub_rearm && blockIdx.x == 0 && t < PRO_PUB_WORDS) fin.pub_rearm[PRO_PUB_STRIDE * t] = 0u;
     uint32_t wd[PER];
     int rb0 = 0, rb1 = 0;
     if constexpr (PK) {  // speculative: a long-row block's segment is padding
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
             if (vcol) {
                 const double v = f[r0] * scale;
                 vcol[r0] = v;
+                if (fin.v32col) fin.v32col[r0] = float(v);
                 if (apart) store_sc1(apart + blockIdx.x, v * (a * scale));
                 if (fin.wpart) fin.wpart[blockIdx.x] = (a * scale) * (a * scale);
             }
@@ -282,6 +284,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         if (t < nr) {
             const double v = fr * scale;
             vcol[r0 + t] = v;
+            if (fin.v32col) fin.v32col[r0 + t] = float(v);
             if (apart) {
                 av = v * yrow[t];
                 wv = yrow[t] * yrow[t];

@@ -3,7 +3,9 @@
 (EK_LIB_PATH), one child process per build: lambda, matvecs, projected steps,
 median solve time and an md5 of the Fiedler vector's bits.
 
-usage: python tools/lib_ab.py LIB_A LIB_B [workload ...]   (lcc1.15 ibm10 ibm01 syn0.25)"""
+usage: python tools/lib_ab.py LIB_A LIB_B [workload ...]   (lcc1.15 ibm10 ibm01 syn0.25)
+A side given as VAR=VALUE instead runs the built library with that variable
+set (e.g. EK_PRO_MERGE=0 EK_PRO_MERGE=1); EK_AB_ROUNDS alternates the sides."""
 import os
 import subprocess
 import sys
@@ -37,11 +39,16 @@ c.close()
 
 
 def main():
-    libs, work = sys.argv[1:3], sys.argv[3:] or ["ibm01", "lcc1.15"]
-    for lib in libs:
-        print(lib, flush=True)
-        subprocess.run([sys.executable, "-c", CHILD] + work, check=True, timeout=600,
-                       env=dict(os.environ, EK_LIB_PATH=os.path.abspath(lib)))
+    sides, work = sys.argv[1:3], sys.argv[3:] or ["ibm01", "lcc1.15"]
+    for _ in range(int(os.environ.get("EK_AB_ROUNDS", "1"))):
+        for side in sides:
+            print(side, flush=True)
+            if "=" in side and not side.endswith(".so"):
+                k, v = side.split("=", 1)
+                env = dict(os.environ, **{k: v})
+            else:
+                env = dict(os.environ, EK_LIB_PATH=os.path.abspath(side))
+            subprocess.run([sys.executable, "-c", CHILD] + work, check=True, timeout=600, env=env)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,8 @@ workgroup inside the projection launch (EK_PRO_INLAUNCH=1, the default).
 Modes alternate per round so box drift hits both; median Lanczos time per
 mode, matvecs, projected steps, and whether the two give the same bits.
 
-usage: python tools/proi_ab.py [ROUNDS] [workload ...]   (lcc1.15 ibm10 ibm01 lcc2 syn0.25)"""
+usage: python tools/proi_ab.py [ROUNDS] [workload ...]   (lcc1.15 ibm10 ibm01 lcc2 syn0.25)
+EK_AB_VAR=NAME toggles that variable instead (0 / 1), e.g. EK_PRO_MERGE."""
 import os
 import sys
 import time
@@ -27,6 +28,7 @@ def graph(ek, w):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    var = os.environ.get("EK_AB_VAR", "EK_PRO_INLAUNCH")
     work = sys.argv[2:] or ["lcc1.15", "ibm10", "ibm01"]
     ek = load_package()
     c = ek.Context(0)
@@ -37,7 +39,7 @@ def main():
         out = {}
         for r in range(rounds + 1):
             for mode in ("0", "1"):
-                os.environ["EK_PRO_INLAUNCH"] = mode
+                os.environ[var] = mode
                 t = time.time()
                 lam, v, st = c.lanczos_fiedler()
                 dt = time.time() - t
@@ -47,11 +49,11 @@ def main():
         same = all(np.array_equal(np.asarray(out["0"][k]).view(np.uint64), np.asarray(out["1"][k]).view(np.uint64))
                    for k in (0, 1))
         st0, st1 = out["0"][2], out["1"][2]
-        print(f"{w}: n={h.nodes} k_pro launch {np.median(ts['0']) * 1e3:.2f} ms | in-launch "
+        print(f"{w}: n={h.nodes} {var}=0 {np.median(ts['0']) * 1e3:.2f} ms | =1 "
               f"{np.median(ts['1']) * 1e3:.2f} ms | matvecs {st0['matvecs']}/{st1['matvecs']} projected "
               f"{st0['projected_steps']}/{st1['projected_steps']} | same bits {same} | "
               f"min {min(ts['0']) * 1e3:.2f} / {min(ts['1']) * 1e3:.2f} ms", flush=True)
-    os.environ.pop("EK_PRO_INLAUNCH", None)
+    os.environ.pop(var, None)
     c.close()
 
 
