@@ -231,6 +231,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip sub-configs, sweep, PMC and syn10 legs")
     ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--prof-dir", default=None,
+                    help="keep the rocprofv3 passes' CSVs here (default: a temporary directory)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -245,6 +247,9 @@ def main():
     if world != args.gpus:
         log(f"WORLD_SIZE {world} != --gpus {args.gpus}: reporting the {world} ranks that run")
     work = tempfile.mkdtemp(prefix=f"ekbench_r{rank}_")
+    if args.prof_dir:
+        work = os.path.join(os.path.abspath(args.prof_dir), f"rank{rank}")
+        os.makedirs(work, exist_ok=True)
     extras = not args.no_extras and world == 1
 
     # rocprofv3 passes first: child processes, before this process touches the GPU
@@ -664,7 +669,8 @@ def main():
     }
     print(json.dumps(out), flush=True)
     ctx.close()
-    shutil.rmtree(work, ignore_errors=True)
+    if not args.prof_dir:
+        shutil.rmtree(work, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
 
