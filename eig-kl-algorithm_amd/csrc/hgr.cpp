@@ -188,26 +188,74 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     ek::run_threads(T, [&](int t) {
         int64_t net = lines[size_t(t)];
         auto& pv = part[size_t(t)];
-        pv.reserve(size_t((cs[size_t(t) + 1] - cs[size_t(t)]) / 2 + 16));
+        const char* p = cs[size_t(t)];
+        const char* const e = cs[size_t(t) + 1];
+        // a pin takes at least two bytes (a digit and a separator) but the last
+        pv.resize(size_t((e - p) / 2 + 16));
+        int32_t* const out = pv.data();
+        size_t cnt = 0;
         const int64_t nodes = h->nodes;
-        for (const char* p = cs[size_t(t)]; p < cs[size_t(t) + 1] && net < nets; ++net) {
-            const char* r = static_cast<const char*>(std::memchr(p, '\n', size_t(cs[size_t(t) + 1] - p)));
-            const char* le = r ? r : cs[size_t(t) + 1];
-            const size_t before = pv.size();
-            if (!parse_line(p, le, [&](uint64_t v) {
-                    if (v < 1 || int64_t(v) > nodes) bad_pin = int64_t(v);
-                    pv.push_back(int32_t(v) - 1);
-                }))
-                bad = true;
-            h->net_ptr[size_t(net) + 1] = int64_t(pv.size() - before);
-            p = r ? r + 1 : cs[size_t(t) + 1];
+        auto emit = [&](uint64_t v) {
+            if (v < 1 || int64_t(v) > nodes) bad_pin = int64_t(v);
+            out[cnt++] = int32_t(v) - 1;
+        };
+        // one pass per line over digits, blanks and the newline; any other
+        // byte (or a token over 10 digits) re-parses the line with
+        // parse_line, the reference-semantics reader
+        while (p < e && net < nets) {
+            const char* const ls = p;
+            const size_t before = cnt;
+            uint64_t v = 0;
+            int nd = 0;
+            bool slow = false;
+            for (; p < e; ++p) {
+                const unsigned c = static_cast<unsigned char>(*p);
+                const unsigned d = c - unsigned('0');
+                if (d < 10u) {
+                    v = v * 10u + d;
+                    if (++nd > 10) {
+                        slow = true;
+                        break;
+                    }
+                } else if (c == ' ' || c == '\t' || c == '\r') {
+                    if (nd) {
+                        if (v > 0xffffffffull) {
+                            slow = true;
+                            break;
+                        }
+                        emit(v);
+                    }
+                    v = 0;
+                    nd = 0;
+                } else {
+                    slow = c != '\n';
+                    break;
+                }
+            }
+            if (!slow && nd) {
+                if (v > 0xffffffffull) slow = true;
+                else emit(v);
+            }
+            if (slow) {
+                cnt = before;
+                const char* r = static_cast<const char*>(std::memchr(ls, '\n', size_t(e - ls)));
+                const char* le = r ? r : e;
+                if (!parse_line(ls, le, emit)) bad = true;
+                p = le;
+            }
+            h->net_ptr[size_t(net) + 1] = int64_t(cnt - before);
+            if (p < e) ++p;  // the newline
+            ++net;
         }
+        pv.resize(cnt);
     });
+    pt.mark("parse (threads)");
     if (bad) ek::fail(EK_EINVAL, "%s: pin id overflows uint32", path);
     if (bad_pin.load() >= 0)
         ek::fail(EK_EINVAL, "%s: pin id %lld outside [1, %lld]", path, (long long)bad_pin.load(),
                  (long long)h->nodes);
     for (int64_t i = 0; i < nets; ++i) h->net_ptr[size_t(i) + 1] += h->net_ptr[size_t(i)];
+    pt.mark("net prefix");
     h->pins.resize(size_t(h->net_ptr.back()));
     std::vector<size_t> off(size_t(T) + 1, 0);
     for (int t = 0; t < T; ++t) off[size_t(t) + 1] = off[size_t(t)] + part[size_t(t)].size();
@@ -218,7 +266,7 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     // (a file far smaller than the cached buffers would keep them: shrink
     // what exceeds 4x this read's needs)
     if (buf.capacity() > 4 * buf.size() + (size_t(1) << 20)) ek::dvec<char>().swap(buf);
-    pt.mark("parse");
+    pt.mark("pins copy");
     *out = h.release();
     return EK_OK;
     EK_CATCH

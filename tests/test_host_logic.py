@@ -171,6 +171,65 @@ def test_hgr_read_errors(ek, tmp_path):
     assert e.value.code == ek.EK_EINVAL
 
 
+def _ref_hgr_lines(text):
+    """The reference readers' per-line extraction (cKL.cpp:92-116: getline, then
+    `ss >> node` until it fails), restated: whitespace-separated unsigned
+    integers (optional '+'), stopping at the first non-numeric token."""
+    ws = " \t\r\v\f"
+    lines = text.split("\n")
+    nets = int(lines[0].split()[0])
+    out = []
+    for i in range(nets):
+        line = lines[1 + i] if 1 + i < len(lines) else ""
+        pins, p, n = [], 0, len(line)
+        while True:
+            while p < n and line[p] in ws:
+                p += 1
+            if p >= n:
+                break
+            if line[p] == "+":
+                p += 1
+            if p >= n or not line[p].isdigit():
+                break
+            v = 0
+            while p < n and line[p].isdigit():
+                v = v * 10 + int(line[p])
+                p += 1
+            pins.append(v)
+            if p < n and line[p] not in ws:
+                break
+        out.append(pins)
+    return out
+
+
+def test_hgr_read_token_semantics(ek, tmp_path):
+    """The multi-threaded reader's fast line scan against the reference's
+    extraction rules on a file large enough for several parse threads, with
+    odd lines mixed in ('+' signs, trailing junk, tabs, CR, VT/FF, blank and
+    missing lines)."""
+    rng = np.random.default_rng(5)
+    nodes, nets = 1000, 90000
+    odd = ["+12 7", "7x 8", "a 5", "\t3\t4\r", "5\v6", "5\f7 9", "  9   10  ", "", "11 +", "4 5x", "0012 13"]
+    rows = []
+    for i in range(nets - 3):
+        if rng.random() < 0.03:
+            rows.append(odd[int(rng.integers(len(odd)))])
+        else:
+            k = int(rng.integers(2, 9))
+            rows.append(" ".join(str(int(x)) for x in rng.integers(1, nodes + 1, k)))
+    text = f"{nets} {nodes}\n" + "\n".join(rows) + "\n"  # the last 3 nets: missing lines
+    path = tmp_path / "odd.hgr"
+    path.write_text(text)
+    assert path.stat().st_size > 3 * 256 * 1024
+    g = ek.Hypergraph.read(str(path))
+    net_ptr, pins = g.pins()
+    ref = _ref_hgr_lines(text)
+    assert len(net_ptr) == nets + 1
+    for e in range(nets):
+        got = (pins[net_ptr[e]:net_ptr[e + 1]] + 1).tolist()
+        assert got == ref[e], (e, rows[e] if e < len(rows) else None, got, ref[e])
+
+
 # ------------------------------------------------------ EIG file + median
 @pytest.mark.parametrize("name", CIRCUITS)
 def test_eig_read_matches_reference_reader(ek, oracle, name):
