@@ -382,6 +382,9 @@ def main():
               ("t_read", "t_laplacian", "t_spmv_setup", "t_lanczos", "t_split", "t_kl_graph_wait", "t_kl_setup",
                "t_kl", "t_write", "t_total")}
     phases["lanczos_device_ms"] = round(float(np.median([x["total_ms"] for x in lz])), 3)
+    # the slowest step's phases (an outlier step shows which phase it lost time in)
+    worst = max(results, key=lambda r: r[0]["t_total"])[0]
+    phases_worst = {k: round(float(worst[k]), 4) for k in phases if k.startswith("t_")}
     off = ek.shard_map(h, world)  # the nnz-balanced map ek_solve_file's device build used
     row0, nrows = int(off[rank]), int(off[rank + 1] - off[rank])
     alg_bytes = ctx.spmv_bytes(fused=False)  # 12 nnz + 4(nrows+1) + 8n (x) + 8 nrows (y)
@@ -656,7 +659,7 @@ def main():
                    "kl_iterations": last["kl"]["iterations"], "kl_loop_ms": round(last["kl"]["loop_ms"], 3),
                    "initial_cut": last["kl"]["initial_cut"], "best_cut": last["kl"]["best_cut"],
                    "net_cut_best": last["kl"]["net_cut_best"], "net_cut_final": last["kl"]["net_cut_final"],
-                   "best_iter": last["kl"]["best_iter"], "phases_median_s": phases,
+                   "best_iter": last["kl"]["best_iter"], "phases_median_s": phases, "phases_slowest_step_s": phases_worst,
                    "step_walls_s": [round(w, 4) for w in step_walls],
                    "step_totals_s": [round(r[0]["t_total"], 4) for r in results],
                    "comm_ms_per_step": round(comm_ms, 3), "spmv_us_max_rank": round(spmv_us_max, 3),

@@ -194,23 +194,25 @@ int main(int argc, char** argv) {
         rep("gemvt (prod, 1024x8 tiles)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_gemvt<false, false>), dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
                                       b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
+                                      nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                      ek::dev::ProLaunch{});
             }),
             vbytes + 8.0 * n);
         rep("gemvt + column-sum hand-off", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_gemvt<false, false>), dim3(nrb * ((J + 1 + GT_COLS - 1) / GT_COLS)), dim3(256), 0, s, a,
                                       b, 0, ldv, nrb, V, J, 1, u0val, n, w, part, nullptr, nullptr, nullptr, nullptr,
-                                      nullptr, nullptr, 1, nullptr, nullptr, 0, nullptr, gctr, h);
+                                      nullptr, nullptr, 1, nullptr, nullptr, 0, nullptr, gctr, h, nullptr, nullptr,
+                                      ek::dev::ProLaunch{});
             }),
             vbytes + 8.0 * n);
         rep("update<true> (prod, RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<true, false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
-                                      1, u0val, n, nullptr, w, f1, npart, part, nrb, h, nullptr, nullptr, nullptr);
+                                      1, u0val, n, nullptr, w, f1, npart, part, nrb, h, nullptr, nullptr, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
         rep("update<false> (prod, h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<false, false, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
-                                      J, 1, u0val, n, h, w, f2, npart, nullptr, 0, nullptr, nullptr, nullptr, nullptr);
+                                      J, 1, u0val, n, h, w, f2, npart, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
             }),
             vbytes + 16.0 * n);
         {  // the fp32 shadow: tiny coefficients (the accuracy test passes), ||src||^2 = 1
@@ -223,12 +225,12 @@ int main(int argc, char** argv) {
         }
         rep("update<true,B32> (RED)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<true, true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V, J,
-                                      1, u0val, n, nullptr, w, f1, npart, psm, nrb, h, V32, fb, nullptr);
+                                      1, u0val, n, nullptr, w, f1, npart, psm, nrb, h, V32, fb, nullptr, nullptr, nullptr);
             }),
             vbytes / 2 + 16.0 * n);
         rep("update<false,B32> (h given)", timeit([&](hipEvent_t a, hipEvent_t b) {
                 hipExtLaunchKernelGGL((k_update<false, true, false>), dim3(ldv / UPD_ROWS), dim3(256), 0, s, a, b, 0, ldv, V,
-                                      J, 1, u0val, n, hsm, w, f2, npart, nullptr, 0, nullptr, V32, fb, nullptr);
+                                      J, 1, u0val, n, hsm, w, f2, npart, nullptr, 0, nullptr, V32, fb, nullptr, nullptr, nullptr);
             }),
             vbytes / 2 + 16.0 * n);
         {
