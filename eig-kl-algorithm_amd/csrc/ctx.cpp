@@ -2123,6 +2123,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         HIPCHK(hipMemcpyAsync(&r2, sc, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
+    if (L.proi) {  // the in-launch hand-offs' waits are bounded: any that gave up fails the solve
+        ek::dev::ProState ps{};
+        HIPCHK(hipMemcpyAsync(&ps, c->prost.p, sizeof(ps), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (ps.timeouts)
+            ek::fail(EK_EHIP, "Lanczos: %d in-launch wait(s) of the partially reorthogonalised step gave up "
+                              "(EK_PRO_INLAUNCH=0 runs the step without them)", ps.timeouts);
+    }
     // deterministic sign: the entry of largest magnitude (first on ties) is positive
     int64_t imax = 0;
     for (int64_t i = 1; i < n; ++i)

@@ -403,6 +403,8 @@ struct ProState {
     double anorm;   // running estimate of ||L|| (max |alpha_j| + beta_j + beta_{j+1})
     int force;      // the next step projects (the second of a pair)
     int projected;  // steps that projected, this solve
+    int timeouts;   // in-launch waits that gave up (PROI; the host fails the solve on any)
+    int pad;
 };
 void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,
               const double* bov_i, const double* alpha, const double* offd, double* omega, ProState* st, int* flags,

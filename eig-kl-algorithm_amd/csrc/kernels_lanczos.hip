@@ -354,7 +354,7 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
 
 // PROI: the step's decision is taken in this launch (ek_internal.hpp
 // ProLaunch); a poller's word, 1 + decision (thread 0)
-__device__ __forceinline__ int pro_poll(const unsigned* pub) {
+__device__ __forceinline__ int pro_poll(const unsigned* pub, int* err) {
     unsigned v = 0u;
     // (bounded: the decider waits on nothing, so this ends in a few us; the
     // bound only keeps a broken hand-off from hanging the GPU)
@@ -363,15 +363,17 @@ __device__ __forceinline__ int pro_poll(const unsigned* pub) {
         if (v != 0u) break;
         __builtin_amdgcn_s_sleep(8);
     }
+    if (v == 0u) atomicAdd(err, 1);  // (the host fails the solve)
     return v != 0u ? int(v) : 2;
 }
 // thread 0: wait until the counter reaches target (bounded like pro_poll);
 // 1 when it did
-__device__ __forceinline__ int pro_wait(const unsigned* ctr, unsigned target) {
+__device__ __forceinline__ int pro_wait(const unsigned* ctr, unsigned target, int* err) {
     for (int it = 0; it < (1 << 22); ++it) {
         if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return 1;
         __builtin_amdgcn_s_sleep(4);
     }
+    atomicAdd(err, 1);  // (the host fails the solve)
     return 0;
 }
 
@@ -385,6 +387,7 @@ struct UpdTT {
     const double* bov_i = nullptr;
     const double* apart = nullptr;
     int nparts = 0;
+    int* err = nullptr;  // ProState::timeouts
 };
 template <bool RED, bool B32, bool NT, bool MRG>
 __device__ __forceinline__ void update_body(int blk, int ldv, const double* __restrict__ V, int ncols, int has_u0,
@@ -442,12 +445,12 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 const int blk = orig - nproj, tot = ncols + has_u0;
                 unsigned* done = pl.pub + PRO_PUB_STRIDE * PRO_PUB;
                 __shared__ int s_ud;
-                if (t == 0) s_ud = pro_poll(pl.pub + PRO_PUB_STRIDE * (orig % 8));
+                if (t == 0) s_ud = pro_poll(pl.pub + PRO_PUB_STRIDE * (orig % 8), &pl.st->timeouts);
                 __syncthreads();
                 if (s_ud == 1) {  // a skipped step: f = f'; ||f||^2 = ||f'||^2 once the norm is in
                     if (blk == 0) {
                         if (t == 0) {
-                            (void)pro_wait(done, 1u);
+                            (void)pro_wait(done, 1u, &pl.st->timeouts);
                             if (fn2_fast) *fn2_fast = ld_sc1(h_out + tot);
                         }
                         if (t < 2 && ncols - 1 - t >= 0) h_out[ncols - 1 - t] = 0.0;  // (the finalize's h[i], h[i-1])
@@ -462,6 +465,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 tt.bov_i = bov_i;
                 tt.apart = apart;
                 tt.nparts = nparts;
+                tt.err = &pl.st->timeouts;
                 update_body<false, B32U, NT, true>(blk, ldv, V, ncols, has_u0, u0val, nreal, h_out, fp, fp, pl.npart,
                                                    nullptr, nrb, nullptr, pl.V32, pl.fb, fn2_fast, done,
                                                    unsigned(ncg + 1), tt);
@@ -487,7 +491,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     __shared__ int s_dec;
     if constexpr (PROI) {
         if (j0 != 0) {
-            if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd);
+            if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd, &pl.st->timeouts);
             __syncthreads();
             if (s_dec == 1) return;
         }
@@ -586,7 +590,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
             // ||f'||^2 (both outcomes need it): its hand-off before the decision
             gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out, MRG ? nullptr : fn2_fast,
                             false, MRG ? pl.pub + PRO_PUB_STRIDE * PRO_PUB : nullptr);
-            if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd);
+            if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd, &pl.st->timeouts);
             __syncthreads();
             skip = s_dec == 1;
             if constexpr (MRG) {
@@ -1065,8 +1069,7 @@ __device__ __forceinline__ void update_body(int blk, int ldv, const double* __re
         load_batch(bb, UB);
     }
     if constexpr (MRG) {
-        __shared__ int s_ok;
-        if (threadIdx.x == 0) s_ok = pro_wait(done, done_target);
+        if (threadIdx.x == 0) (void)pro_wait(done, done_target, tt.err);
         __syncthreads();
     }
     auto put = [&](int j, double v) {

@@ -240,7 +240,8 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
         // default format is printf's %g; std::to_chars(general, 6) is specified
         // as that printf conversion and runs ~4x faster than snprintf (equal on
         // 20 M random floats)
-        const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, iters / 4096)));
+        // (~0.1 us a row: 1,024 rows a thread at least)
+        const int T = int(std::min<int64_t>(host_threads(), std::max<int64_t>(1, iters / 1024)));
         // one text buffer, each thread's rows in its own 48-B-per-row region
         // (kept across calls like the parse buffers: no zero-fill, no
         // first-touch faults per step)
