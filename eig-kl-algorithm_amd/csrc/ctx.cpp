@@ -1200,6 +1200,7 @@ struct Lanczos {
     // recurrence against thresh; eps1 = eps sqrt(n), its rounding term)
     bool pro = false;
     double pro_thresh = 0.0, pro_eps1 = 0.0;
+    int pro_cgw = 0;  // ProLaunch::cgw (EK_PRO_CGW)
     // the decision inside the projection launch (no k_pro launch; needs the
     // projection's hand-off, upd_red 2).  EK_PRO_INLAUNCH=0: the k_pro launch
     bool proi = false;
@@ -1369,6 +1370,7 @@ struct Lanczos {
             pl.m = m;
             pl.thresh = pro_thresh;
             pl.eps1 = pro_eps1;
+            pl.cgw = pro_cgw;
             if (pro_merge) {
                 pl.merged = 1;
                 pl.npart = c->npart.as<double>();
@@ -1640,6 +1642,15 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.pro_eps1 = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     if (const char* e = std::getenv("EK_PRO_INLAUNCH"); L.pro) L.proi = !(e && e[0] == '0');
     if (const char* e = std::getenv("EK_PRO_MERGE"); L.proi) L.pro_merge = !(e && e[0] == '0');
+    // column groups walked per projection workgroup: about 850 projection
+    // workgroups, at least 3 per row block (the 1.15x LCC, 207 row blocks:
+    // 4; ibm01 / ibm10: one workgroup per tile as before).  A skipped step
+    // then dispatches ~850 + 422 workgroups instead of up to ~3,100 (headline
+    // Lanczos 20.4 -> 19.4 ms; ibm10 and ibm01 lost 3-10 % at 3-4 per row
+    // block: too few workgroups for the projecting steps;
+    // profiles/r04/cgw/).  EK_PRO_CGW overrides (0: one workgroup per tile)
+    L.pro_cgw = std::max(3, 850 / std::max(1, L.nrb));
+    if (const char* e = std::getenv("EK_PRO_CGW"); e && e[0]) L.pro_cgw = std::atoi(e);
 
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);

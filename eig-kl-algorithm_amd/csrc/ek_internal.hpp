@@ -434,6 +434,12 @@ struct ProLaunch {
     const float* V32 = nullptr;   // the fp32 shadow (B32 update), column i from the SpMV
     unsigned* fb = nullptr;       // B32 fp64-fallback count
     int merged = 0;               // the update's workgroups in this launch (no update launch)
+    // > 0: at most cgw workgroups per row block, each walking the column
+    // groups cg0, cg0 + cgw, ... (f' formed once per workgroup; a skipped
+    // step dispatches nrb * cgw projection workgroups instead of nrb * ncg).
+    // The partials of every (row block, column group) tile, and so every
+    // bit, are the same as with one workgroup per tile (cgw = 0)
+    int cgw = 0;
     int seg0 = 0, m = 0;
     double thresh = 0.0, eps1 = 0.0;
 };

@@ -420,6 +420,8 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     __shared__ double s_alpha;
     const int t = threadIdx.x;
     const int ncg = (ncols + has_u0 + GT_COLS - 1) / GT_COLS;
+    // PROI with pl.cgw: ncgl workgroups per row block walk the ncg groups
+    const int ncgl = PROI && pl.cgw > 0 ? min(ncg, pl.cgw) : ncg;
     int nwg = int(gridDim.x), orig = int(blockIdx.x);
     if constexpr (PROI) {
         // the decider: the first of 8 extra workgroups ahead of the map (the
@@ -440,7 +442,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         if constexpr (MRG) {
             // the update's workgroups, after every projection workgroup (so
             // they wait only on workgroups dispatched before them)
-            const int nproj = nrb * ncg;
+            const int nproj = nrb * ncgl;
             if (orig >= nproj) {
                 const int blk = orig - nproj, tot = ncols + has_u0;
                 unsigned* done = pl.pub + PRO_PUB_STRIDE * PRO_PUB;
@@ -486,8 +488,8 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     // f' first.  skip is uniform over the workgroup in every form
     bool skip = !PROI && flag && *flag == 0;
     if (skip && orig >= nrb) return;
-    const int v = skip ? orig * ncg : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-    const int rbk = v / ncg, j0 = (v % ncg) * GT_COLS;
+    const int v = skip ? orig * ncgl : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+    const int rbk = v / ncgl, j0 = (v % ncgl) * GT_COLS;
     __shared__ int s_dec;
     if constexpr (PROI) {
         if (j0 != 0) {
@@ -602,21 +604,26 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
             }
             if (skip) return;
         }
-        if (!skip) {
-            {
-#pragma unroll
-                for (int k = 0; k < KR; ++k) {
-                    const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
-#pragma unroll
-                    for (int jj = 0; jj < GT_COLS; ++jj)
-                        vs[k][jj] = ld_basis<NT>(V + size_t(min(j0 + jj, jmax)) * ldv + r);
-                }
-            }
-        }
     }
     if (skip) {
         gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr, h_out, fn2_fast);
         return;
+    }
+    // the tiles: this workgroup's column groups (one unless PROI walks several)
+    const int jstep = ncgl * GT_COLS, jend = PROI ? ncg * GT_COLS : j0 + 1;
+    for (int jc = j0; jc < jend; jc += jstep) {
+    if (PROI) {
+        if (jc != j0) {
+            __syncthreads();  // (red and s_last of the previous tile read)
+#pragma unroll
+            for (int jj = 0; jj < GT_COLS; ++jj) acc[jj] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
+#pragma unroll
+            for (int jj = 0; jj < GT_COLS; ++jj) vs[k][jj] = ld_basis<NT>(V + size_t(min(jc + jj, jmax)) * ldv + r);
+        }
     }
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -624,7 +631,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         const double2 x = xs[k];
 #pragma unroll
         for (int jj = 0; jj < GT_COLS; ++jj) {
-            const int j = j0 + jj;
+            const int j = jc + jj;
             if (j < ncols) {
                 const double2 v = vs[k][jj];
                 acc[jj] += __builtin_fma(v.x, x.x, v.y * x.y);
@@ -661,15 +668,15 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     __syncthreads();
     const int tot = ncols + has_u0;
     if (!h_out) {
-        if (t < GT_COLS && j0 + t < tot) part[size_t(j0 + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-        if (nrm && j0 == 0 && t == 0) part[size_t(tot) * nrb + rbk] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
-        return;
+        if (t < GT_COLS && jc + t < tot) part[size_t(jc + t) * nrb + rbk] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+        if (nrm && jc == 0 && t == 0) part[size_t(tot) * nrb + rbk] = (nred[0] + nred[1]) + (nred[2] + nred[3]);
+        continue;
     }
     // hand-off: every store below is made by wave 0
     __shared__ int s_last;
-    if (t < GT_COLS && j0 + t < tot) st_sc1(part + size_t(j0 + t) * nrb + rbk, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]));
-    if (!PROI && nrm && j0 == 0 && t == 0) st_sc1(part + size_t(tot) * nrb + rbk, (nred[0] + nred[1]) + (nred[2] + nred[3]));
-    const int cg = j0 / GT_COLS;
+    if (t < GT_COLS && jc + t < tot) st_sc1(part + size_t(jc + t) * nrb + rbk, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]));
+    if (!PROI && nrm && jc == 0 && t == 0) st_sc1(part + size_t(tot) * nrb + rbk, (nred[0] + nred[1]) + (nred[2] + nred[3]));
+    const int cg = jc / GT_COLS;
     unsigned* ctr = gctr + size_t(cg) * (GT_SUB + 1) * 64;
     if (t == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -682,14 +689,14 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         s_last = last;
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) continue;
     // this group's columns (+ ||rhs||^2 in group 0): 8 lanes per column, lane
     // l summing blocks l, l + 8, ... in order (col_sum2's loads and adds), then
     // the xor tree
     const int gq = t / CS_LANES, l = t % CS_LANES;
-    const int ncol = min(GT_COLS, tot - j0) + ((nrm && j0 == 0 && !PROI) ? 1 : 0);  // (PROI: the norm went before)
+    const int ncol = min(GT_COLS, tot - jc) + ((nrm && jc == 0 && !PROI) ? 1 : 0);  // (PROI: the norm went before)
     if (gq < ncol) {
-        const int j = gq < GT_COLS && j0 + gq < tot ? j0 + gq : tot;  // (the last group member: the norm column)
+        const int j = gq < GT_COLS && jc + gq < tot ? jc + gq : tot;  // (the last group member: the norm column)
         const double* pc = part + size_t(j) * nrb;
         constexpr int CB = 32;
         double a = 0.0;
@@ -714,6 +721,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
             __hip_atomic_fetch_add(pl.pub + PRO_PUB_STRIDE * PRO_PUB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t < GT_SUB + 1) ctr[t * 64] = 0u;  // re-armed for the next launch (visible at the kernel boundary)
+    }  // tiles
 }
 
 #define EK_GEMVT_PARAMS                                                                                               \
@@ -1486,7 +1494,8 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
               unsigned* gctr, double* h_out, bool nt, const int* flag, double* fn2_fast, const ProLaunch* pl) {
     const int cols = ncols + has_u0;
     const bool mrg = pl && pl->merged;
-    const dim3 g(nrb * ((cols + GT_COLS - 1) / GT_COLS) + (pl ? 8 : 0) + (mrg ? ldv / UPD_ROWS : 0));
+    const int ncg = (cols + GT_COLS - 1) / GT_COLS, ncgl = pl && pl->cgw > 0 ? std::min(ncg, pl->cgw) : ncg;
+    const dim3 g(nrb * ncgl + (pl ? 8 : 0) + (mrg ? ldv / UPD_ROWS : 0));
     // pl (PROI): the decision in this launch (8 more workgroups); alpha reduced by every
     // workgroup from apart (required) and published to pl->a3
     const ProLaunch pv = pl ? *pl : ProLaunch{};

@@ -399,7 +399,8 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
 @pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_ALPHA_LAST=1", "EK_UPD_RED=0", "EK_UPD_RED=1",
                                     "EK_UPD_RED=2", "EK_V_NT=1", "pro:EK_UPD_RED=0", "pro:EK_UPD_RED=2",
-                                    "pro:EK_V_NT=1", "pro:EK_PRO_INLAUNCH=0", "pro:EK_PRO_MERGE=0"])
+                                    "pro:EK_V_NT=1", "pro:EK_PRO_INLAUNCH=0", "pro:EK_PRO_MERGE=0",
+                                    "pro:EK_PRO_CGW=0", "pro:EK_PRO_CGW=1"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
@@ -414,7 +415,11 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     * the partial reorthogonalisation's decision taken inside the projection
       launch (the default with the projection's hand-off) against the k_pro
       launch (EK_PRO_INLAUNCH=0), and the update inside that launch (the
-      default) against its own launch (EK_PRO_MERGE=0).
+      default) against its own launch (EK_PRO_MERGE=0);
+    * that launch's projection workgroups walking several column groups
+      each (the default: ~850 projection workgroups, at least 3 per row
+      block; EK_PRO_CGW=1: one per row block walking them all) against one
+      workgroup per (row block, column group) tile (EK_PRO_CGW=0).
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses.  These run the full
     reorthogonalisation (EK_REORTH=1); "pro:" switches hold the partial one
