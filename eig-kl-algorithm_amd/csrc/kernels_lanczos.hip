@@ -1393,40 +1393,51 @@ __global__ __launch_bounds__(256) void k_three_term(const double* __restrict__ a
 // fetched from memory once and re-read from that XCD's L2.  (A 2-D grid ran
 // every row block of column group 0 first: at 10x, V = 1.6 GB, the tile came
 // from HBM once per column group, 1.34 ms per restart.)
+template <int IB>
 __global__ __launch_bounds__(256) void k_gemm_vq(int ldv, const double* __restrict__ V, int m,
                                                  const double* __restrict__ Q, int kk, double* __restrict__ out,
                                                  float* __restrict__ out32) {
     constexpr int TJ = 8;
-    __shared__ double qs[MAX_NCV][TJ];
+    // coefficient rows past m are zero (the last trip's clamped basis rows
+    // are multiplied by 0.0, as before: the same products and sums)
+    __shared__ __attribute__((aligned(16))) double qs[MAX_NCV + IB][TJ];
     const int ncg = (kk + TJ - 1) / TJ;
     const int nwg = int(gridDim.x), orig = int(blockIdx.x), xcd = orig % 8, q8 = nwg / 8, rr = nwg % 8;
     const int vb = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
     const int rbk = vb / ncg, j0 = (vb % ncg) * TJ;
-    for (int i = threadIdx.x; i < m * TJ; i += 256) {
+    const int mp = (m + IB - 1) / IB * IB;
+    for (int i = threadIdx.x; i < mp * TJ; i += 256) {
         const int row = i / TJ, jj = i % TJ;
-        qs[row][jj] = (j0 + jj < kk) ? Q[size_t(j0 + jj) * m + row] : 0.0;
+        qs[row][jj] = (row < m && j0 + jj < kk) ? Q[size_t(j0 + jj) * m + row] : 0.0;
     }
     __syncthreads();
     const size_t r = (size_t(rbk) * 256 + threadIdx.x) * 2;
     double2 acc[TJ];
 #pragma unroll
     for (int jj = 0; jj < TJ; ++jj) acc[jj] = make_double2(0.0, 0.0);
-    // 8 basis rows' loads in flight per trip (clamped index, coefficient 0
-    // past the end; the sums keep their order)
-    constexpr int IB = 8;
+    // IB basis rows' loads in flight per trip (clamped index; the sums keep
+    // their order, so IB does not change a bit)
     for (int i0 = 0; i0 < m; i0 += IB) {
         double2 v[IB];
 #pragma unroll
         for (int u = 0; u < IB; ++u) v[u] = *reinterpret_cast<const double2*>(V + size_t(min(i0 + u, m - 1)) * ldv + r);
+        // (every load of the trip issued before the first product: left
+        // alone the scheduler interleaved them, two loads in flight)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < IB; ++u) {
-            const int i = min(i0 + u, m - 1);
-            const bool live = i0 + u < m;
+            const double2* qr = reinterpret_cast<const double2*>(&qs[i0 + u][0]);
+            double q[TJ];
+#pragma unroll
+            for (int h = 0; h < TJ / 2; ++h) {
+                const double2 qq = qr[h];
+                q[2 * h] = qq.x;
+                q[2 * h + 1] = qq.y;
+            }
 #pragma unroll
             for (int jj = 0; jj < TJ; ++jj) {
-                const double q = live ? qs[i][jj] : 0.0;
-                acc[jj].x += v[u].x * q;
-                acc[jj].y += v[u].y * q;
+                acc[jj].x += v[u].x * q[jj];
+                acc[jj].y += v[u].y * q[jj];
             }
         }
     }
@@ -1658,8 +1669,14 @@ void inject_random(hipStream_t s, double* f, int ldv, long long row0, long long 
 }
 
 void gemm_vq(hipStream_t s, int ldv, const double* V, int m, const double* Q, int kk, double* out, float* out32) {
-    hipLaunchKernelGGL(k_gemm_vq, dim3((ldv / UPD_ROWS) * ((kk + 7) / 8)), dim3(256), 0, s, ldv, V, m, Q, kk, out,
-                       out32);
+    static const int ib = [] {
+        const char* e = std::getenv("EK_VQ_IB");
+        return e && e[0] ? std::atoi(e) : 16;
+    }();
+    const dim3 g((ldv / UPD_ROWS) * ((kk + 7) / 8));
+    if (ib >= 32) hipLaunchKernelGGL(k_gemm_vq<32>, g, dim3(256), 0, s, ldv, V, m, Q, kk, out, out32);
+    else if (ib >= 16) hipLaunchKernelGGL(k_gemm_vq<16>, g, dim3(256), 0, s, ldv, V, m, Q, kk, out, out32);
+    else hipLaunchKernelGGL(k_gemm_vq<8>, g, dim3(256), 0, s, ldv, V, m, Q, kk, out, out32);
 }
 
 void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart) {
