@@ -2031,7 +2031,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // one workgroup, k_apply_rots, lost: ~9k dependent rotations took 1.36
         // ms per restart against ~0.3 ms on the host for all of Q.)
         rots.clear();
-        for (int i = knew; i < m; ++i) ek::tridiag_qr_shift(m, dd.data(), ee.data(), theta[size_t(i)], rots);
+        ek::tridiag_qr_shifts(m, dd.data(), ee.data(), theta.data() + knew, m - knew, rots);
         double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
         ek::accumulate_q(m, rots, knew + 1, Q, qscratch);
         const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)

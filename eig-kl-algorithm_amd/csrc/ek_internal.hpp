@@ -126,6 +126,9 @@ struct QRot {
     double c, s;
 };
 void tridiag_qr_shift(int m, double* d, double* e, double mu, std::vector<QRot>& rots);
+// tridiag_qr_shift with mus[0], ..., mus[ns-1] in turn (the same bits and
+// rotations, in the same order), two consecutive chases interleaved
+void tridiag_qr_shifts(int m, double* d, double* e, const double* mus, int ns, std::vector<QRot>& rots);
 // columns [0, kk) of Q = I G_1 ... G_R (rots in order) into Qcm (col-major
 // m x kk); X is scratch
 void accumulate_q(int m, const std::vector<QRot>& rots, int kk, double* Qcm, std::vector<double>& X);
