@@ -1749,8 +1749,21 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     if (c->mr) HIPCHK(hipMemsetAsync(c->xfull.p, 0, c->xfull.bytes, s));
     if (!c->cstream) {  // mid-cycle check resources, created once per context
         HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+        // chk_done orders the check's copy (cstream, same device) after a
+        // chunk: a device-scope release is all it needs.  With the default
+        // system-scope fence every chunk boundary left the compute queue idle
+        // for the fence's L2 write-back (6-15 us at each of ~58 boundaries a
+        // solve, kernel trace).  EK_CHK_FENCE: 0 system (the HIP default), 1
+        // device-scope release (default), 2 no fence
+        static const int chk_fence = [] {
+            const char* e = std::getenv("EK_CHK_FENCE");
+            return e && e[0] ? std::atoi(e) : 1;
+        }();
+        const unsigned done_flags = hipEventDisableTiming | (chk_fence == 1   ? hipEventReleaseToDevice
+                                                             : chk_fence == 2 ? hipEventDisableSystemFence
+                                                                              : 0u);
         for (int i = 0; i < 2; ++i) {
-            HIPCHK(hipEventCreateWithFlags(&c->chk_done[i], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&c->chk_done[i], done_flags));
             HIPCHK(hipEventCreateWithFlags(&c->chk_copied[i], hipEventDisableTiming));
         }
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 4 * size_t(ek::dev::MAX_NCV + 2) * 8,
