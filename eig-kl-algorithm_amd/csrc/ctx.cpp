@@ -178,6 +178,7 @@ struct ek_ctx {
     // pinned slots of {alpha, offd, fn2} and their events (created on first use)
     hipStream_t cstream = nullptr;
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
+    hipEvent_t fin_ev = nullptr;  // the final Ritz vector's host copy landed
     double* chk_pin = nullptr;
     double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1)), then the kept
                               // projected matrix for k_pro (2 x (MAX_NCV + 2))
@@ -396,6 +397,7 @@ void ek_destroy(ek_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {
+        if (i == 0 && c->fin_ev) (void)hipEventDestroy(c->fin_ev);
         if (c->chk_done[i]) (void)hipEventDestroy(c->chk_done[i]);
         if (c->chk_copied[i]) (void)hipEventDestroy(c->chk_copied[i]);
     }
@@ -2103,7 +2105,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     ek::dev::gemm_vq(s, L.ldv, L.V(), mf, c->Qd.as<double>(), 1, xloc);
     // full vector on every rank; copied out through pinned staging kept by the
     // context (pageable copies of these 2 x 8n bytes cost ~0.5 ms a solve)
-    const size_t need = size_t(n) + size_t(std::max<int64_t>(c->nrows, 1));
+    // (+ 4,096: the final step's small read-backs, below)
+    const size_t need = size_t(n) + size_t(std::max<int64_t>(c->nrows, 1)) + 4096;
     if (c->pin_doubles < need) {
         if (c->pin) HIPCHK(hipHostFree(c->pin));
         c->pin = nullptr;
@@ -2127,8 +2130,73 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         }
     }
     HIPCHK(hipMemcpyAsync(v, xc, size_t(n) * 8, hipMemcpyDeviceToHost, s));
+    // single context: the residual (a diagnostic) is reduced on the device
+    // while the host scales the vector, and the final read-backs (residual
+    // partials, the in-launch waits' state, the fp64-fallback count) land with
+    // ONE synchronisation after fiedler_scale is queued.  (Reading the
+    // 1.7 MB residual vector back, summing it on the host and syncing three
+    // times left the GPU idle ~0.35 ms a solve at the headline.)
+    const bool fin_fast = !c->mr;
+    double* rpart = c->pin + size_t(n) + size_t(std::max<int64_t>(c->nrows, 1));  // nub <= 4,096 - 8
+    ek::dev::ProState* ps_pin = reinterpret_cast<ek::dev::ProState*>(rpart + 4096 - 8);
+    unsigned* fb_pin = reinterpret_cast<unsigned*>(rpart + 4096 - 2);
+    if (fin_fast && L.nub > 4096 - 8) ek::fail(EK_ESTATE, "Lanczos: %d residual partials", L.nub);
+    if (fin_fast) {
+        if (!c->fin_ev) HIPCHK(hipEventCreateWithFlags(&c->fin_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->fin_ev, s));
+    }
     // residual ||L x - lambda x|| on the owned rows
     ek::dev::spmv(s, spmv_mat(c), xg, c->w.as<double>(), nullptr, nullptr, nullptr, nullptr);
+    if (fin_fast) {
+        ek::dev::resid_partial(s, L.ldv, c->w.as<double>(), xc, lambda, int(c->nrows), c->npart.as<double>());
+        HIPCHK(hipMemcpyAsync(rpart, c->npart.p, size_t(L.nub) * 8, hipMemcpyDeviceToHost, s));
+        if (L.pro) HIPCHK(hipMemcpyAsync(ps_pin, c->prost.p, sizeof(ek::dev::ProState), hipMemcpyDeviceToHost, s));
+        if (L.b32) HIPCHK(hipMemcpyAsync(fb_pin, c->fbk.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventSynchronize(c->fin_ev));
+        double nx2 = 0.0;
+        for (int64_t i = 0; i < n; ++i) nx2 += v[i] * v[i];
+        if (!(nx2 > 0.0) || !std::isfinite(nx2)) {
+            HIPCHK(hipStreamSynchronize(s));
+            ek::fail(EK_ENOCONV, "Lanczos: the Ritz vector is zero or not finite (|x|^2 = %g)", nx2);
+        }
+        const double inv = 1.0 / std::sqrt(nx2);
+        int64_t imax = 0;
+        for (int64_t i = 1; i < n; ++i)
+            if (std::fabs(v[i]) > std::fabs(v[imax])) imax = i;
+        const double sgn = v[imax] < 0 ? -inv : inv;
+        c->fied.ensure(size_t(n) * 8);
+        ek::dev::fiedler_scale(s, xc, sgn, int(n), c->fied.as<double>());
+        HIPCHK(hipGetLastError());
+        c->fied_n = n;
+        HIPCHK(hipStreamSynchronize(s));
+        double rs = 0.0;
+        for (int b = 0; b < L.nub; ++b) rs += rpart[b];
+        const double r2 = rs * inv * inv;
+        if (L.proi && ps_pin->timeouts)
+            ek::fail(EK_EHIP, "Lanczos: %d in-launch wait(s) of the partially reorthogonalised step gave up "
+                              "(EK_PRO_INLAUNCH=0 runs the step without them)", ps_pin->timeouts);
+        if (lambda_out) *lambda_out = lambda;
+        if (v_out)
+            for (int64_t i = 0; i < n; ++i) v_out[i] = v[i] * sgn;
+        if (stats) {
+            stats->restarts = restarts;
+            stats->matvecs = L.matvecs;
+            stats->converged = 1;
+            stats->residual = std::sqrt(r2);
+            stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            stats->spmv_ms = L.spmv_ms;
+            stats->spmv_timed = L.spmv_timed;
+            stats->comm_ms = c->comm_ms;
+            stats->allgathers = int32_t(c->n_ag);
+            stats->allreduces = int32_t(c->n_ar);
+            stats->update32_steps = L.u32_steps;
+            stats->update32_fallbacks = L.b32 ? int32_t(*fb_pin) : 0;
+            stats->projected_steps = L.pro ? ps_pin->projected : L.matvecs;
+            stats->reprojected = L.repairs;
+            stats->ortho_max = ortho_max;
+        }
+        return EK_OK;
+    }
     if (c->nrows) HIPCHK(hipMemcpyAsync(y, c->w.p, size_t(c->nrows) * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     double r2 = 0.0, nx2 = 0.0;

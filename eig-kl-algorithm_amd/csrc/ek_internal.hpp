@@ -477,6 +477,8 @@ void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x
 // x = x / sqrt(*n2) ... and deflate helpers
 void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* mean_sum, double inv_n);
 void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares);
+// part[b] = sum over block b's real rows (512 a block) of (w - lambda x)^2
+void resid_partial(hipStream_t s, int ldv, const double* w, const double* x, double lambda, int nreal, double* part);
 // x[0:ldv) = Park-Miller start vector over global rows row0.. (0 past nreal)
 void start_vector(hipStream_t s, int ldv, long long row0, int nreal, double* x);
 

@@ -1477,6 +1477,20 @@ __global__ __launch_bounds__(256) void k_sum_partial(const double* __restrict__ 
     if (threadIdx.x == 0) npart[blockIdx.x] = s;
 }
 
+// per 512-row block: sum over the real rows of (w[r] - lambda x[r])^2 (the
+// final residual, a diagnostic: a fixed tree per block, the blocks summed on
+// the host in order)
+__global__ __launch_bounds__(256) void k_resid_partial(const double* __restrict__ w, const double* __restrict__ x,
+                                                       double lambda, int nreal, double* __restrict__ part) {
+    __shared__ double lds4[4];
+    const size_t r = (size_t(blockIdx.x) * 256 + threadIdx.x) * 2;
+    const double2 a = *reinterpret_cast<const double2*>(w + r);
+    const double2 b = *reinterpret_cast<const double2*>(x + r);
+    const double tx = r < size_t(nreal) ? a.x - lambda * b.x : 0.0, ty = r + 1 < size_t(nreal) ? a.y - lambda * b.y : 0.0;
+    const double s = block_sum256(tx * tx + ty * ty, lds4);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
 // x[r] -= (*mean_sum) * inv_n on real rows (projection off the constant vector)
 __global__ __launch_bounds__(256) void k_sub_mean(double* __restrict__ x, int nreal, const double* __restrict__ sum,
                                                   double inv_n) {
@@ -1706,6 +1720,10 @@ __global__ __launch_bounds__(256) void k_start_vector(double* __restrict__ x, in
 
 void start_vector(hipStream_t s, int ldv, long long row0, int nreal, double* x) {
     hipLaunchKernelGGL(k_start_vector, dim3((ldv + 255) / 256), dim3(256), 0, s, x, ldv, row0, nreal);
+}
+
+void resid_partial(hipStream_t s, int ldv, const double* w, const double* x, double lambda, int nreal, double* part) {
+    hipLaunchKernelGGL(k_resid_partial, dim3(ldv / UPD_ROWS), dim3(256), 0, s, w, x, lambda, nreal, part);
 }
 
 void sum_partial(hipStream_t s, int ldv, const double* x, int nreal, double* npart, int squares) {
