@@ -785,12 +785,16 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         ek::fail(EK_EINVAL, "ek_spmv_setup_pins: bad argument");
     const int64_t npins = net_ptr[nets];
     if (npins > INT32_MAX) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: too many pins");
+    ek::PhaseTimer pt("spmv_setup_pins");
+    // (both scans branch-free, so they vectorise; the error paths re-scan)
     int64_t raw_bound = 0;  // raw entries: every pin of a net of k >= 2 pins sees k - 1 others
+    bool non_monotone = false;
     for (int64_t e = 0; e < nets; ++e) {
         const int64_t k = net_ptr[e + 1] - net_ptr[e];
-        if (k < 0) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: net_ptr not monotone");
-        if (k >= 2) raw_bound += k * (k - 1);
+        non_monotone |= k < 0;
+        raw_bound += k >= 2 ? k * (k - 1) : 0;
     }
+    if (non_monotone) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: net_ptr not monotone");
     // this rank's rows: the nnz-balanced shard map, computed from the pins
     // identically on every rank (no collective)
     std::vector<int64_t> off(size_t(c->nranks) + 1, 0);
@@ -800,7 +804,7 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         if (rc != EK_OK) throw ek::Error{rc};
     }
     const int64_t row0 = off[size_t(c->rank)], nrows = off[size_t(c->rank) + 1] - row0;
-    ek::PhaseTimer pt("spmv_setup_pins");
+    pt.mark("raw bound, shard map");
     hipStream_t s = c->stream;
     auto host_fallback = [&](const char* why) {
         if (std::getenv("EK_TRACE")) std::fprintf(stderr, "[spmv_setup_pins] host build: %s\n", why);
@@ -818,13 +822,23 @@ int ek_spmv_setup_pins(ek_ctx* c, int64_t n, int64_t nets, const int64_t* net_pt
         host_fallback("EK_HOST_LAPLACIAN");
         return EK_OK;
     }
-    for (int64_t p = 0; p < npins; ++p)
-        if (pins[p] < 0 || pins[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: pin %d out of range", pins[p]);
+    {
+        int32_t lo = INT32_MAX, hi = INT32_MIN;
+        for (int64_t p = 0; p < npins; ++p) {
+            lo = std::min(lo, pins[p]);
+            hi = std::max(hi, pins[p]);
+        }
+        if (npins > 0 && (lo < 0 || int64_t(hi) >= n))
+            for (int64_t p = 0; p < npins; ++p)  // the first offender, for the message
+                if (pins[p] < 0 || pins[p] >= n) ek::fail(EK_EINVAL, "ek_spmv_setup_pins: pin %d out of range", pins[p]);
+    }
+    pt.mark("input checks");
     {
         Uploader up(c, s, (size_t(nets) + 1) * 8 + size_t(std::max<int64_t>(npins, 1)) * 4);
         up.put(c->lb_netptr, net_ptr, size_t(nets) + 1);
         up.put(c->lb_pins, pins, size_t(std::max<int64_t>(npins, 1)));
     }
+    pt.mark("pins staged");
     const size_t nr = size_t(nrows);
     ek::dev::LapBuild b;
     b.nets = nets;

@@ -109,3 +109,28 @@ def test_device_build_shard_rows(ek, ctxs, ranks):
             assert np.all(np.abs(y - y_full[row0: row0 + nrows]) <= 1e-14 * absrow + 1e-300)
     finally:
         dev_ctx.comm_init_host(1, 0, never, never)
+
+
+def test_device_build_rejects_bad_pins(ek, ctxs):
+    """ek_spmv_setup_pins validates its input before any upload: a pin outside
+    [0, n) (reported with the first offender's value) or a decreasing net_ptr
+    is EK_EINVAL, and the context then still builds a valid matrix."""
+    import ctypes
+    lib = ek._lib
+    ctx, _ = ctxs
+    dev = ctypes.c_int32(0)
+
+    def setup(n, net_ptr, pins):
+        net_ptr = np.ascontiguousarray(net_ptr, np.int64)
+        pins = np.ascontiguousarray(pins, np.int32)
+        rc = lib.ek_spmv_setup_pins(ctx._c, n, len(net_ptr) - 1, ek._p(net_ptr), ek._p(pins), ctypes.byref(dev))
+        return rc, lib.ek_last_error().decode(errors="replace")
+
+    rc, msg = setup(4, [0, 2, 4], [0, 1, 2, 7])
+    assert rc == ek.EK_EINVAL and "pin 7 out of range" in msg
+    rc, msg = setup(4, [0, 2, 4], [0, -3, 2, 9])
+    assert rc == ek.EK_EINVAL and "pin -3 out of range" in msg
+    rc, msg = setup(4, [0, 3, 2, 4], [0, 1, 2, 3])
+    assert rc == ek.EK_EINVAL and "not monotone" in msg
+    h = ek.Hypergraph.read(circuit_path("fract"))
+    assert ctx.spmv_setup_pins(h) is True
