@@ -86,7 +86,14 @@ struct ek_hgr {
     int64_t nets = 0, nodes = 0;
     ek::dvec<int64_t> net_ptr;  // nets + 1
     ek::dvec<int32_t> pins;     // 0-based
+    // sum over nets of k (k - 1), k >= 2 pins (the clique expansion's raw
+    // entries), when the reader counted it; -1: not known
+    int64_t raw_pairs = -1;
 };
+namespace ek {
+// ek_spmv_setup_pins for an ek_hgr (ctx.cpp): its pins need no range scan
+int spmv_setup_hgr(ek_ctx* c, const ek_hgr& h, int32_t* on_device);
+}  // namespace ek
 
 struct ek_csr {
     int64_t nrows = 0;

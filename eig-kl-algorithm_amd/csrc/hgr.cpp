@@ -185,7 +185,9 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
     for (int t = 0; t < T; ++t) part[size_t(t)].clear();  // (capacity kept)
     std::atomic<bool> bad{false};
     std::atomic<int64_t> bad_pin{-1};
+    std::atomic<int64_t> raw_pairs{0};
     ek::run_threads(T, [&](int t) {
+        int64_t pairs = 0;  // this thread's nets' k (k - 1), k >= 2
         int64_t net = lines[size_t(t)];
         auto& pv = part[size_t(t)];
         const char* p = cs[size_t(t)];
@@ -243,11 +245,14 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
                 if (!parse_line(ls, le, emit)) bad = true;
                 p = le;
             }
-            h->net_ptr[size_t(net) + 1] = int64_t(cnt - before);
+            const int64_t k = int64_t(cnt - before);
+            h->net_ptr[size_t(net) + 1] = k;
+            pairs += k >= 2 ? k * (k - 1) : 0;
             if (p < e) ++p;  // the newline
             ++net;
         }
         pv.resize(cnt);
+        raw_pairs += pairs;
     });
     pt.mark("parse (threads)");
     if (bad) ek::fail(EK_EINVAL, "%s: pin id overflows uint32", path);
@@ -255,6 +260,7 @@ int ek_hgr_read(const char* path, ek_hgr** out) {
         ek::fail(EK_EINVAL, "%s: pin id %lld outside [1, %lld]", path, (long long)bad_pin.load(),
                  (long long)h->nodes);
     for (int64_t i = 0; i < nets; ++i) h->net_ptr[size_t(i) + 1] += h->net_ptr[size_t(i)];
+    h->raw_pairs = raw_pairs.load();
     pt.mark("net prefix");
     h->pins.resize(size_t(h->net_ptr.back()));
     std::vector<size_t> off(size_t(T) + 1, 0);

@@ -96,7 +96,7 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
     // this rank's rows, assembled on the GPU from the pins into the SpMV's
     // coded form (the host build only as ek_spmv_setup_pins' fallback)
     cold_stamp("laplacian_start");
-    chk(ek_spmv_setup_pins(ctx, n, h.nets, h.net_ptr.data(), h.pins.data(), nullptr));
+    chk(spmv_setup_hgr(ctx, h, nullptr));
     cold_stamp("laplacian_done");
     if (t_laplacian) *t_laplacian = since(t);
     if (t_spmv_setup) *t_spmv_setup = 0.0;

@@ -13,6 +13,8 @@ int absent(const char* what) {
 }
 }  // namespace
 
+int ek::spmv_setup_hgr(ek_ctx*, const ek_hgr&, int32_t*) { return absent("ek_spmv_setup_pins"); }
+
 void ek::ctx_ranks(ek_ctx*, int* rank, int* nranks) {
     if (rank) *rank = 0;
     if (nranks) *nranks = 1;
