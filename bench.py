@@ -208,6 +208,9 @@ def reap_strays():
             p.terminate()
         except psutil.Error:
             pass
+    # the whole child tree at exit, logged even when empty (the
+    # driver's procs_at_end 1 with no stray of ours listed)
+    log(f"child tree at exit: {left if left else 'none'}")
     if left:
         log(f"processes this bench left behind (terminated): {left}")
         _, alive = psutil.wait_procs([psutil.Process(x["pid"]) for x in left if psutil.pid_exists(x["pid"])], timeout=5)
@@ -362,9 +365,10 @@ def main():
     elapsed = max_over_ranks(time.time() - t0)
     sec_per_step = elapsed / args.steps
     last, swap_log = results[-1]
-    # the SpMV's kernel timestamps come from one more step, untimed: a step
-    # with timing events runs its Lanczos chunks eagerly (the events are not
-    # graph nodes), the timed steps replay their captured graphs
+    # the SpMV's kernel timestamps come from one more step, untimed: the timed
+    # steps launch without timing events (a launch with events costs the host
+    # ~7 us more, tools/lanczos_wall.py).  Both launch eagerly: the default
+    # partial reorthogonalisation (reorth=3) captures no HIP graphs
     ev_step = step(time_spmv=True)
     barrier()
     log(f"timed: {args.steps} steps, {sec_per_step * 1e3:.2f} ms/step; last step {last['t_total']:.4f} s "
@@ -676,6 +680,12 @@ def main():
         shutil.rmtree(work, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
+    try:  # last word on descendants, after the context and the process group are gone
+        import psutil
+        kids = [(p.pid, " ".join(p.cmdline())[:120]) for p in psutil.Process().children(recursive=True)]
+        log(f"descendants at return: {kids if kids else 'none'}")
+    except Exception as e:  # noqa: BLE001 (diagnostic only)
+        log(f"descendants at return: unknown ({e})")
 
 
 if __name__ == "__main__":

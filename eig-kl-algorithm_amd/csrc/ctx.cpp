@@ -1635,6 +1635,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     const auto t0 = std::chrono::steady_clock::now();
     c->comm_ms = 0.0;
     c->n_ag = c->n_ar = 0;
+    c->fied_n = 0;  // any earlier vector is void once a solve starts; set again only on success
     const int64_t n = c->n;
     const bool deflate = o.deflate != 0;
     const int nev = deflate ? 1 : 2;
@@ -2139,8 +2140,11 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     ek::dev::gemm_vq(s, L.ldv, L.V(), mf, c->Qd.as<double>(), 1, xloc);
     // full vector on every rank; copied out through pinned staging kept by the
     // context (pageable copies of these 2 x 8n bytes cost ~0.5 ms a solve)
-    // (+ 4,096: the final step's small read-backs, below)
-    const size_t need = size_t(n) + size_t(std::max<int64_t>(c->nrows, 1)) + 4096;
+    // (+ tail: the final step's small read-backs, below: one residual partial
+    // per 512 rows, then the in-launch waits' state and the fallback count in
+    // the last 8 doubles; at least 4,096 so small graphs keep one allocation)
+    const size_t tail = std::max<size_t>(4096, (size_t(std::max(L.nub, 0)) + 8 + 63) & ~size_t(63));
+    const size_t need = size_t(n) + size_t(std::max<int64_t>(c->nrows, 1)) + tail;
     if (c->pin_doubles < need) {
         if (c->pin) HIPCHK(hipHostFree(c->pin));
         c->pin = nullptr;
@@ -2171,10 +2175,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // 1.7 MB residual vector back, summing it on the host and syncing three
     // times left the GPU idle ~0.35 ms a solve at the headline.)
     const bool fin_fast = !c->mr;
-    double* rpart = c->pin + size_t(n) + size_t(std::max<int64_t>(c->nrows, 1));  // nub <= 4,096 - 8
-    ek::dev::ProState* ps_pin = reinterpret_cast<ek::dev::ProState*>(rpart + 4096 - 8);
-    unsigned* fb_pin = reinterpret_cast<unsigned*>(rpart + 4096 - 2);
-    if (fin_fast && L.nub > 4096 - 8) ek::fail(EK_ESTATE, "Lanczos: %d residual partials", L.nub);
+    double* rpart = c->pin + size_t(n) + size_t(std::max<int64_t>(c->nrows, 1));  // nub <= tail - 8
+    ek::dev::ProState* ps_pin = reinterpret_cast<ek::dev::ProState*>(rpart + tail - 8);
+    unsigned* fb_pin = reinterpret_cast<unsigned*>(rpart + tail - 2);
+    static_assert(sizeof(ek::dev::ProState) <= 6 * sizeof(double), "ProState overlaps the fallback count");
     if (fin_fast) {
         if (!c->fin_ev) HIPCHK(hipEventCreateWithFlags(&c->fin_ev, hipEventDisableTiming));
         HIPCHK(hipEventRecord(c->fin_ev, s));
@@ -2199,16 +2203,17 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             if (std::fabs(v[i]) > std::fabs(v[imax])) imax = i;
         const double sgn = v[imax] < 0 ? -inv : inv;
         c->fied.ensure(size_t(n) * 8);
+        c->fied_n = 0;  // set only once the solve is known good (a failed solve leaves no vector)
         ek::dev::fiedler_scale(s, xc, sgn, int(n), c->fied.as<double>());
         HIPCHK(hipGetLastError());
-        c->fied_n = n;
         HIPCHK(hipStreamSynchronize(s));
-        double rs = 0.0;
-        for (int b = 0; b < L.nub; ++b) rs += rpart[b];
-        const double r2 = rs * inv * inv;
         if (L.proi && ps_pin->timeouts)
             ek::fail(EK_EHIP, "Lanczos: %d in-launch wait(s) of the partially reorthogonalised step gave up "
                               "(EK_PRO_INLAUNCH=0 runs the step without them)", ps_pin->timeouts);
+        c->fied_n = n;
+        double rs = 0.0;
+        for (int b = 0; b < L.nub; ++b) rs += rpart[b];
+        const double r2 = rs * inv * inv;
         if (lambda_out) *lambda_out = lambda;
         if (v_out)
             for (int64_t i = 0; i < n; ++i) v_out[i] = v[i] * sgn;

@@ -261,3 +261,24 @@ def test_device_fiedler_split_equals_host_split(ek, ctx, case):
     swap_fields_equal(log_d, log_h)
     for k in ("iterations", "best_iter", "initial_cut", "best_cut", "final_cut", "net_cut_best"):
         assert res_d[k] == res_h[k], k
+
+
+def test_single_context_solve_above_fast_finish_tail(ek):
+    """the single-context finish reads one residual partial
+    per 512 rows back through the context's pinned tail, which was fixed at
+    4,096 doubles, so any graph above ~2.09M rows failed with EK_ESTATE after
+    the whole solve.  The tail is now sized from the partial count: a 10.6x
+    synthetic (> 4,088 partials) must solve on ONE context and return a
+    converged, finite pair (and the context must hold the vector for the
+    device split)."""
+    h = ek.Hypergraph.generate(10.6, 10)
+    assert h.nodes > 4096 * 512, h.nodes
+    c = ek.Context(0)
+    try:
+        c.spmv_setup_pins(h)
+        lam, v, st = c.lanczos_fiedler()
+        assert st["converged"] and st["residual"] < 1e-8, st
+        assert np.all(np.isfinite(v)) and abs(np.linalg.norm(v) - 1) < 1e-10
+        assert abs(lam) < 1e-8  # disconnected synthetic: lambda1 = 0
+    finally:
+        c.close()
