@@ -90,6 +90,10 @@ def _sig(name, res, *args):
 
 _sig("ek_last_error", ctypes.c_char_p)
 _sig("ek_version", ctypes.c_char_p)
+_sig("ek_abi_version", ctypes.c_int)
+ABI_VERSION = 4  # eigkl.h EIGKL_ABI_VERSION: the ctypes struct mirrors below follow that layout
+if _lib.ek_abi_version() != ABI_VERSION:
+    raise ImportError(f"libeigkl_hip ABI {_lib.ek_abi_version()} != the {ABI_VERSION} these bindings mirror: rebuild")
 _sig("ek_hgr_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_P))
 _sig("ek_hgr_generate", ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.POINTER(_P))
 _sig("ek_hgr_from_pins", ctypes.c_int, _I64, _I64, _P, _P, ctypes.POINTER(_P))

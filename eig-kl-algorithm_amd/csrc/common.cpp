@@ -171,4 +171,5 @@ void pool_run(int T, void (*fn)(void*, int), void* ctx) {
 extern "C" {
 const char* ek_last_error(void) { return ek::g_last_error.c_str(); }
 const char* ek_version(void) { return "eigkl-mi355x 0.1 (gfx950)"; }
+int ek_abi_version(void) { return EIGKL_ABI_VERSION; }
 }

@@ -1255,6 +1255,7 @@ struct Lanczos {
         static const bool unfused = std::getenv("EK_LANCZOS_UNFUSED") != nullptr;
         if (reorth == 1) {
             if (!c->mr && !unfused) return graphs && !time_spmv ? factorize_graph(k, kend) : factorize_fused(k, kend);
+            if (pro) return factorize_mr_pro(k, kend);
             return factorize_mr(k, kend);
         }
         double* fn2 = c->fn2.as<double>();
@@ -1302,36 +1303,46 @@ struct Lanczos {
     // overlap (sharded): the owned-slot SpMV runs on the context stream while
     // the all-gather runs on gstream; the halo SpMV then starts from its sums
     bool overlap = false;
+    // The exchange of one sharded step: this rank's ||f||^2 partial (from the
+    // update's npart) into its slot, f to every rank, and the SpMV's
+    // prologue operands in fin (the ranks' partials, in rank order; with the
+    // overlap, the owned slot's rows summed while the all-gather runs).
+    // Returns the x the SpMV reads.
+    const double* exchange_f(int i, ek::dev::StepFin& fin) {
+        double* f = c->f.as<double>();
+        ek::dev::finalize_step(s, c->npart.as<double>(), nub, f + ldv, nullptr, nullptr, -1, nullptr, nullptr);
+        const double* x = f;
+        if (c->mr && overlap) {
+            // f (with this rank's ||f||^2 partial at f[ldv]) is final: the
+            // all-gather goes out on gstream, and the owned slot's rows are
+            // summed meanwhile (unscaled: ||f|| comes with the all-gather)
+            HIPCHK(hipEventRecord(c->ag_ev[0], s));
+            HIPCHK(hipStreamWaitEvent(c->gstream, c->ag_ev[0], 0));
+            ek::dev::spmv(s, own_mat(c), f, c->yown.as<double>(), nullptr, nullptr, nullptr, nullptr);
+            allgather(c, f, size_t(c->slot), c->xfull.as<double>(), c->gstream);
+            HIPCHK(hipEventRecord(c->ag_ev[1], c->gstream));
+            HIPCHK(hipStreamWaitEvent(s, c->ag_ev[1], 0));
+            x = c->xfull.as<double>();
+            fin.own_lo = int(c->rank * c->slot);
+            fin.own_hi = int(c->rank * c->slot + c->nrows);
+            fin.ybase = c->yown.as<double>();
+        } else if (c->mr) {
+            allgather(c, f, size_t(c->slot), c->xfull.as<double>());
+            x = c->xfull.as<double>();
+        }
+        fin.npart = x + ldv;
+        fin.nb = c->nranks;
+        fin.nstride = int(c->slot);
+        fin.fn2_out = c->fn2.as<double>() + i;
+        return x;
+    }
+
     void factorize_mr(int k, int kend) {
         double* fn2 = c->fn2.as<double>();
         double* f = c->f.as<double>();
-        const bool sharded = c->mr;
         for (int i = k; i < kend; ++i) {
-            ek::dev::finalize_step(s, c->npart.as<double>(), nub, f + ldv, nullptr, nullptr, -1, nullptr, nullptr);
-            const double* x = f;
             ek::dev::StepFin fin;
-            if (sharded && overlap) {
-                // f (with this rank's ||f||^2 partial at f[ldv]) is final: the
-                // all-gather goes out on gstream, and the owned slot's rows are
-                // summed meanwhile (unscaled: ||f|| comes with the all-gather)
-                HIPCHK(hipEventRecord(c->ag_ev[0], s));
-                HIPCHK(hipStreamWaitEvent(c->gstream, c->ag_ev[0], 0));
-                ek::dev::spmv(s, own_mat(c), f, c->yown.as<double>(), nullptr, nullptr, nullptr, nullptr);
-                allgather(c, f, size_t(c->slot), c->xfull.as<double>(), c->gstream);
-                HIPCHK(hipEventRecord(c->ag_ev[1], c->gstream));
-                HIPCHK(hipStreamWaitEvent(s, c->ag_ev[1], 0));
-                x = c->xfull.as<double>();
-                fin.own_lo = int(c->rank * c->slot);
-                fin.own_hi = int(c->rank * c->slot + c->nrows);
-                fin.ybase = c->yown.as<double>();
-            } else if (sharded) {
-                allgather(c, f, size_t(c->slot), c->xfull.as<double>());
-                x = c->xfull.as<double>();
-            }
-            fin.npart = x + ldv;
-            fin.nb = c->nranks;
-            fin.nstride = int(c->slot);
-            fin.fn2_out = fn2 + i;
+            const double* x = exchange_f(i, fin);
             const bool timed = spmv_timed_step(i);
             ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), nullptr, f, col(i), nullptr, &fin,
                           timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
@@ -1348,6 +1359,78 @@ struct Lanczos {
                                c->cflag.as<double>(), mr_cancel);
         }
         if (kend == m) reduce_scalar(fn2 + m);  // the cycle's last residual norm
+        HIPCHK(hipGetLastError());
+    }
+
+    // The sharded step under partial reorthogonalisation (reorth 3; VERDICT
+    // r4 next-3).  The single-context PRO step needs alpha_i and ||w||^2
+    // before it decides, and the decision before it projects, so the step has
+    // two reductions:
+    //  1. exchange_f: the all-gather of f (every rank's ||f||^2 partial with it);
+    //  2. SpMV: w = L f/||f||, v_i, and per-block partials of alpha and ||w||^2;
+    //  3. this rank's (alpha, ||w||^2) -> ONE all-reduce of 2 doubles;
+    //  4. k_pro on the global sums: Simon's omega recurrence runs replicated on
+    //     every rank (the same alpha, T and state everywhere: the same decision);
+    //  5. the projection of f' = w - alpha v_i - beta v_{i-1} (f' formed per row
+    //     and stored to f; on a skipped step only that, and ||f'||^2);
+    //  6. ONE all-reduce of the column sums h (+ ||f'||^2): issued on every step,
+    //     since the host cannot see the device's decision without waiting for
+    //     it; a skipped step's kernels have no basis pass and its h entries
+    //     the finalize reads are exact zeros;
+    //  7. the update f = f' - V h (a skipped step: nothing; ||f||^2 = ||f'||^2
+    //     reaches the next SpMV as one global value).
+    // A skipped step is the all-gather, the SpMV, two small all-reduces and no
+    // pass over V; a projecting one adds the two basis passes (the sharded
+    // reorth-1 step always made them, through k_gemvt3 / k_update_mr).  f' is
+    // projected directly (not by linearity as in factorize_mr), so there is no
+    // cancellation to repair.  H's alpha[i] / offd[i] are written by step i+1's
+    // SpMV prologue (the single-context lag) or the cycle's closing finalize.
+    void factorize_mr_pro(int k, int kend) {
+        double* fn2 = c->fn2.as<double>();
+        double* f = c->f.as<double>();
+        double* a3 = c->scal.as<double>() + 2;
+        double* fast = c->scal.as<double>() + 4;  // ||f||^2 of a skipped step for the next SpMV (NaN: the partials)
+        double* aw = c->scal.as<double>() + 6;    // (alpha, ||w||^2): this rank's, then all-reduced
+        const double* bov = c->bov.as<double>();
+        double* h2 = c->h2.as<double>();
+        for (int i = k; i < kend; ++i) {
+            ek::dev::StepFin fin;
+            const double* x = exchange_f(i, fin);
+            fin.wpart = c->wpart.as<double>();
+            if (i > seg0) {  // step i-1's finalize in this SpMV's prologue; ||f||^2 from its update when not NaN
+                fin.fast = fast;
+                fin.h2 = h2;
+                fin.step = i - 1;
+                fin.alpha = c->alpha.as<double>();
+                fin.offd = c->offd.as<double>();
+                fin.a3 = a3;
+                fin.fn2_i = fn2 + i - 1;
+                fin.bov_i = bov + i - 1;
+            }
+            const bool timed = spmv_timed_step(i);
+            ek::dev::spmv(s, spmv_mat(c), x, c->w.as<double>(), nullptr, f, col(i), c->apart.as<double>(), &fin,
+                          timed ? ev[size_t(2 * (i - seg0))] : nullptr, timed ? ev[size_t(2 * (i - seg0) + 1)] : nullptr);
+            ++matvecs;
+            ek::dev::sum_pair(s, c->apart.as<double>(), c->wpart.as<double>(), c->nrb_spmv, aw);
+            allreduce(c, aw, 2);
+            ek::dev::pro_step(s, aw, aw + 1, 1, a3, fn2 + i, bov + i, c->alpha.as<double>(), c->offd.as<double>(),
+                              c->omega.as<double>(), c->prost.as<ek::dev::ProState>(), c->pflags.as<int>(), i, seg0, m,
+                              pro_thresh, pro_eps1);
+            const int* flag = c->pflags.as<int>() + i;
+            const int nc = i + 1, tot = nc + has_u0;
+            ek::dev::gemvt_tt(s, ldv, nrb, V(), nc, has_u0, u0val, nreal, c->w.as<double>(), a3, col(i),
+                              i > 0 ? col(i - 1) : nullptr, fn2 + i, bov + i, f, c->part.as<double>(), nullptr, nullptr,
+                              0, nullptr, nullptr, nt, flag, nullptr, nullptr);
+            ek::dev::reduce_cols(s, c->part.as<double>(), nrb, tot + 1, h2);  // (+ ||f'||^2)
+            allreduce(c, h2, size_t(tot + 1));
+            ek::dev::update(s, ldv, V(), nc, has_u0, u0val, nreal, h2, f, f, c->npart.as<double>(), nullptr, nullptr,
+                            fast, nt, flag);
+        }
+        if (kend == m) {  // the cycle's last step (always projected): its finalize and residual norm
+            ek::dev::finalize_step(s, c->npart.as<double>(), nub, fn2 + m, nullptr, h2, m - 1, c->alpha.as<double>(),
+                                   c->offd.as<double>(), a3, fn2 + m - 1, bov + m - 1);
+            allreduce(c, fn2 + m, 1);
+        }
         HIPCHK(hipGetLastError());
     }
 
@@ -1663,11 +1746,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.time_spmv = o.time_spmv != 0;
     L.reorth = o.reorth == 2 ? 2 : 1;
     hipStream_t s = c->stream;
-    // reorth 3: partial reorthogonalisation on the single-context step (the
-    // sharded and CGS2 steps always project).  EK_REORTH=1|3 overrides (A/B).
+    // reorth 3: partial reorthogonalisation, on the single-context step and
+    // on the sharded one (factorize_mr_pro; the CGS2 step always projects).
+    // EK_REORTH=1|3 overrides (A/B).
     int reorth_mode = o.reorth;
     if (const char* e = std::getenv("EK_REORTH"); e && e[0]) reorth_mode = std::atoi(e);
-    L.pro = reorth_mode == 3 && !c->mr && std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
+    L.pro = reorth_mode == 3 && L.reorth == 1 && std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
     // threshold 1e-10, not Simon's sqrt(eps): across implicit restarts the
     // kept Ritz block carries the basis's loss of orthogonality into the next
     // cycle, and the dropped projection coefficients (O(threshold) beta) stay
@@ -1677,7 +1761,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // 44 % of the steps projected; the headline LCC 32 %, residual unchanged
     L.pro_thresh = o.reorth_thresh > 0 ? o.reorth_thresh : 1e-10;
     L.pro_eps1 = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
-    if (const char* e = std::getenv("EK_PRO_INLAUNCH"); L.pro) L.proi = !(e && e[0] == '0');
+    // (the in-launch decision and merged update: single context only; the
+    // sharded step all-reduces alpha and ||w||^2 before its k_pro launch)
+    if (const char* e = std::getenv("EK_PRO_INLAUNCH"); L.pro && !c->mr) L.proi = !(e && e[0] == '0');
     if (const char* e = std::getenv("EK_PRO_MERGE"); L.proi) L.pro_merge = !(e && e[0] == '0');
     // column groups walked per projection workgroup: about 850 projection
     // workgroups, at least 3 per row block (the 1.15x LCC, 207 row blocks:
@@ -1855,7 +1941,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     };
     // the sharded step's re-projection of a cancelled f' (Lanczos::repair);
     // EK_LANCZOS_UNFUSED runs that step (and its flags) on a single context too
-    const bool mr_step = (c->mr || std::getenv("EK_LANCZOS_UNFUSED") != nullptr) && L.reorth == 1;
+    const bool mr_step = (c->mr || std::getenv("EK_LANCZOS_UNFUSED") != nullptr) && L.reorth == 1 && !L.pro;
     // the owned-slot / halo split of the sharded SpMV (EK_MR_OVERLAP=0: one
     // SpMV after the all-gather, the round-3 step; A/B and tests)
     {

@@ -416,6 +416,8 @@ struct ProState {
     int timeouts;   // in-launch waits that gave up (PROI; the host fails the solve on any)
     int pad;
 };
+// out[0..1] = the sums of a[0:n) and b[0:n) (one workgroup; pro_decide's order)
+void sum_pair(hipStream_t s, const double* a, const double* b, int n, double* out);
 void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,
               const double* bov_i, const double* alpha, const double* offd, double* omega, ProState* st, int* flags,
               int i, int seg0, int m, double thresh, double eps1);

@@ -1323,6 +1323,27 @@ __global__ __launch_bounds__(256) void k_finalize_step(const double* __restrict_
     }
 }
 
+// out[0] = sum(a[0:n)), out[1] = sum(b[0:n)) in pro_decide's order (the
+// sharded partially reorthogonalised step: this rank's alpha and ||w||^2
+// from its SpMV partials, all-reduced before k_pro reads them as one partial)
+__global__ __launch_bounds__(256) void k_sum_pair(const double* __restrict__ a, const double* __restrict__ b, int n,
+                                                  double* __restrict__ out) {
+    __shared__ double la[4], lb[4];
+    double sa, sb;
+    strided_sum256x2(a, b, n, sa, sb);
+    sa = wave_sum(sa);
+    sb = wave_sum(sb);
+    if ((threadIdx.x & 63) == 0) {
+        la[threadIdx.x >> 6] = sa;
+        lb[threadIdx.x >> 6] = sb;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] = (la[0] + la[1]) + (la[2] + la[3]);
+        out[1] = (lb[0] + lb[1]) + (lb[2] + lb[3]);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_pro(const double* __restrict__ apart, const double* __restrict__ wpart,
                                              int nparts, double* __restrict__ a3, const double* __restrict__ fn2_i,
                                              const double* __restrict__ bov_i, const double* __restrict__ alpha,
@@ -1630,6 +1651,10 @@ void pro_step(hipStream_t s, const double* apart, const double* wpart, int npart
               int i, int seg0, int m, double thresh, double eps1) {
     hipLaunchKernelGGL(k_pro, dim3(1), dim3(256), 0, s, apart, wpart, nparts, a3, fn2_i, bov_i, alpha, offd, omega, st,
                        flags, i, seg0, m, thresh, eps1);
+}
+
+void sum_pair(hipStream_t s, const double* a, const double* b, int n, double* out) {
+    hipLaunchKernelGGL(k_sum_pair, dim3(1), dim3(256), 0, s, a, b, n, out);
 }
 
 void three_term(hipStream_t s, int ldv, const double* apart, int nparts, double* alpha_io, const double* w,

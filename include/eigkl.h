@@ -38,6 +38,13 @@ enum ek_status {
 
 const char* ek_last_error(void);
 const char* ek_version(void);
+/* The struct layouts of this header (ek_lanczos_opts / _stats, ek_solve_opts,
+ * ek_swap ...) carry no size field; a binding checks ek_abi_version() ==
+ * EIGKL_ABI_VERSION before passing any of them.  Bumped whenever a public
+ * struct changes layout (4: reorth_thresh, the stats' projected_steps /
+ * reprojected / ortho_max, and reorth 3 as the default). */
+#define EIGKL_ABI_VERSION 4
+int ek_abi_version(void);
 
 /* ------------------------------------------------------------------ */
 /* Hypergraph ingest (host, no GPU)                                     */
@@ -206,10 +213,13 @@ typedef struct {
                            recurrence, and the full classical Gram-Schmidt pass of 1
                            only on the steps Simon's omega recurrence asks for (loss of
                            orthogonality estimate > reorth_thresh), the step after each,
-                           every cycle's first and last step (single context; sharded
-                           steps always project); 1: that pass on every step
-                           (Spectra's full reorthogonalisation); 2: CGS2 (twice) from
-                           the matvec; 0: as 1 */
+                           every cycle's first and last step (single context and
+                           sharded alike; the sharded step all-reduces alpha and
+                           ||w||^2 first).  CHANGED DEFAULT (EIGKL_ABI_VERSION 4): rounds 1-3
+                           defaulted to 1.  1: that pass on every step (Spectra's
+                           full reorthogonalisation, the reference's algorithm;
+                           `--spectra` / `--reorth full` on the CLI); 2: CGS2 (twice)
+                           from the matvec; 0: as 1 */
     int32_t check_every; /* after the first restart cycle, test Spectra's convergence
                             criterion on the projected matrix every this many steps
                             (and stop there) instead of at cycle ends only; 0: cycle

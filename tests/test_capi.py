@@ -59,6 +59,12 @@ def test_library_carries_gfx950_code_only():
 
 def test_version(ek):
     assert ek.version()
+    # the structs carry no size field; the ABI number the header
+    # declares is what the library reports and what the ctypes mirror follows
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "eigkl.h")).read()
+    declared = int(re.search(r"#define EIGKL_ABI_VERSION (\d+)", hdr).group(1))
+    assert ek._lib.ek_abi_version() == declared == ek.ABI_VERSION
 
 
 def test_gpu_entry_fails_cleanly_without_device(ek):
