@@ -130,6 +130,7 @@ _sig("ek_spmv_host", ctypes.c_int, _P, _P, _P)
 _sig("ek_spmv_bytes", _I64, _P)
 _sig("ek_spmv_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("ek_spmv_format", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64))
+_sig("ek_spmv_exchange", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("ek_spmv_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
 _sig("ek_lanczos_fiedler", ctypes.c_int, _P, ctypes.POINTER(LanczosOpts), ctypes.POINTER(ctypes.c_double), _P,
@@ -447,6 +448,12 @@ class Context:
         pk, b = ctypes.c_int32(0), _I64(0)
         _chk(_lib.ek_spmv_format(self._c, ctypes.byref(pk), ctypes.byref(b)), "ek_spmv_format")
         return bool(pk.value), int(b.value) + (16 * self.spmv_dims()[2] if fused else 0)
+
+    def spmv_exchange(self):
+        """(halo, doubles received, doubles sent) per sharded Lanczos step (ek_spmv_exchange)."""
+        hl, rv, sd = ctypes.c_int32(0), _I64(0), _I64(0)
+        _chk(_lib.ek_spmv_exchange(self._c, ctypes.byref(hl), ctypes.byref(rv), ctypes.byref(sd)), "ek_spmv_exchange")
+        return bool(hl.value), int(rv.value), int(sd.value)
 
     def spmv_bench(self, iters=200, fused=True):
         """Average microseconds per back-to-back SpMV launch on resident buffers."""

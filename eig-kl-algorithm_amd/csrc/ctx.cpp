@@ -128,6 +128,22 @@ struct ek_ctx {
     int64_t slot = 0;
     DBuf off_d, xexp;
     DBuf spx;  // ek_spmv's x in the all-gather layout (sharded), sized when the shard map is set
+    // The halo exchange of the sharded step (halo_build): instead of every
+    // rank's whole slot, each rank receives only the rows of f its columns
+    // read, into a compact x: block q (ranks in order) holds the rows of rank
+    // q this rank reads, ascending (its own block: all its rows), then q's
+    // ||f||^2 partial.  The columns are remapped monotonically to it, so rows
+    // stay sorted and every product is summed in the same order as over the
+    // slot layout: the same bits.  Used where it moves fewer bytes than the
+    // all-gather (EK_MR_HALO=0/1 forces either).
+    bool halo = false;
+    std::vector<int64_t> hx_base;             // nranks + 1: block q at [hx_base[q], hx_base[q+1]); last = partial
+    std::vector<int64_t> hx_rcnt;             // rows received from q (own: nrows)
+    std::vector<int64_t> hx_scnt, hx_soff;    // rows sent to q, and that message's offset in hx_sbuf (+1: the partial)
+    std::vector<int64_t> hx_src;              // host-staged: q's message to this rank inside q's (padded) sbuf
+    std::vector<int32_t> hx_gidx_h;           // X[t]'s global row (-1: a partial slot)
+    int64_t hx_nsend = 0, hx_smax = 0;
+    DBuf hx_sidx, hx_sbuf, hx_X, hx_gidx, hx_gbuf;
     // the owned-slot part of a sharded rank's rows (plain CSR, local column
     // ids), summed while the all-gather of the other slots runs on `gstream`
     DBuf own_rowptr, own_col, own_val, own_rb, yown;
@@ -500,6 +516,7 @@ void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
         mx = std::max(mx, off[size_t(r) + 1] - off[size_t(r)]);
     }
     c->shard_off = off;
+    c->halo = false;
     c->row0 = off[size_t(c->rank)];
     c->nrows = off[size_t(c->rank) + 1] - c->row0;
     c->nloc = c->mr ? mx : n;
@@ -511,8 +528,176 @@ void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
     if (c->mr) c->spx.ensure(size_t(c->slot * c->nranks) * 8);
 }
 
-// The column space the SpMV reads: global ids, or the padded all-gather layout
-int64_t x_extent(const ek_ctx* c) { return c->mr ? c->slot * c->nranks : c->n; }
+// The column space the SpMV reads: global ids, the padded all-gather layout,
+// or the compact halo layout
+int64_t x_extent(const ek_ctx* c) { return c->halo ? c->hx_base.back() : c->mr ? c->slot * c->nranks : c->n; }
+
+// The halo layout from this rank's columns in the slot layout (col, host, nnz
+// entries; remapped in place when the halo exchange is taken).  One
+// all-gather of the request counts (every rank then takes the same decision)
+// and one of the request lists: setup only.
+bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
+    c->halo = false;
+    if (!c->mr || c->nranks > ek::dev::MAX_HALO_RANKS) return false;
+    const char* env = std::getenv("EK_MR_HALO");
+    if (env && env[0] == '0') return false;
+    const int R = c->nranks, me = c->rank;
+    const int64_t S = c->slot;
+    const auto& off = c->shard_off;
+    // which rows of each other rank this rank's columns read
+    std::vector<std::vector<int32_t>> pos(static_cast<size_t>(R));
+    for (int q = 0; q < R; ++q)
+        if (q != me) pos[size_t(q)].assign(size_t(off[size_t(q) + 1] - off[size_t(q)]), -1);
+    for (int64_t p = 0; p < nnz; ++p) {
+        const int q = int(col[p] / S);
+        if (q != me) pos[size_t(q)][size_t(col[p] - q * S)] = 0;
+    }
+    std::vector<std::vector<int32_t>> req(static_cast<size_t>(R));
+    for (int q = 0; q < R; ++q) {
+        auto& pq = pos[size_t(q)];
+        for (size_t l = 0; l < pq.size(); ++l)
+            if (pq[l] == 0) {
+                pq[l] = int32_t(req[size_t(q)].size());
+                req[size_t(q)].push_back(int32_t(l));
+            }
+    }
+    // C[r * R + q] = rows rank r reads from rank q
+    c->scal.ensure(64);
+    DBuf cnt_d, all_d;
+    cnt_d.ensure(size_t(R) * 8);
+    all_d.ensure(size_t(R) * size_t(R) * 8);
+    std::vector<double> mine(static_cast<size_t>(R), 0.0), C(size_t(R) * size_t(R));
+    for (int q = 0; q < R; ++q) mine[size_t(q)] = double(req[size_t(q)].size());
+    HIPCHK(hipMemcpyAsync(cnt_d.p, mine.data(), size_t(R) * 8, hipMemcpyHostToDevice, c->stream));
+    allgather(c, cnt_d.as<double>(), size_t(R), all_d.as<double>());
+    HIPCHK(hipMemcpyAsync(C.data(), all_d.p, C.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    auto Cat = [&](int r, int q) { return int64_t(C[size_t(r) * size_t(R) + size_t(q)]); };
+    int64_t tot_halo = 0, lmax = 0;
+    for (int r = 0; r < R; ++r) {
+        int64_t lr = 0;
+        for (int q = 0; q < R; ++q)
+            if (q != r) {
+                tot_halo += Cat(r, q) + 1;
+                lr += Cat(r, q);
+            }
+        lmax = std::max(lmax, lr);
+    }
+    const int64_t full = int64_t(R) * int64_t(R - 1) * S;
+    // (one forced rank: nothing to exchange either way; the slot layout)
+    const bool use = env && env[0] ? env[0] != '0' : R > 1 && double(tot_halo) <= 0.75 * double(full);
+    if (!use) return false;
+    // the request lists, padded to the longest: rank r's request from this
+    // rank starts at sum_{q < me, q != r} C[r][q] of r's list
+    std::vector<double> lst(size_t(std::max<int64_t>(lmax, 1)), 0.0), lall(size_t(std::max<int64_t>(lmax, 1)) * R);
+    {
+        size_t o = 0;
+        for (int q = 0; q < R; ++q)
+            for (int32_t l : req[size_t(q)]) lst[o++] = double(l);
+        DBuf ld, la;
+        ld.ensure(lst.size() * 8);
+        la.ensure(lall.size() * 8);
+        HIPCHK(hipMemcpyAsync(ld.p, lst.data(), lst.size() * 8, hipMemcpyHostToDevice, c->stream));
+        allgather(c, ld.as<double>(), lst.size(), la.as<double>());
+        HIPCHK(hipMemcpyAsync(lall.data(), la.p, lall.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    const int32_t ldv = int32_t(S - 64);  // f[ldv]: the rank's ||f||^2 partial (the Lanczos vectors' ld)
+    std::vector<int32_t> sidx;
+    c->hx_scnt.assign(size_t(R), 0);
+    c->hx_soff.assign(size_t(R), 0);
+    for (int r = 0; r < R; ++r) {
+        if (r == me) continue;
+        int64_t o = 0;
+        for (int q = 0; q < me; ++q)
+            if (q != r) o += Cat(r, q);
+        c->hx_soff[size_t(r)] = int64_t(sidx.size());
+        c->hx_scnt[size_t(r)] = Cat(r, me);
+        for (int64_t k = 0; k < Cat(r, me); ++k) sidx.push_back(int32_t(lall[size_t(r) * size_t(lst.size()) + size_t(o + k)]));
+        sidx.push_back(ldv);
+    }
+    c->hx_nsend = int64_t(sidx.size());
+    c->hx_rcnt.assign(size_t(R), 0);
+    c->hx_base.assign(size_t(R) + 1, 0);
+    for (int q = 0; q < R; ++q) {
+        c->hx_rcnt[size_t(q)] = q == me ? c->nrows : Cat(me, q);
+        c->hx_base[size_t(q) + 1] = c->hx_base[size_t(q)] + c->hx_rcnt[size_t(q)] + 1;
+    }
+    // host-staged exchange: q's sbuf lists its messages to r = 0, 1, ... (r != q)
+    c->hx_src.assign(size_t(R), 0);
+    c->hx_smax = 1;
+    for (int q = 0; q < R; ++q) {
+        int64_t o = 0;
+        for (int r = 0; r < R; ++r) {
+            if (r == q) continue;
+            if (r == me) c->hx_src[size_t(q)] = o;
+            o += Cat(r, q) + 1;
+        }
+        c->hx_smax = std::max(c->hx_smax, o);
+    }
+    // the columns, remapped (monotone: rows stay sorted)
+    const int64_t base_me = c->hx_base[size_t(me)];
+    for (int64_t p = 0; p < nnz; ++p) {
+        const int q = int(col[p] / S);
+        const int64_t l = col[p] - q * S;
+        col[p] = int32_t(q == me ? base_me + l : c->hx_base[size_t(q)] + pos[size_t(q)][size_t(l)]);
+    }
+    // X's global rows (ek_spmv with a global x)
+    c->hx_gidx_h.assign(size_t(c->hx_base.back()), -1);
+    for (int q = 0; q < R; ++q) {
+        const int64_t b = c->hx_base[size_t(q)];
+        if (q == me)
+            for (int64_t k = 0; k < c->nrows; ++k) c->hx_gidx_h[size_t(b + k)] = int32_t(c->row0 + k);
+        else
+            for (size_t k = 0; k < req[size_t(q)].size(); ++k)
+                c->hx_gidx_h[size_t(b) + k] = int32_t(off[size_t(q)] + req[size_t(q)][k]);
+    }
+    if (sidx.empty()) sidx.push_back(0);  // (one forced rank: no messages; a valid upload)
+    upload(c->hx_sidx, sidx.data(), sidx.size(), c->stream);
+    upload(c->hx_gidx, c->hx_gidx_h.data(), c->hx_gidx_h.size(), c->stream);
+    c->hx_sbuf.ensure(size_t(std::max(c->hx_smax, c->hx_nsend)) * 8);
+    c->hx_X.ensure(size_t(c->hx_base.back()) * 8);
+    if (!c->comm) c->hx_gbuf.ensure(size_t(c->hx_smax) * size_t(R) * 8);
+    HIPCHK(hipMemsetAsync(c->hx_sbuf.p, 0, c->hx_sbuf.bytes, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->halo = true;
+    return true;
+}
+
+// One halo exchange of src (this rank's rows, its ||f||^2 partial at
+// src[ldv]) into the compact x (c->hx_X), on stream st: the pack, then RCCL
+// point-to-point messages to and from every peer in one group, or, staged
+// through the host, an all-gather of every rank's (padded) messages of which
+// this rank keeps its pieces.  Counted as the step's one all-gather.
+void halo_exchange(ek_ctx* c, const double* src, hipStream_t st) {
+    const int R = c->nranks, me = c->rank;
+    double* X = c->hx_X.as<double>();
+    double* sb = c->hx_sbuf.as<double>();
+    ek::dev::halo_pack(st, src, int(c->slot - 64), c->hx_sidx.as<int>(), c->hx_nsend, sb, X, c->hx_base[size_t(me)],
+                       c->nrows);
+    if (c->comm) {
+        ++c->n_ag;
+        if (R == 1) return;
+        NCCLCHK(ncclGroupStart());
+        for (int q = 0; q < R; ++q) {
+            if (q == me) continue;
+            NCCLCHK(ncclSend(sb + c->hx_soff[size_t(q)], size_t(c->hx_scnt[size_t(q)] + 1), ncclDouble, q, c->comm, st));
+            NCCLCHK(ncclRecv(X + c->hx_base[size_t(q)], size_t(c->hx_rcnt[size_t(q)] + 1), ncclDouble, q, c->comm, st));
+        }
+        NCCLCHK(ncclGroupEnd());
+        return;
+    }
+    if (R == 1) {
+        ++c->n_ag;
+        return;
+    }
+    double* g = c->hx_gbuf.as<double>();
+    allgather(c, sb, size_t(c->hx_smax), g, st);
+    for (int q = 0; q < R; ++q)
+        if (q != me)
+            HIPCHK(hipMemcpyAsync(X + c->hx_base[size_t(q)], g + size_t(q) * size_t(c->hx_smax) + c->hx_src[size_t(q)],
+                                  size_t(c->hx_rcnt[size_t(q)] + 1) * 8, hipMemcpyDeviceToDevice, st));
+}
 
 // The column-panel form when x outgrows an XCD's L2 (EK_SPMV_PANEL=0/1 forces
 // it off/on; default: x > 8 MB, the 10x synthetic.  At 2x (3.2 MB) the two
@@ -663,6 +848,7 @@ void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, cons
         remap_cols_host(c, col, nnz, colx);
         col = colx.data();
         own_build_host(c, rowptr, col, val);
+        halo_build(c, colx.data(), nnz);  // (the owned rows were taken in the slot layout)
     }
     c->n = n;
     c->nnz = nnz;
@@ -924,6 +1110,14 @@ static int spmv_setup_pins_impl(ek_ctx* c, int64_t n, int64_t nets, const int64_
         upload(c->off_d, offll.data(), offll.size(), s);
         ek::dev::remap_cols(s, nnz, c->col.as<int>(), c->off_d.as<long long>(), c->nranks, c->slot);
         own_build_dev(c, s, tiles);
+        // the halo layout is worked out on the host from this rank's columns
+        std::vector<int32_t> ch(size_t(std::max<int64_t>(nnz, 1)));
+        if (nnz) HIPCHK(hipMemcpyAsync(ch.data(), c->col.p, size_t(nnz) * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (halo_build(c, ch.data(), nnz) && nnz)
+            HIPCHK(hipMemcpyAsync(c->col.p, ch.data(), size_t(nnz) * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        pt.mark("halo layout");
     }
     // the same greedy row blocks as the host path (ek_spmv_setup)
     int colbits = 1;
@@ -1011,7 +1205,11 @@ int ek_spmv(ek_ctx* c, const double* x, double* y, void* stream) {
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv before ek_spmv_setup");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     const double* xs = x;
-    if (c->mr) {
+    if (c->halo) {  // the compact halo layout, gathered from the global x
+        if (c->spx.bytes < size_t(x_extent(c)) * 8) ek::fail(EK_ESTATE, "ek_spmv: shard layout not set up");
+        ek::dev::gather_idx(s, x, c->hx_gidx.as<int>(), (long long)x_extent(c), c->spx.as<double>());
+        xs = c->spx.as<double>();
+    } else if (c->mr) {
         if (c->spx.bytes < size_t(x_extent(c)) * 8) ek::fail(EK_ESTATE, "ek_spmv: shard layout not set up");
         for (int r = 0; r < c->nranks; ++r) {
             const int64_t a = c->shard_off[size_t(r)], b = c->shard_off[size_t(r) + 1];
@@ -1032,8 +1230,13 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     check_ctx(c);
     if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_host before ek_spmv_setup");
     DBuf dx, dy;
-    std::vector<double> xp;  // sharded: the padded all-gather layout
-    if (c->mr) {
+    std::vector<double> xp;  // sharded: the padded all-gather layout (or the halo layout)
+    if (c->halo) {
+        xp.assign(size_t(x_extent(c)), 0.0);
+        for (size_t t = 0; t < xp.size(); ++t)
+            if (c->hx_gidx_h[t] >= 0) xp[t] = x[c->hx_gidx_h[t]];
+        x = xp.data();
+    } else if (c->mr) {
         xp.assign(size_t(x_extent(c)), 0.0);
         for (int r = 0; r < c->nranks; ++r)
             std::copy(x + c->shard_off[size_t(r)], x + c->shard_off[size_t(r) + 1], xp.begin() + r * c->slot);
@@ -1070,7 +1273,8 @@ int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
     for (double v : h) nrm += v * v;
     HIPCHK(hipMemcpyAsync(x.p, h.data(), X * 8, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(fn2.p, &nrm, 8, hipMemcpyHostToDevice, s));
-    const double* fsrc = x.as<double>() + (c->mr ? size_t(c->rank * c->slot) : 0);  // this rank's rows of x
+    // this rank's rows of x
+    const double* fsrc = x.as<double>() + (c->halo ? size_t(c->hx_base[size_t(c->rank)]) : c->mr ? size_t(c->rank * c->slot) : 0);
     // fused == 2: also the Lanczos step's finalize folded into the prologue
     // (||f||^2 from the update's one value, block 0 publishing alpha / offd)
     // and the ||w||^2 partials of partial reorthogonalisation: the SpMV exactly
@@ -1142,6 +1346,28 @@ int ek_spmv_format(ek_ctx* c, int32_t* packed, int64_t* stored_bytes) {
     EK_CATCH
 }
 
+int ek_spmv_exchange(ek_ctx* c, int32_t* halo, int64_t* recv_doubles, int64_t* send_doubles) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_exchange before ek_spmv_setup");
+    int64_t rv = 0, sd = 0;
+    if (c->halo) {
+        for (int q = 0; q < c->nranks; ++q)
+            if (q != c->rank) {
+                rv += c->hx_rcnt[size_t(q)] + 1;
+                sd += c->hx_scnt[size_t(q)] + 1;
+            }
+    } else if (c->mr) {
+        rv = (c->nranks - 1) * c->slot;
+        sd = (c->nranks - 1) * c->slot;
+    }
+    if (halo) *halo = c->halo ? 1 : 0;
+    if (recv_doubles) *recv_doubles = rv;
+    if (send_doubles) *send_doubles = sd;
+    return EK_OK;
+    EK_CATCH
+}
+
 // ---------------------------------------------------------------------------
 // Lanczos (Spectra SymEigsSolver restated, cEIG.cpp:194-207)
 void ek_lanczos_default_opts(ek_lanczos_opts* o) {
@@ -1205,6 +1431,10 @@ struct Lanczos {
     // slot layout the matrix's columns were remapped to)
     const double* gather_f() {
         if (!c->mr) return c->f.as<double>();
+        if (c->halo) {
+            halo_exchange(c, c->f.as<double>(), s);
+            return c->hx_X.as<double>();
+        }
         allgather(c, c->f.as<double>(), size_t(c->slot), c->xfull.as<double>());
         return c->xfull.as<double>();
     }
@@ -1312,6 +1542,28 @@ struct Lanczos {
         double* f = c->f.as<double>();
         ek::dev::finalize_step(s, c->npart.as<double>(), nub, f + ldv, nullptr, nullptr, -1, nullptr, nullptr);
         const double* x = f;
+        if (c->halo) {  // only the rows each rank reads, into the compact x (its partials inside)
+            if (overlap) {
+                HIPCHK(hipEventRecord(c->ag_ev[0], s));
+                HIPCHK(hipStreamWaitEvent(c->gstream, c->ag_ev[0], 0));
+                ek::dev::spmv(s, own_mat(c), f, c->yown.as<double>(), nullptr, nullptr, nullptr, nullptr);
+                halo_exchange(c, f, c->gstream);
+                HIPCHK(hipEventRecord(c->ag_ev[1], c->gstream));
+                HIPCHK(hipStreamWaitEvent(s, c->ag_ev[1], 0));
+                fin.own_lo = int(c->hx_base[size_t(c->rank)]);
+                fin.own_hi = int(c->hx_base[size_t(c->rank)] + c->nrows);
+                fin.ybase = c->yown.as<double>();
+            } else {
+                halo_exchange(c, f, s);
+            }
+            x = c->hx_X.as<double>();
+            fin.npart = x;
+            fin.nb = c->nranks;
+            fin.nstride = 0;
+            for (int q = 0; q < c->nranks; ++q) fin.nat[q] = int(c->hx_base[size_t(q) + 1] - 1);
+            fin.fn2_out = c->fn2.as<double>() + i;
+            return x;
+        }
         if (c->mr && overlap) {
             // f (with this rank's ||f||^2 partial at f[ldv]) is final: the
             // all-gather goes out on gstream, and the owned slot's rows are
@@ -2251,6 +2503,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             const int64_t a = c->shard_off[size_t(r)], b = c->shard_off[size_t(r) + 1];
             if (b > a)
                 HIPCHK(hipMemcpyAsync(xc + a, xg + r * c->slot, size_t(b - a) * 8, hipMemcpyDeviceToDevice, s));
+        }
+        if (c->halo) {  // the residual's SpMV reads the compact layout: from the full vector, no collective
+            ek::dev::gather_idx(s, xc, c->hx_gidx.as<int>(), (long long)x_extent(c), c->hx_X.as<double>());
+            xg = c->hx_X.as<double>();
         }
     }
     HIPCHK(hipMemcpyAsync(v, xc, size_t(n) * 8, hipMemcpyDeviceToHost, s));

@@ -169,6 +169,7 @@ typedef struct ihipEvent_t* hipEvent_t;
 // block sums the same partials in the same order — and block 0 publishes
 // fn2_out, alpha[step] = *a3 + h2[step], offd[step] = beta_step + h2[step-1]
 // with beta_step = *bov_i unless NaN, else sqrt(*fn2_i).  npart == null: none.
+constexpr int MAX_HALO_RANKS = 16;  // ranks of the halo exchange (ctx.cpp halo_build); more: the full all-gather
 struct StepFin {
     const double* npart = nullptr;
     int nb = 0;
@@ -181,6 +182,9 @@ struct StepFin {
     const double* fn2_i = nullptr;
     const double* bov_i = nullptr;
     int nstride = 1;  // npart[k * nstride], k < nb (the sharded step: each rank's ||f||^2 in its all-gather slot)
+    // the halo exchange's compact x (nstride 0): rank k's partial at
+    // npart[nat[k]], after its block (k < nb <= MAX_HALO_RANKS)
+    int nat[MAX_HALO_RANKS] = {};
     // ||f||^2 from the update (||f'||^2 - ||h||^2, k_update B32) when not
     // NaN; NaN: summed from npart
     const double* fast = nullptr;
@@ -314,6 +318,13 @@ void remap_cols(hipStream_t s, long long nnz, int* col, const long long* off, in
 // a second call with the output arrays (orp: nr + 1) fills them
 long long own_split(hipStream_t s, long long nr, const int* rowptr, const int* col, const double* val, int lo, int hi,
                     int* cnt, long long* off, long long* tiles, int* orp, int* ocol, double* oval);
+// the halo exchange (ctx.cpp halo_build): sbuf[t] = f[sidx[t]] for t <
+// nsend, and the rank's own block X[base + k] = f[k] (k < nrows), X[base +
+// nrows] = f[ldv] (its ||f||^2 partial)
+void halo_pack(hipStream_t s, const double* f, int ldv, const int* sidx, long long nsend, double* sbuf, double* X,
+               long long base, long long nrows);
+// X[t] = x[gidx[t]], 0.0 where gidx[t] < 0
+void gather_idx(hipStream_t s, const double* x, const int* gidx, long long len, double* X);
 
 // The memory order of the counter adds that pick the last workgroup of an
 // in-launch hand-off (kernels_spmv/lanczos/panel.hip).  The partials travel

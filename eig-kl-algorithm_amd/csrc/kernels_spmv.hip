@@ -58,6 +58,18 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ x, int 
     return s;
 }
 
+// the thread partial of the ranks' ||f||^2 partials (StepFin): strided, or
+// at the halo layout's offsets (nstride 0; nb <= MAX_HALO_RANKS, so thread t
+// holds partial t alone: strided_sum's order)
+__device__ __forceinline__ double fin_partials(const StepFin& fin) {
+    if (fin.nstride != 0) return strided_sum(fin.npart, fin.nb, fin.nstride);
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < MAX_HALO_RANKS; ++k)
+        if (k < fin.nb && int(threadIdx.x) == k) v = fin.npart[fin.nat[k]];
+    return v;
+}
+
 // the fixed tree over the workgroup of the thread partials; every thread gets it.
 // (A barrier-free form where every wave reduces all 1024 partials itself, same
 // bits, measured slower inside the solve: 15.3 vs 12.7 us per SpMV.)
@@ -172,7 +184,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     // only when it is NaN, a breakdown)
     const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
     const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
-    const double npart_t = sum_parts ? strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
+    const double npart_t = sum_parts ? fin_partials(fin) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
             const double n2 = sum_parts ? block_sum_all(npart_t, wsum) : fastv;

@@ -188,6 +188,13 @@ int64_t ek_spmv_bytes(ek_ctx* ctx);
  * entries + table + rowptr + 8*n (x) + 8*nrows (y).  Either pointer may be
  * NULL. */
 int ek_spmv_format(ek_ctx* ctx, int32_t* packed, int64_t* stored_bytes);
+/* The sharded step's exchange of f as set up: *halo = 1 when each rank
+ * receives only the rows its columns read (point-to-point messages in one
+ * RCCL group), 0 for the all-gather of whole slots; the doubles this rank
+ * receives and sends per Lanczos step (each message carries the sender's
+ * ||f||^2 partial).  A single context: 0, 0, 0.  No reference counterpart
+ * (the reference has no sharded path). */
+int ek_spmv_exchange(ek_ctx* ctx, int32_t* halo, int64_t* recv_doubles, int64_t* send_doubles);
 /* Back-to-back SpMV launches on context-owned buffers, timed with HIP events
  * around the batch: *avg_us = average per launch (a sharded context: this
  * rank's rows over the all-gather layout, no collective).  fused = 2: also the

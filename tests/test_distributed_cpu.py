@@ -181,3 +181,112 @@ def test_shard_map_is_what_the_library_enforces():
         assert all(s[2] == nloc for s in slices)
         assert nloc * world >= n and nloc * (world - 1) < n
         assert sum(s[1] for s in slices) == n
+
+
+def _halo_worker(rank, world, port, out):
+    """ctx.cpp halo_build / halo_exchange restated: the request lists from the
+    slot-layout columns, one all-gather of the counts and one of the lists
+    (setup), then per step ONE exchange of packed messages (here the
+    host-staged form: an all-gather of every rank's padded messages, of which
+    each rank keeps its pieces) into the compact x whose block q holds q's
+    rows this rank reads and q's ||f||^2 partial."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ek = load_package()
+        h = ek.Hypergraph.generate(0.05, 3)
+        n = h.nodes
+        L = h.laplacian()
+        off = ek.shard_map(h, world)
+        row0, nrows = int(off[rank]), int(off[rank + 1] - off[rank])
+        ldv = -(-int(np.diff(off).max()) // 1024) * 1024
+        S = ldv + 64
+        Sr = h.laplacian_rows(row0, row0 + nrows)
+        owner = np.searchsorted(off[1:-1], Sr.col, side="right")
+        colx = owner * S + (Sr.col - off[owner])
+
+        def ag(a):
+            parts = [torch.zeros(len(a), dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(a, np.float64)))
+            return np.stack([p.numpy() for p in parts])
+
+        req = [np.unique(Sr.col[owner == q]) - off[q] if q != rank else np.zeros(0, np.int64) for q in range(world)]
+        C = ag(np.array([len(r) for r in req], np.float64)).astype(np.int64)  # C[r, q]
+        lmax = max(1, max(sum(C[r, q] for q in range(world) if q != r) for r in range(world)))
+        mine = np.zeros(lmax)
+        cat = np.concatenate([req[q] for q in range(world)]) if world > 1 else np.zeros(0)
+        mine[:len(cat)] = cat
+        lall = ag(mine).astype(np.int64)
+        # send lists: rank r's request from this rank inside r's list
+        sidx = []
+        for r in range(world):
+            if r == rank:
+                continue
+            o = sum(C[r, q] for q in range(rank) if q != r)
+            sidx += list(lall[r, o:o + C[r, rank]]) + [ldv]
+        sidx = np.array(sidx, np.int64)
+        rcnt = [nrows if q == rank else C[rank, q] for q in range(world)]
+        base = np.concatenate([[0], np.cumsum([c + 1 for c in rcnt])])
+        src = []
+        smax = 1
+        for q in range(world):
+            o = 0
+            for r in range(world):
+                if r == q:
+                    continue
+                if r == rank:
+                    src.append(o)
+                o += C[r, q] + 1
+            if q == rank:
+                src.append(0)
+            smax = max(smax, o)
+        # the compact column map (monotone)
+        pos = [dict((int(l), k) for k, l in enumerate(req[q])) for q in range(world)]
+        colh = np.array([base[q] + (c - q * S if q == rank else pos[q][c - q * S])
+                         for q, c in zip(colx // S, colx)], np.int64)
+        rp = Sr.rowptr.astype(np.int64)
+        for r_ in range(nrows):  # rows stay sorted
+            seg = colh[rp[r_]:rp[r_ + 1]]
+            assert np.all(np.diff(seg) > 0)
+        # one step's exchange of a vector f (its partial at f[ldv])
+        x0 = np.random.default_rng(5).standard_normal(n)
+        f = np.zeros(S)
+        f[:nrows] = x0[row0: row0 + nrows]
+        f[ldv] = f[:nrows] @ f[:nrows]
+        sbuf = np.zeros(smax)
+        sbuf[:len(sidx)] = f[sidx]                        # k_halo_pack (messages)
+        X = np.zeros(base[-1])
+        X[base[rank]: base[rank] + nrows] = f[:nrows]      # ... and the own block
+        X[base[rank] + nrows] = f[ldv]
+        g = ag(sbuf)                                       # the step's one exchange
+        for q in range(world):
+            if q != rank:
+                X[base[q]: base[q + 1]] = g[q, src[q]: src[q] + rcnt[q] + 1]
+        # the same products in the same order: y bit-equal to the slot layout's
+        xs = np.zeros(world * S)
+        for q in range(world):
+            xs[q * S: q * S + off[q + 1] - off[q]] = x0[off[q]: off[q + 1]]
+        y_slot = _local_spmv(rp, colx, Sr.val, xs)
+        y_halo = _local_spmv(rp, colh, Sr.val, X)
+        parts = [X[base[q + 1] - 1] for q in range(world)]
+        out[rank] = {"same_bits": y_slot.tobytes() == y_halo.tobytes(),
+                     "partials": [float(p) for p in parts],
+                     "recv": int(sum(rcnt[q] + 1 for q in range(world) if q != rank)),
+                     "recv_full": int((world - 1) * S)}
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange_layout(world):
+    """The compact halo layout gives the slot layout's SpMV bit for bit, and
+    every rank reads every rank's ||f||^2 partial (the same values, rank
+    order) out of the blocks it received."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_halo_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r]["same_bits"], out[r]
+        assert out[r]["partials"] == out[0]["partials"]
+        assert out[r]["recv"] <= out[r]["recv_full"]

@@ -118,6 +118,22 @@ def _worker(rank, port, tmp, out):
             absrow = np.add.reduceat(np.abs(S.val * x[S.col]), S.rowptr[:-1])
             r["spmv_rows_ok"] = bool(np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300))
             r["spmv_max_abs_diff"] = float(np.abs(y - y1).max())
+            # the halo exchange (each rank receives only the rows its columns
+            # read) against the all-gather of whole slots: the same bits
+            hb = {}
+            for mode in ("1", "0"):
+                os.environ["EK_MR_HALO"] = mode
+                try:
+                    ctx.spmv_setup(n, row0, S.rowptr, S.col, S.val)
+                    c0 = dict(counts)
+                    lam_h, v_h, st_h = ctx.lanczos_fiedler()
+                    hb[mode] = dict(lam=lam_h, v=v_h.tobytes(), ex=ctx.spmv_exchange(), matvecs=st_h["matvecs"],
+                                    ag=counts["allgather"] - c0["allgather"], y=ctx.spmv_host(x).tobytes())
+                finally:
+                    del os.environ["EK_MR_HALO"]
+            r["halo"] = {"same_bits": hb["1"]["lam"] == hb["0"]["lam"] and hb["1"]["v"] == hb["0"]["v"],
+                         "spmv_same": hb["1"]["y"] == hb["0"]["y"], "ex1": hb["1"]["ex"], "ex0": hb["0"]["ex"],
+                         "ag": hb["1"]["ag"], "matvecs": hb["1"]["matvecs"]}
             res[name] = r
         # the whole file path, sharded: rank 0 writes the results file
         rr, _ = ctx.solve_file(circuit_path("ibm01"), eig=1, out_dir=os.path.join(tmp, f"r{rank}"))
@@ -174,6 +190,13 @@ def test_two_rank_sharded_lanczos_through_comm_seam(tmp_path):
             assert p["projected"] < 0.6 * p["matvecs"] and r[name][1]["projected"] == r[name][1]["matvecs"], p
             assert p["ortho_max"] <= 1e-8 and p["same_bits_with_ortho_check"], p
             assert p["matvecs"] <= 1.05 * r[name][1]["matvecs"], (p, r[name][1])
+    for r in (r0, r1):
+        for name in ("ibm01", "industry2"):
+            hl = r[name]["halo"]
+            print(name, "halo", hl)
+            assert hl["same_bits"] and hl["spmv_same"], hl
+            assert hl["ex1"][0] and not hl["ex0"][0] and hl["ex1"][1] <= hl["ex0"][1], hl
+            assert hl["ag"] == hl["matvecs"] + 1, hl  # (one exchange a step + the final vector's all-gather)
     assert r1["ibm01"]["row0"] > 0 and r0["ibm01"]["nrows"] + r1["ibm01"]["nrows"] == 12752
     assert r0["industry2"]["nrows"] != r1["industry2"]["nrows"]  # nnz-balanced: unequal slices
     # every rank holds the same full vector: identical Ritz pairs
@@ -308,7 +331,20 @@ def test_rccl_one_rank_production_path(ek, monkeypatch, name, reorth):
         lam_n, v_n, st_n = c.lanczos_fiedler(reorth=reorth)
     finally:
         c.close()
+    # the halo layout forced on (one rank: the own block alone, the pack kernel and the
+    # compact column map): the same bits as the slot layout
+    monkeypatch.setenv("EK_MR_HALO", "1")
+    monkeypatch.delenv("EK_MR_OVERLAP")
+    c = ek.Context(0)
+    try:
+        c.comm_init(1, 0, ek.comm_unique_id())
+        c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+        assert c.spmv_exchange() == (True, 0, 0)
+        lam_x, v_x, st_x = c.lanczos_fiedler(reorth=reorth)
+    finally:
+        c.close()
     (lam, v, st), (lam_h, v_h, st_h) = out["rccl"], out["host"]
+    assert lam_x == lam and v_x.tobytes() == v.tobytes() and st_x["allgathers"] == st["allgathers"]
     print(name, {k: st[k] for k in ("matvecs", "restarts", "allgathers", "allreduces", "reprojected", "residual")})
     assert abs(lam_n - lam) <= 1e-10 and st_n["residual"] < 1e-9
     assert _fiedler_ok(ek, name, lam_n, v_n)["bits_equal"]
@@ -380,6 +416,17 @@ def _worker_head(rank, port, out):
         finally:
             del os.environ["EK_LANCZOS_ORTHO"]
         res["ortho_max"] = st["ortho_max"]
+        res["exchange_default"] = ctx.spmv_exchange()
+        # the halo exchange forced on and off: the same pair, bit for bit
+        for mode in ("1", "0"):
+            os.environ["EK_MR_HALO"] = mode
+            try:
+                assert ctx.spmv_setup_pins(h) is True
+                lam, v, st = ctx.lanczos_fiedler()
+                res[f"halo{mode}"] = dict(lam=lam, v_sha=__import__("hashlib").sha1(v.tobytes()).hexdigest(),
+                                          ex=ctx.spmv_exchange())
+            finally:
+                del os.environ["EK_MR_HALO"]
         ctx.close()
     except Exception:
         import traceback
@@ -429,3 +476,8 @@ def test_two_rank_headline_partial_reorth():
         assert r["ortho_max"] <= 1e-8
     for reorth in (3, 1):
         assert r0[reorth]["lam"] == r1[reorth]["lam"] and r0[reorth]["v_sha"] == r1[reorth]["v_sha"]
+    for r in (r0, r1):
+        print("exchange", r["exchange_default"], r["halo1"]["ex"], r["halo0"]["ex"])
+        assert r["halo1"]["lam"] == r["halo0"]["lam"] == r[3]["lam"]
+        assert r["halo1"]["v_sha"] == r["halo0"]["v_sha"] == r[3]["v_sha"]
+        assert r["halo1"]["ex"][0] and not r["halo0"]["ex"][0] and r["halo1"]["ex"][1] < r["halo0"]["ex"][1]
