@@ -440,6 +440,7 @@ def main():
         c10 = ctx
         c10.spmv_setup_pins(h10)  # this rank's nnz-balanced rows, built on the device
         _, r0, nr = c10.spmv_dims()
+        hl10, rv10, sd10 = c10.spmv_exchange()
         st10 = None
         tt = []
         for i in range(2):
@@ -460,7 +461,12 @@ def main():
                  "spmv_GBps_aggregate": round(world * b10 / us10_max / 1e3, 1),
                  "spmv_timing": "HIP kernel start/end events of every 4th SpMV (this process)",
                  "collectives_per_solve": {"allgather": st10["allgathers"], "allreduce": st10["allreduces"]},
-                 "comm_ms_per_solve": round(max_over_ranks(st10["comm_ms"]), 3), "comm": comm if world > 1 else None}
+                 "comm_ms_per_solve": round(max_over_ranks(st10["comm_ms"]), 3), "comm": comm if world > 1 else None,
+                 "exchange": {"form": ("halo (rows each rank reads, RCCL send/recv)" if hl10 else
+                                       "all-gather of whole slots") if world > 1 else None,
+                              "recv_MB_per_step_rank0": round(8 * rv10 / 1e6, 3),
+                              "send_MB_per_step_rank0": round(8 * sd10 / 1e6, 3)},
+                 "projected_steps": st10["projected_steps"]}
         calls10, us10_rp = kernel_avg_us(prof.get("trace10"), "k_spmv")
         if us10_rp:  # the rocprofv3 kernel trace (a child pass before this process touched the GPU)
             syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,

@@ -82,7 +82,12 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ct
 
 
 def _sig(name, res, *args):
-    fn = getattr(_lib, name)
+    try:
+        fn = getattr(_lib, name)
+    except AttributeError:
+        if os.environ.get("EK_LIB_PATH"):  # (a lab's older A/B build: the entry is simply absent)
+            return None
+        raise
     fn.restype = res
     fn.argtypes = list(args)
     return fn
@@ -90,10 +95,10 @@ def _sig(name, res, *args):
 
 _sig("ek_last_error", ctypes.c_char_p)
 _sig("ek_version", ctypes.c_char_p)
-_sig("ek_abi_version", ctypes.c_int)
 ABI_VERSION = 4  # eigkl.h EIGKL_ABI_VERSION: the ctypes struct mirrors below follow that layout
-if _lib.ek_abi_version() != ABI_VERSION:
-    raise ImportError(f"libeigkl_hip ABI {_lib.ek_abi_version()} != the {ABI_VERSION} these bindings mirror: rebuild")
+if _sig("ek_abi_version", ctypes.c_int) is not None:
+    if _lib.ek_abi_version() != ABI_VERSION:
+        raise ImportError(f"libeigkl_hip ABI {_lib.ek_abi_version()} != the {ABI_VERSION} these bindings mirror: rebuild")
 _sig("ek_hgr_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_P))
 _sig("ek_hgr_generate", ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.POINTER(_P))
 _sig("ek_hgr_from_pins", ctypes.c_int, _I64, _I64, _P, _P, ctypes.POINTER(_P))

@@ -131,19 +131,19 @@ struct ek_ctx {
     // The halo exchange of the sharded step (halo_build): instead of every
     // rank's whole slot, each rank receives only the rows of f its columns
     // read, into a compact x: block q (ranks in order) holds the rows of rank
-    // q this rank reads, ascending (its own block: all its rows), then q's
-    // ||f||^2 partial.  The columns are remapped monotonically to it, so rows
-    // stay sorted and every product is summed in the same order as over the
-    // slot layout: the same bits.  Used where it moves fewer bytes than the
-    // all-gather (EK_MR_HALO=0/1 forces either).
+    // q this rank reads, ascending (its own block: all its rows); the ranks'
+    // ||f||^2 partials land in hx_P[q].  The columns are remapped
+    // monotonically to it, so rows stay sorted and every product is summed in
+    // the same order as over the slot layout: the same bits.  Used where it
+    // moves fewer bytes than the all-gather (EK_MR_HALO=0/1 forces either).
     bool halo = false;
-    std::vector<int64_t> hx_base;             // nranks + 1: block q at [hx_base[q], hx_base[q+1]); last = partial
+    std::vector<int64_t> hx_base;             // nranks + 1: block q at [hx_base[q], hx_base[q+1])
     std::vector<int64_t> hx_rcnt;             // rows received from q (own: nrows)
     std::vector<int64_t> hx_scnt, hx_soff;    // rows sent to q, and that message's offset in hx_sbuf (+1: the partial)
     std::vector<int64_t> hx_src;              // host-staged: q's message to this rank inside q's (padded) sbuf
     std::vector<int32_t> hx_gidx_h;           // X[t]'s global row (-1: a partial slot)
     int64_t hx_nsend = 0, hx_smax = 0;
-    DBuf hx_sidx, hx_sbuf, hx_X, hx_gidx, hx_gbuf;
+    DBuf hx_sidx, hx_sbuf, hx_X, hx_P, hx_gidx, hx_gbuf;
     // the owned-slot part of a sharded rank's rows (plain CSR, local column
     // ids), summed while the all-gather of the other slots runs on `gstream`
     DBuf own_rowptr, own_col, own_val, own_rb, yown;
@@ -156,6 +156,7 @@ struct ek_ctx {
     int pn_G = 0, pn_P = 0, pn_pb = 0, pn_max_rows = 0, pn_ndict = 0;
     DBuf pn_wrow, pn_start, pn_word, pn_rid;
     int block_nnz = 1024, nrb_spmv = 0;
+    bool spmv_long = true;  // a row block is one row longer than block_nnz (the SpMV's vector mode)
     DBuf rb, rowptr, col, val, pk, rel, dict;
     int colbits = 0;  // > 0: the dictionary-coded matrix (pk, dict) is the one the SpMV reads
     int64_t mat_bytes = 0;  // bytes of the matrix arrays one SpMV reads, as stored
@@ -255,6 +256,7 @@ ek::dev::SpmvMat spmv_mat(const ek_ctx* c) {
         return m;
     }
     m.block_nnz = c->block_nnz;
+    m.has_long = c->spmv_long;
     m.desc = c->rb.as<int32_t>();
     m.rowptr = c->rowptr.as<int32_t>();
     if (c->colbits > 0) {
@@ -621,7 +623,7 @@ bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
     c->hx_base.assign(size_t(R) + 1, 0);
     for (int q = 0; q < R; ++q) {
         c->hx_rcnt[size_t(q)] = q == me ? c->nrows : Cat(me, q);
-        c->hx_base[size_t(q) + 1] = c->hx_base[size_t(q)] + c->hx_rcnt[size_t(q)] + 1;
+        c->hx_base[size_t(q) + 1] = c->hx_base[size_t(q)] + c->hx_rcnt[size_t(q)];
     }
     // host-staged exchange: q's sbuf lists its messages to r = 0, 1, ... (r != q)
     c->hx_src.assign(size_t(R), 0);
@@ -656,7 +658,8 @@ bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
     upload(c->hx_sidx, sidx.data(), sidx.size(), c->stream);
     upload(c->hx_gidx, c->hx_gidx_h.data(), c->hx_gidx_h.size(), c->stream);
     c->hx_sbuf.ensure(size_t(std::max(c->hx_smax, c->hx_nsend)) * 8);
-    c->hx_X.ensure(size_t(c->hx_base.back()) * 8);
+    c->hx_X.ensure(size_t(std::max<int64_t>(c->hx_base.back(), 1)) * 8);
+    c->hx_P.ensure(size_t(R) * 8);
     if (!c->comm) c->hx_gbuf.ensure(size_t(c->hx_smax) * size_t(R) * 8);
     HIPCHK(hipMemsetAsync(c->hx_sbuf.p, 0, c->hx_sbuf.bytes, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -665,24 +668,31 @@ bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
 }
 
 // One halo exchange of src (this rank's rows, its ||f||^2 partial at
-// src[ldv]) into the compact x (c->hx_X), on stream st: the pack, then RCCL
-// point-to-point messages to and from every peer in one group, or, staged
-// through the host, an all-gather of every rank's (padded) messages of which
-// this rank keeps its pieces.  Counted as the step's one all-gather.
+// src[ldv]) into the compact x (c->hx_X) and the ranks' partials (c->hx_P),
+// on stream st: the pack, then RCCL point-to-point messages to and from every
+// peer in one group (the rows, then the partial: each message is closed by
+// it in sbuf), or, staged through the host, an all-gather of every rank's
+// (padded) messages of which this rank keeps its pieces.  Counted as the
+// step's one all-gather.
 void halo_exchange(ek_ctx* c, const double* src, hipStream_t st) {
     const int R = c->nranks, me = c->rank;
     double* X = c->hx_X.as<double>();
+    double* P = c->hx_P.as<double>();
     double* sb = c->hx_sbuf.as<double>();
     ek::dev::halo_pack(st, src, int(c->slot - 64), c->hx_sidx.as<int>(), c->hx_nsend, sb, X, c->hx_base[size_t(me)],
-                       c->nrows);
+                       c->nrows, P + me);
     if (c->comm) {
         ++c->n_ag;
         if (R == 1) return;
         NCCLCHK(ncclGroupStart());
         for (int q = 0; q < R; ++q) {
             if (q == me) continue;
-            NCCLCHK(ncclSend(sb + c->hx_soff[size_t(q)], size_t(c->hx_scnt[size_t(q)] + 1), ncclDouble, q, c->comm, st));
-            NCCLCHK(ncclRecv(X + c->hx_base[size_t(q)], size_t(c->hx_rcnt[size_t(q)] + 1), ncclDouble, q, c->comm, st));
+            const int64_t sc = c->hx_scnt[size_t(q)], rc = c->hx_rcnt[size_t(q)];
+            double* sq = sb + c->hx_soff[size_t(q)];
+            if (sc) NCCLCHK(ncclSend(sq, size_t(sc), ncclDouble, q, c->comm, st));
+            NCCLCHK(ncclSend(sq + sc, 1, ncclDouble, q, c->comm, st));
+            if (rc) NCCLCHK(ncclRecv(X + c->hx_base[size_t(q)], size_t(rc), ncclDouble, q, c->comm, st));
+            NCCLCHK(ncclRecv(P + q, 1, ncclDouble, q, c->comm, st));
         }
         NCCLCHK(ncclGroupEnd());
         return;
@@ -694,9 +704,12 @@ void halo_exchange(ek_ctx* c, const double* src, hipStream_t st) {
     double* g = c->hx_gbuf.as<double>();
     allgather(c, sb, size_t(c->hx_smax), g, st);
     for (int q = 0; q < R; ++q)
-        if (q != me)
-            HIPCHK(hipMemcpyAsync(X + c->hx_base[size_t(q)], g + size_t(q) * size_t(c->hx_smax) + c->hx_src[size_t(q)],
-                                  size_t(c->hx_rcnt[size_t(q)] + 1) * 8, hipMemcpyDeviceToDevice, st));
+        if (q != me) {
+            const double* m = g + size_t(q) * size_t(c->hx_smax) + c->hx_src[size_t(q)];
+            const int64_t rc = c->hx_rcnt[size_t(q)];
+            if (rc) HIPCHK(hipMemcpyAsync(X + c->hx_base[size_t(q)], m, size_t(rc) * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(P + q, m + rc, 8, hipMemcpyDeviceToDevice, st));
+        }
 }
 
 // The column-panel form when x outgrows an XCD's L2 (EK_SPMV_PANEL=0/1 forces
@@ -881,9 +894,11 @@ void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, cons
             return;
         }
     }
-    c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
+    c->block_nnz = ek::dev::SPMV_SEG_NNZ;  // (coded or plain: the same row blocks, so the same sums)
     auto rbv = ek::dev::spmv_row_blocks(rowptr, nrows, c->block_nnz);
     c->nrb_spmv = int(rbv.size() / 4);
+    c->spmv_long = false;
+    for (size_t bk = 0; bk < rbv.size() / 4; ++bk) c->spmv_long = c->spmv_long || rbv[4 * bk + 3] > c->block_nnz;
     c->colbits = packed ? colbits : 0;
     if (packed) {
         std::vector<uint32_t> segv;
@@ -1154,9 +1169,11 @@ static int spmv_setup_pins_impl(ek_ctx* c, int64_t n, int64_t nets, const int64_
             return EK_OK;
         }
     }
-    c->block_nnz = packed ? ek::dev::SPMV_SEG_NNZ : 512;
+    c->block_nnz = ek::dev::SPMV_SEG_NNZ;  // (coded or plain: the same row blocks, so the same sums)
     auto rbv = ek::dev::spmv_row_blocks(rowptr.data(), nrows, c->block_nnz);
     c->nrb_spmv = int(rbv.size() / 4);
+    c->spmv_long = false;
+    for (size_t bk = 0; bk < rbv.size() / 4; ++bk) c->spmv_long = c->spmv_long || rbv[4 * bk + 3] > c->block_nnz;
     if (packed) {
         const size_t nb = size_t(c->nrb_spmv), SEG = size_t(ek::dev::SPMV_SEG_NNZ);
         size_t over = 0;  // long rows: overflow area after the segments (spmv_segment's layout)
@@ -1402,14 +1419,16 @@ namespace {
 // the 10 x DBL_MIN bound (an exact-zero test) the restarts kept 50 vectors
 // and ibm10 took 11,006 matvecs instead of 1,201, the 1x synthetic 2,683
 // instead of 507 (tools/lanczos_trace.py)
-int nev_adjusted(int nev, int ncv, int nconv, const std::vector<double>& est) {
+// arpack_half: ARPACK's (and Spectra's) jump to ncv/2 kept vectors when
+// nothing else counts (false: the caller's floor decides instead)
+int nev_adjusted(int nev, int ncv, int nconv, const std::vector<double>& est, bool arpack_half = true) {
     const double eps = std::numeric_limits<double>::epsilon();
     int nev_new = nev;
     for (int i = nev; i < ncv; ++i)
         if (std::fabs(est[size_t(i)]) < eps) ++nev_new;
     nev_new += std::min(nconv, (ncv - nev_new) / 2);
-    if (nev_new == 1 && ncv >= 6) nev_new = ncv / 2;
-    else if (nev_new == 1 && ncv > 2) nev_new = 2;
+    if (arpack_half && nev_new == 1 && ncv >= 6) nev_new = ncv / 2;
+    else if (arpack_half && nev_new == 1 && ncv > 2) nev_new = 2;
     if (nev_new > ncv - 1) nev_new = ncv - 1;
     return nev_new;
 }
@@ -1557,10 +1576,9 @@ struct Lanczos {
                 halo_exchange(c, f, s);
             }
             x = c->hx_X.as<double>();
-            fin.npart = x;
+            fin.npart = c->hx_P.as<double>();
             fin.nb = c->nranks;
-            fin.nstride = 0;
-            for (int q = 0; q < c->nranks; ++q) fin.nat[q] = int(c->hx_base[size_t(q) + 1] - 1);
+            fin.nstride = 1;
             fin.fn2_out = c->fn2.as<double>() + i;
             return x;
         }
@@ -2398,7 +2416,16 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // (a fixed restart size of 8, 12 or 20 kept vectors, or a cap of 10-30,
         // was no better over ibm01 / industry2 / ibm10 / the 1x synthetic and
         // its largest component, and some sizes lost 3-12x on one of them)
-        int knew = nev_adjusted(nev, m, nconv, zl);
+        const bool floor_on = keep_min > 0 && std::fabs(theta[size_t(nev - 1)]) > 1e-8 * anorm_of();
+        // Where the floor applies, it replaces ARPACK's jump to ncv/2 kept
+        // vectors (taken when no unwanted Ritz estimate is below eps): which
+        // side of eps those estimates fall on is rounding noise, and the jump
+        // turned the headline's 6 restarts into 9 (50 kept instead of 20, the
+        // same 527 matvecs: 20.0 -> 18.5 ms, tools/restart_ab.py,
+        // profiles/r05/restart_ab_keephalf.txt).  EK_KEEP_HALF=1 keeps it.
+        const char* kh_env = std::getenv("EK_KEEP_HALF");
+        const bool keep_half = kh_env && kh_env[0] == '1';
+        int knew = nev_adjusted(nev, m, nconv, zl, !floor_on || keep_half);
         // a floor on Spectra's count: its rule keeps ncv/2 when no unwanted
         // Ritz value has converged but only 1 + (those with |e_m^T y| < eps)
         // otherwise, 2-4 vectors on these Laplacians, and a restart that
@@ -2409,7 +2436,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         // slowed convergence to a null vector (10x synthetic: 362 matvecs
         // with Spectra's rule, 756 with a floor of 10, 994 with 20; the 1x
         // and 2x synthetics likewise)
-        if (keep_min > 0 && std::fabs(theta[size_t(nev - 1)]) > 1e-8 * anorm_of()) knew = std::max(knew, std::min(keep_min, m - 1));
+        if (floor_on) knew = std::max(knew, std::min(keep_min, m - 1));
         if (trace) std::fprintf(stderr, "[lanczos]   keep %d (matvecs so far %d)\n", knew, L.matvecs);
         std::vector<double> dd(d), ee(e);
         const auto tq0 = std::chrono::steady_clock::now();

@@ -182,9 +182,6 @@ struct StepFin {
     const double* fn2_i = nullptr;
     const double* bov_i = nullptr;
     int nstride = 1;  // npart[k * nstride], k < nb (the sharded step: each rank's ||f||^2 in its all-gather slot)
-    // the halo exchange's compact x (nstride 0): rank k's partial at
-    // npart[nat[k]], after its block (k < nb <= MAX_HALO_RANKS)
-    int nat[MAX_HALO_RANKS] = {};
     // ||f||^2 from the update (||f'||^2 - ||h||^2, k_update B32) when not
     // NaN; NaN: summed from npart
     const double* fast = nullptr;
@@ -252,6 +249,7 @@ void encode_words(hipStream_t s, long long nnz, const int* col, const double* va
 // same summation order: results are bit-identical to the plain form.
 struct SpmvMat {
     int nblocks = 0, block_nnz = 512, colbits = 0;
+    bool has_long = true;  // some block is one row longer than block_nnz (vector mode); false: that code is compiled out
     const int32_t* desc = nullptr;
     const int32_t* rowptr = nullptr;
     const int32_t* col = nullptr;
@@ -261,7 +259,10 @@ struct SpmvMat {
     const double* dict = nullptr;
     SpmvPanel panel;  // panel.G > 0: the column-panel form (pk/rel/col/val unused)
 };
-constexpr int SPMV_SEG_NNZ = 512;     // default block_nnz (segment size) of the coded form
+#ifndef EK_SPMV_SEG
+#define EK_SPMV_SEG 768
+#endif
+constexpr int SPMV_SEG_NNZ = EK_SPMV_SEG;  // block_nnz (segment size) of the coded form (a multiple of 256)
 constexpr int SPMV_REL_STRIDE = 258;  // rel entries per block (nrows + 1 <= 257, padded)
 // dictionary coding of (col, val): false (pk untouched) when the distinct
 // values do not fit the 32 - colbits code bits.  dict is ordered by frequency.
@@ -319,10 +320,10 @@ void remap_cols(hipStream_t s, long long nnz, int* col, const long long* off, in
 long long own_split(hipStream_t s, long long nr, const int* rowptr, const int* col, const double* val, int lo, int hi,
                     int* cnt, long long* off, long long* tiles, int* orp, int* ocol, double* oval);
 // the halo exchange (ctx.cpp halo_build): sbuf[t] = f[sidx[t]] for t <
-// nsend, and the rank's own block X[base + k] = f[k] (k < nrows), X[base +
-// nrows] = f[ldv] (its ||f||^2 partial)
+// nsend, the rank's own block X[base + k] = f[k] (k < nrows), and its
+// ||f||^2 partial P[0] = f[ldv]
 void halo_pack(hipStream_t s, const double* f, int ldv, const int* sidx, long long nsend, double* sbuf, double* X,
-               long long base, long long nrows);
+               long long base, long long nrows, double* P);
 // X[t] = x[gidx[t]], 0.0 where gidx[t] < 0
 void gather_idx(hipStream_t s, const double* x, const int* gidx, long long len, double* X);
 

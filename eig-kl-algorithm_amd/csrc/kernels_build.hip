@@ -532,24 +532,25 @@ long long own_split(hipStream_t s, long long nr, const int* rowptr, const int* c
 // The halo exchange of the sharded step (ctx.cpp halo_build): one launch
 // packs every peer's message and this rank's own block of the compact x.
 // Messages: sbuf[t] = f[sidx[t]] for t < nsend (sidx = the rows each peer
-// reads, its block closed by the index ldv: this rank's ||f||^2 partial);
-// own block: X[base + k] = f[k] for k < nrows, X[base + nrows] = f[ldv].
+// reads, each message closed by the index ldv: this rank's ||f||^2
+// partial); own block: X[base + k] = f[k] for k < nrows, and P[0] = f[ldv].
 __global__ __launch_bounds__(BT) void k_halo_pack(const double* __restrict__ f, int ldv, const int* __restrict__ sidx,
                                                   long long nsend, double* __restrict__ sbuf, double* __restrict__ X,
-                                                  long long base, long long nrows) {
+                                                  long long base, long long nrows, double* __restrict__ P) {
     const long long t = (long long)blockIdx.x * BT + threadIdx.x;
     if (t < nsend) {
         sbuf[t] = f[sidx[t]];
         return;
     }
     const long long k = t - nsend;
-    if (k <= nrows) X[base + k] = f[k < nrows ? k : ldv];
+    if (k < nrows) X[base + k] = f[k];
+    else if (k == nrows) P[0] = f[ldv];
 }
 
 void halo_pack(hipStream_t s, const double* f, int ldv, const int* sidx, long long nsend, double* sbuf, double* X,
-               long long base, long long nrows) {
+               long long base, long long nrows, double* P) {
     const long long tot = nsend + nrows + 1;
-    hipLaunchKernelGGL(k_halo_pack, dim3(grid_of(tot)), dim3(BT), 0, s, f, ldv, sidx, nsend, sbuf, X, base, nrows);
+    hipLaunchKernelGGL(k_halo_pack, dim3(grid_of(tot)), dim3(BT), 0, s, f, ldv, sidx, nsend, sbuf, X, base, nrows, P);
 }
 
 // X[t] = x[gidx[t]] (gidx < 0: 0.0): a global n-vector into the compact halo

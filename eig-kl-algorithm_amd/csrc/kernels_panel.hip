@@ -61,16 +61,6 @@ __device__ __forceinline__ double panel_strided_sum(const double* __restrict__ x
     return s;
 }
 
-// ... of the ranks' ||f||^2 partials (kernels_spmv.hip fin_partials' rule)
-__device__ __forceinline__ double panel_fin_partials(const StepFin& fin) {
-    if (fin.nstride != 0) return panel_strided_sum(fin.npart, fin.nb, fin.nstride);
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < MAX_HALO_RANKS; ++k)
-        if (k < fin.nb && int(threadIdx.x) == k) v = fin.npart[fin.nat[k]];
-    return v;
-}
-
 __device__ __forceinline__ double panel_block_sum(double s, double* wsum) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -191,7 +181,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     // or, when that is NaN (a breakdown), the partials, whose loads go out first
     const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
     const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
-    const double npart_t = sum_parts ? panel_fin_partials(fin) : 0.0;
+    const double npart_t = sum_parts ? panel_strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
     __syncthreads();
     // The workgroup's chunks, panel by panel (every workgroup walks the panels
     // in the same order).  The next chunk's words and row indices are loaded

@@ -58,18 +58,6 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ x, int 
     return s;
 }
 
-// the thread partial of the ranks' ||f||^2 partials (StepFin): strided, or
-// at the halo layout's offsets (nstride 0; nb <= MAX_HALO_RANKS, so thread t
-// holds partial t alone: strided_sum's order)
-__device__ __forceinline__ double fin_partials(const StepFin& fin) {
-    if (fin.nstride != 0) return strided_sum(fin.npart, fin.nb, fin.nstride);
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < MAX_HALO_RANKS; ++k)
-        if (k < fin.nb && int(threadIdx.x) == k) v = fin.npart[fin.nat[k]];
-    return v;
-}
-
 // the fixed tree over the workgroup of the thread partials; every thread gets it.
 // (A barrier-free form where every wave reduces all 1024 partials itself, same
 // bits, measured slower inside the solve: 15.3 vs 12.7 us per SpMV.)
@@ -141,8 +129,14 @@ __device__ __forceinline__ void alpha_handoff(const double* apart, double* alpha
 // and row starts sit at addresses given by b alone, so their loads go out
 // together with the descriptor's instead of after it: the x gathers are two
 // dependent memory round trips from the kernel start, not three.
-template <int BLOCK_NNZ, bool PK>
-__global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __restrict__ desc,
+#ifndef EK_SPMV_WAVES
+#define EK_SPMV_WAVES 1  // minimum waves per SIMD asked of the compiler (its register budget; 1: unconstrained)
+#endif
+// LONG: some block is a single row longer than BLOCK_NNZ (vector mode);
+// ALAST: the last block reduces alpha (alpha_out).  Without them the kernel
+// carries neither path: fewer registers, more resident workgroups.
+template <int BLOCK_NNZ, bool PK, bool LONG = true, bool ALAST = true>
+__global__ __launch_bounds__(SPMV_THREADS, EK_SPMV_WAVES) void k_spmv_adaptive(const int4* __restrict__ desc,
                                                                 const int32_t* __restrict__ rowptr,
                                                                 const int32_t* __restrict__ col,
                                                                 const double* __restrict__ val, int colbits,
@@ -156,7 +150,6 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     constexpr int PER = BLOCK_NNZ / SPMV_THREADS;
     __shared__ double prod[BLOCK_NNZ];
     __shared__ int rbeg[SPMV_THREADS + 1];
-    __shared__ double yrow[SPMV_THREADS];
     __shared__ double wsum[SPMV_THREADS / 64];
     __shared__ double wsum2[SPMV_THREADS / 64];
     __shared__ int s_last;
@@ -184,7 +177,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     // only when it is NaN, a breakdown)
     const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
     const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
-    const double npart_t = sum_parts ? fin_partials(fin) : 0.0;
+    const double npart_t = sum_parts ? strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
             const double n2 = sum_parts ? block_sum_all(npart_t, wsum) : fastv;
@@ -197,7 +190,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
     // driver detects it and injects a fresh vector (Lanczos::inject)
     auto scale_of = [&](double n2) { return (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0; };
 
-    if (cnt > BLOCK_NNZ) {  // vector mode: single long row
+    if (LONG && cnt > BLOCK_NNZ) {  // vector mode: single long row
         const double scale = scale_of(norm2());
         double s = 0.0;
         const uint32_t cmask = (1u << colbits) - 1u;
@@ -228,7 +221,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
                 if (fin.wpart) fin.wpart[blockIdx.x] = (a * scale) * (a * scale);
             }
         }
-        if (alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
+        if (ALAST && alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
         return;
     }
     // stream mode: every global load of the block is issued before the first
@@ -254,7 +247,13 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         rb0 = t <= nr ? rowptr[r0 + t] - p0 : 0;
         rb1 = (t == 0 && nr == SPMV_THREADS) ? rowptr[r0 + SPMV_THREADS] - p0 : 0;
     }
-    const double fr = (vcol && t < nr) ? f[r0 + t] : 0.0;  // prefetched for the epilogue
+    // lanes per row: largest power of two with nr * L <= 256, capped at one wave
+    int L = SPMV_THREADS / (nr > 0 ? nr : 1);
+    L = L >= 64 ? 64 : L >= 32 ? 32 : L >= 16 ? 16 : L >= 8 ? 8 : L >= 4 ? 4 : L >= 2 ? 2 : 1;
+    const int g = t / L, lane = t % L;
+    // the epilogue runs in each row's first lane (it holds the row's sum): its
+    // f is prefetched now (no LDS hand-off of y and no barrier before it)
+    const double fr = (vcol && g < nr && lane == 0) ? f[r0 + g] : 0.0;
     double xv[PER];
     if (fin.own_hi > fin.own_lo) {  // the halo SpMV: the own slot's entries are summed by the owned-slot SpMV
 #pragma unroll
@@ -276,32 +275,24 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
         if (i < cnt) prod[i] = vv[u] * xv[u];
     }
     __syncthreads();
-    // lanes per row: largest power of two with nr * L <= 256, capped at one wave
-    int L = SPMV_THREADS / (nr > 0 ? nr : 1);
-    L = L >= 64 ? 64 : L >= 32 ? 32 : L >= 16 ? 16 : L >= 8 ? 8 : L >= 4 ? 4 : L >= 2 ? 2 : 1;
-    const int g = t / L, lane = t % L;
     double s = 0.0;
     if (g < nr)
         for (int i = rbeg[g] + lane; i < rbeg[g + 1]; i += L) s += prod[i];
     for (int o = L >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, L);
+    // y, and the basis column + alpha / ||w||^2 terms of row g, in its first lane
+    double av = 0.0, wv = 0.0;
     if (g < nr && lane == 0) {
         const double yr = (fin.ybase ? fin.ybase[r0 + g] + s : s) * scale;
         y[r0 + g] = yr;
-        if (apart) yrow[g] = yr;
-    }
-    // basis column + alpha partial: thread t owns row t (its f was prefetched)
-    if (vcol) {
-        double av = 0.0, wv = 0.0;
-        if (apart) __syncthreads();  // yrow complete
-        if (t < nr) {
+        if (vcol) {
             const double v = fr * scale;
-            vcol[r0 + t] = v;
-            if (fin.v32col) fin.v32col[r0 + t] = float(v);
-            if (apart) {
-                av = v * yrow[t];
-                wv = yrow[t] * yrow[t];
-            }
+            vcol[r0 + g] = v;
+            if (fin.v32col) fin.v32col[r0 + g] = float(v);
+            av = v * yr;
+            wv = yr * yr;
         }
+    }
+    if (vcol) {
         if (apart) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) av += __shfl_xor(av, o, 64);
@@ -316,7 +307,7 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_adaptive(const int4* __re
             if (t == 0 && fin.wpart) fin.wpart[blockIdx.x] = (wsum2[0] + wsum2[1]) + (wsum2[2] + wsum2[3]);
         }
     }
-    if (alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
+    if (ALAST && alpha_out) alpha_handoff(apart, alpha_out, actr, wsum, &s_last);
 }
 
 void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
@@ -334,26 +325,33 @@ void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const dou
     // with events: HIP records the kernel's own start/end timestamps (what
     // rocprofv3 reports), not event packets around it
     // (without events a plain launch: the one a captured HIP graph records)
-#define EK_SPMV_LAUNCH(BN, PK)                                                                                     \
+#define EK_SPMV_LAUNCH_K(KERNEL_)                                                                                  \
     do {                                                                                                           \
         if (ev_start || ev_stop)                                                                                   \
-            hipExtLaunchKernelGGL(k_spmv_adaptive<BN, PK>, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, ev_start,    \
-                                  ev_stop, 0, d, m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv,  \
-                                  alpha_out, actr);                                                                \
+            hipExtLaunchKernelGGL(KERNEL_, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, ev_start, ev_stop, 0, d,       \
+                                  m.rowptr, c, v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);  \
         else                                                                                                       \
-            hipLaunchKernelGGL((k_spmv_adaptive<BN, PK>), dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, d, m.rowptr, c, \
-                               v, m.colbits, m.rel, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);               \
+            hipLaunchKernelGGL(KERNEL_, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, d, m.rowptr, c, v, m.colbits,      \
+                               m.rel, x, y, fn2, f, vcol, apart, fv, alpha_out, actr);                              \
     } while (0)
+#define EK_SPMV_LAUNCH(BN, PK) EK_SPMV_LAUNCH_K((k_spmv_adaptive<BN, PK>))
     if (m.pk) {
-        EK_SPMV_LAUNCH(SPMV_SEG_NNZ, true);
+        if (m.has_long || alpha_out) EK_SPMV_LAUNCH(SPMV_SEG_NNZ, true);
+        else EK_SPMV_LAUNCH_K((k_spmv_adaptive<SPMV_SEG_NNZ, true, false, false>));
     } else {
-        switch (m.block_nnz) {
-            case 512: EK_SPMV_LAUNCH(512, false); break;
-            case 2048: EK_SPMV_LAUNCH(2048, false); break;
-            default: EK_SPMV_LAUNCH(1024, false); break;
+        if (m.block_nnz == SPMV_SEG_NNZ) {
+            if (m.has_long) EK_SPMV_LAUNCH(SPMV_SEG_NNZ, false);
+            else EK_SPMV_LAUNCH_K((k_spmv_adaptive<SPMV_SEG_NNZ, false, false, false>));
+        } else {
+            switch (m.block_nnz) {
+                case 512: EK_SPMV_LAUNCH(512, false); break;
+                case 2048: EK_SPMV_LAUNCH(2048, false); break;
+                default: EK_SPMV_LAUNCH(1024, false); break;
+            }
         }
     }
 #undef EK_SPMV_LAUNCH
+#undef EK_SPMV_LAUNCH_K
 }
 
 }  // namespace dev

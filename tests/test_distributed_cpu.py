@@ -189,7 +189,8 @@ def _halo_worker(rank, world, port, out):
     (setup), then per step ONE exchange of packed messages (here the
     host-staged form: an all-gather of every rank's padded messages, of which
     each rank keeps its pieces) into the compact x whose block q holds q's
-    rows this rank reads and q's ||f||^2 partial."""
+    rows this rank reads, and the ranks' ||f||^2 partials into P (each
+    message is closed by its sender's partial)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -226,7 +227,7 @@ def _halo_worker(rank, world, port, out):
             sidx += list(lall[r, o:o + C[r, rank]]) + [ldv]
         sidx = np.array(sidx, np.int64)
         rcnt = [nrows if q == rank else C[rank, q] for q in range(world)]
-        base = np.concatenate([[0], np.cumsum([c + 1 for c in rcnt])])
+        base = np.concatenate([[0], np.cumsum(rcnt)])
         src = []
         smax = 1
         for q in range(world):
@@ -256,19 +257,21 @@ def _halo_worker(rank, world, port, out):
         sbuf = np.zeros(smax)
         sbuf[:len(sidx)] = f[sidx]                        # k_halo_pack (messages)
         X = np.zeros(base[-1])
-        X[base[rank]: base[rank] + nrows] = f[:nrows]      # ... and the own block
-        X[base[rank] + nrows] = f[ldv]
+        P = np.zeros(world)
+        X[base[rank]: base[rank] + nrows] = f[:nrows]      # ... the own block and partial
+        P[rank] = f[ldv]
         g = ag(sbuf)                                       # the step's one exchange
         for q in range(world):
             if q != rank:
-                X[base[q]: base[q + 1]] = g[q, src[q]: src[q] + rcnt[q] + 1]
+                X[base[q]: base[q + 1]] = g[q, src[q]: src[q] + rcnt[q]]
+                P[q] = g[q, src[q] + rcnt[q]]
         # the same products in the same order: y bit-equal to the slot layout's
         xs = np.zeros(world * S)
         for q in range(world):
             xs[q * S: q * S + off[q + 1] - off[q]] = x0[off[q]: off[q + 1]]
         y_slot = _local_spmv(rp, colx, Sr.val, xs)
         y_halo = _local_spmv(rp, colh, Sr.val, X)
-        parts = [X[base[q + 1] - 1] for q in range(world)]
+        parts = list(P)
         out[rank] = {"same_bits": y_slot.tobytes() == y_halo.tobytes(),
                      "partials": [float(p) for p in parts],
                      "recv": int(sum(rcnt[q] + 1 for q in range(world) if q != rank)),

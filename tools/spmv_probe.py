@@ -52,6 +52,9 @@ def main():
         def no_collective(*_):
             raise RuntimeError("the shard probe runs no collective")
 
+        # (the slot layout: the halo layout's setup all-gathers the other
+        # ranks' requests, which this one-process probe cannot answer)
+        os.environ["EK_MR_HALO"] = "0"
         ctx.comm_init_host(nranks, 0, no_collective, no_collective)
         ctx.spmv_setup_pins(h)
         us = ctx.spmv_bench(200, fused=True)
