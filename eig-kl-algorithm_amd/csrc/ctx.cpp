@@ -2032,7 +2032,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.pro_thresh = o.reorth_thresh > 0 ? o.reorth_thresh : 1e-10;
     L.pro_eps1 = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     // (the in-launch decision and merged update: single context only; the
-    // sharded step all-reduces alpha and ||w||^2 before its k_pro launch)
+    // sharded step all-reduces alpha and ||w||^2 before its k_pro launch.
+    // Their spin-waits assume workgroups are dispatched in index order, which
+    // HIP does not promise: every wait is bounded, the first to give up aborts
+    // the launch's other waiters (kernels_lanczos.hip pro_poll), and the solve
+    // fails with EK_EHIP.  EK_PRO_INLAUNCH=0 runs the step with no in-launch
+    // wait at all.)
     if (const char* e = std::getenv("EK_PRO_INLAUNCH"); L.pro && !c->mr) L.proi = !(e && e[0] == '0');
     if (const char* e = std::getenv("EK_PRO_MERGE"); L.proi) L.pro_merge = !(e && e[0] == '0');
     // column groups walked per projection workgroup: about 850 projection
@@ -2204,6 +2209,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     int mf = m;  // steps the returned Ritz pair is taken from (< m: converged at a mid-cycle check)
     const double beta_eps = std::numeric_limits<double>::epsilon() * std::sqrt(double(n));
     double host_restart_ms = 0.0, device_cycle_ms = 0.0, host_qr_ms = 0.0;  // EK_LANCZOS_TRACE diagnostics
+    double host_ql_ms = 0.0, restart_sync_ms = 0.0;
     auto anorm_of = [&] {
         double a = 1.0;
         for (int i = 0; i < m; ++i) a = std::max(a, std::fabs(d[size_t(i)]) + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0));
@@ -2383,6 +2389,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         device_cycle_ms += std::chrono::duration<double, std::milli>(th - tc).count();
         if (!ek::tridiag_eig(m, d.data(), e.data(), theta.data(), zl.data(), nullptr))
             ek::fail(EK_ENOCONV, "tridiagonal eigensolver failed");
+        host_ql_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
         const double fnorm = std::sqrt(std::max(0.0, fn2_h[size_t(m)]));
         if (!std::isfinite(fnorm)) ek::fail(EK_ENOCONV, "Lanczos breakdown (non-finite residual)");
         nconv = 0;
@@ -2474,7 +2481,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                 HIPCHK(hipMemcpyAsync(c->offd.as<double>() + 1, kp + knew + 1, size_t(knew - 1) * 8,
                                       hipMemcpyHostToDevice, s));
         }
+        const auto tsy = std::chrono::steady_clock::now();
         HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read (and k_pro's staging)
+        restart_sync_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tsy).count();
         if (L.pro && std::getenv("EK_PRO_TRACE")) {  // (lab: the cycle's per-step decisions)
             std::vector<int> fl(static_cast<size_t>(m));
             HIPCHK(hipMemcpy(fl.data(), c->pflags.p, size_t(m) * 4, hipMemcpyDeviceToHost));
@@ -2490,8 +2499,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         host_restart_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th).count();
     }
     if (trace)
-        std::fprintf(stderr, "[lanczos] factorization cycles %.3f ms, restarts %.3f ms (of which QR shifts %.3f ms)\n",
-                     device_cycle_ms, host_restart_ms, host_qr_ms);
+        std::fprintf(stderr, "[lanczos] factorization cycles %.3f ms, restarts %.3f ms (of which QL %.3f ms, QR shifts "
+                     "%.3f ms, waiting for the restart's device work %.3f ms)\n",
+                     device_cycle_ms, host_restart_ms, host_ql_ms, host_qr_ms, restart_sync_ms);
     if (!converged)
         ek::fail(EK_ENOCONV, "Eigenvalue computation failed: %d of %d Ritz pairs converged after %d restarts", nconv,
                  nev, restarts);

@@ -112,6 +112,20 @@ static int sturm_below(int m, const double* d, const double* e2, double x, doubl
 
 bool tridiag_smallest(int m, const double* d, const double* e, int k, double* evals, double* zlast) {
     if (m <= 0 || k <= 0 || k > m) return false;
+    if (k > 1) {
+        // Inverse iteration for two close eigenvalues, without orthogonalising
+        // the vectors against each other (LAPACK dstein does), can converge to
+        // the same vector and report the wrong last component.
+        // Several values are only asked for with nev = 2 (no deflation): the
+        // full QL gives them all, exactly.
+        std::vector<double> ev(static_cast<size_t>(m)), zl(static_cast<size_t>(m));
+        if (!tridiag_eig(m, d, e, ev.data(), zl.data(), nullptr)) return false;
+        for (int j = 0; j < k; ++j) {
+            evals[j] = ev[size_t(j)];
+            zlast[j] = zl[size_t(j)];
+        }
+        return true;
+    }
     std::vector<double> e2(size_t(std::max(m - 1, 1)), 0.0);
     double lo = d[0], hi = d[0], tnorm = 0.0, emax2 = 0.0;
     for (int i = 0; i < m; ++i) {

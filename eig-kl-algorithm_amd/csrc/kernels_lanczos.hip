@@ -354,6 +354,18 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
 
 // PROI: the step's decision is taken in this launch (ek_internal.hpp
 // ProLaunch); a poller's word, 1 + decision (thread 0)
+// Dispatch order: every wait here is on a workgroup with a LOWER index than
+// the waiter (the decider is block 0; the update's blocks follow the whole
+// projection), which relies on workgroups being dispatched in index order.
+// HIP does not promise that; the waits are therefore bounded, and *err (the
+// launch's ProState::timeouts, zero at the start of every solve) doubles as
+// an abort word: the first waiter that gives up counts itself there, and
+// every other waiter of the launch sees it within 256 polls and gives up too,
+// so a broken hand-off costs one bound, not one per workgroup; the host then
+// fails the solve with EK_EHIP (ctx.cpp).
+__device__ __forceinline__ bool pro_aborted(int* err) {
+    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
 __device__ __forceinline__ int pro_poll(const unsigned* pub, int* err) {
     unsigned v = 0u;
     // (bounded: the decider waits on nothing, so this ends in a few us; the
@@ -361,6 +373,7 @@ __device__ __forceinline__ int pro_poll(const unsigned* pub, int* err) {
     for (int it = 0; it < (1 << 22); ++it) {
         v = __hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v != 0u) break;
+        if ((it & 255) == 255 && pro_aborted(err)) break;
         __builtin_amdgcn_s_sleep(8);
     }
     if (v == 0u) atomicAdd(err, 1);  // (the host fails the solve)
@@ -371,6 +384,7 @@ __device__ __forceinline__ int pro_poll(const unsigned* pub, int* err) {
 __device__ __forceinline__ int pro_wait(const unsigned* ctr, unsigned target, int* err) {
     for (int it = 0; it < (1 << 22); ++it) {
         if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return 1;
+        if ((it & 255) == 255 && pro_aborted(err)) break;
         __builtin_amdgcn_s_sleep(4);
     }
     atomicAdd(err, 1);  // (the host fails the solve)
