@@ -605,7 +605,12 @@ def main():
     # steps is kept beside it
     calls_rp, us_rp = kernel_avg_us(prof.get("trace"), "k_spmv")
     us_line = us_rp if us_rp else spmv_us
-    roof = {"bound": "hbm", "kernel": f"k_spmv_adaptive<512,{str(packed).lower()}> (Lanczos CSR SpMV, fp64)",
+    trace = prof.get("trace") or {}
+    spmv_names = sorted((k for k in trace if "k_spmv" in k), key=lambda k: -trace[k][0]) \
+        if "error" not in trace else []
+    kname = spmv_names[0].replace("ek::dev::", "") if spmv_names else \
+        f"k_spmv_adaptive<{'coded' if packed else 'plain'}>"
+    roof = {"bound": "hbm", "kernel": f"{kname} (Lanczos CSR SpMV, fp64)",
             "achieved": round(alg_bytes / us_line / 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg_bytes / us_line / 1e3 / HBM_PEAK_GBS, 4), "traffic": None,
             "bytes_per_launch": int(alg_bytes),
