@@ -2228,6 +2228,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         c->cflag.ensure(size_t(m + 2) * 8);  // (update_mr writes one flag per step)
         if (const char* e = std::getenv("EK_MR_CANCEL"); e && e[0]) L.mr_cancel = std::atof(e);  // (tests)
     }
+    const bool chk_kernel = [] {
+        const char* e = std::getenv("EK_CHK_KERNEL");
+        return !(e && e[0] == '0');
+    }();
     for (;;) {
         HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
         if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));
@@ -2272,12 +2276,17 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                     double* pinned = L.chk_slot(slot);
                     HIPCHK(hipEventRecord(c->chk_done[slot], s));
                     HIPCHK(hipStreamWaitEvent(c->cstream, c->chk_done[slot], 0));
-                    HIPCHK(hipMemcpyAsync(pinned, c->alpha.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
-                    HIPCHK(hipMemcpyAsync(pinned + m, c->offd.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
-                    HIPCHK(hipMemcpyAsync(pinned + 2 * m, c->fn2.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
-                    if (mr_step)
-                        HIPCHK(hipMemcpyAsync(pinned + L.CHK_FLAGS, c->cflag.p, size_t(b) * 8, hipMemcpyDeviceToHost,
-                                              c->cstream));
+                    if (chk_kernel) {  // one launch writing the pinned slot (device-accessible host memory)
+                        ek::dev::chk_gather(c->cstream, c->alpha.as<double>(), c->offd.as<double>(), c->fn2.as<double>(),
+                                            mr_step ? c->cflag.as<double>() : nullptr, b, m, L.CHK_FLAGS, pinned);
+                    } else {  // (EK_CHK_KERNEL=0: one DMA blit per array)
+                        HIPCHK(hipMemcpyAsync(pinned, c->alpha.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                        HIPCHK(hipMemcpyAsync(pinned + m, c->offd.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                        HIPCHK(hipMemcpyAsync(pinned + 2 * m, c->fn2.p, size_t(b) * 8, hipMemcpyDeviceToHost, c->cstream));
+                        if (mr_step)
+                            HIPCHK(hipMemcpyAsync(pinned + L.CHK_FLAGS, c->cflag.p, size_t(b) * 8, hipMemcpyDeviceToHost,
+                                                  c->cstream));
+                    }
                     HIPCHK(hipEventRecord(c->chk_copied[slot], c->cstream));
                     cur = b - 1;  // complete: alpha, offd of steps < b - 1 (the fused finalize lags one step), fn2 <= b - 1
                 }
@@ -2328,9 +2337,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             if (j1 < 0 && jr < 0) {  // the whole cycle ran: its projected matrix and residuals (pinned slot 0:
                            // no check copy is in flight at the cycle's end)
                 double* pin0 = L.chk_slot(0);
-                HIPCHK(hipMemcpyAsync(pin0, c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(pin0 + m, c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(pin0 + 2 * m, c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
+                if (chk_kernel) {
+                    ek::dev::chk_gather(s, c->alpha.as<double>(), c->offd.as<double>(), c->fn2.as<double>(), nullptr, m,
+                                        m, 0, pin0, m + 1);
+                } else {
+                    HIPCHK(hipMemcpyAsync(pin0, c->alpha.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipMemcpyAsync(pin0 + m, c->offd.p, size_t(m) * 8, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipMemcpyAsync(pin0 + 2 * m, c->fn2.p, size_t(m + 1) * 8, hipMemcpyDeviceToHost, s));
+                }
                 HIPCHK(hipStreamSynchronize(s));
                 std::copy(pin0, pin0 + m, alpha_h.begin());
                 std::copy(pin0 + m, pin0 + 2 * m, offd_h.begin());

@@ -428,6 +428,11 @@ struct ProState {
     int timeouts;   // in-launch waits that gave up (PROI; the host fails the solve on any)
     int pad;
 };
+// dst[i], dst[m + i] (, dst[flags_off + i]) = alpha, offd (, flags) [i] for
+// i < b and dst[2m + i] = fn2[i] for i < bf (< 0: b): the mid-cycle check's
+// copy, one launch into pinned host memory
+void chk_gather(hipStream_t s, const double* alpha, const double* offd, const double* fn2, const double* flags, int b,
+                int m, size_t flags_off, double* dst, int bf = -1);
 // out[0..1] = the sums of a[0:n) and b[0:n) (one workgroup; pro_decide's order)
 void sum_pair(hipStream_t s, const double* a, const double* b, int n, double* out);
 void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,

@@ -23,6 +23,28 @@
 namespace ek {
 namespace dev {
 
+// Lab only (EXTRA_DEFS=-DEK_PRO_STAMPS, tools/pro_stamps.py): per workgroup of
+// the projection launch with the in-launch decision, its role and wall-clock
+// stamps (s_memrealtime, 100 MHz) at entry, at its phase marks and at exit,
+// for steps [PRO_STAMP_LO, PRO_STAMP_LO + PRO_STAMP_NS) of the last cycle to
+// reach them; read by ek_lab_pro_stamps.  Compiled out otherwise.
+#ifdef EK_PRO_STAMPS
+constexpr int PRO_STAMP_LO = 20, PRO_STAMP_NS = 80, PRO_STAMP_WG = 2048, PRO_STAMP_W = 6;
+__device__ unsigned long long g_pro_stamps[size_t(PRO_STAMP_NS) * PRO_STAMP_WG * PRO_STAMP_W];
+__device__ __forceinline__ void pro_stamp(int step, int slot, unsigned long long val) {
+    const int k = step - PRO_STAMP_LO;
+    if (threadIdx.x == 0 && k >= 0 && k < PRO_STAMP_NS && int(blockIdx.x) < PRO_STAMP_WG)
+        g_pro_stamps[(size_t(k) * PRO_STAMP_WG + blockIdx.x) * PRO_STAMP_W + slot] = val;
+}
+#define PRO_STAMP(slot) pro_stamp(ncols - 1, (slot), __builtin_amdgcn_s_memrealtime())
+#define PRO_ROLE(r) pro_stamp(ncols - 1, 0, (r))
+#define PRO_DECISION(v) pro_stamp(ncols - 1, 5, (v))
+#else
+#define PRO_STAMP(slot) ((void)0)
+#define PRO_ROLE(r) ((void)0)
+#define PRO_DECISION(v) ((void)0)
+#endif
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -437,18 +459,23 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     // PROI with pl.cgw: ncgl workgroups per row block walk the ncg groups
     const int ncgl = PROI && pl.cgw > 0 ? min(ncg, pl.cgw) : ncg;
     int nwg = int(gridDim.x), orig = int(blockIdx.x);
+    if constexpr (PROI) PRO_STAMP(1);
     if constexpr (PROI) {
         // the decider: the first of 8 extra workgroups ahead of the map (the
         // other seven return; the offset keeps every workgroup's XCD) runs
         // k_pro's body and publishes at once to every XCD's word
         if (orig < 8) {
+            PRO_ROLE(orig == 0 ? 1 : 2);
             if (orig == 0) {
                 const bool d = pro_decide(apart, pl.wpart, nparts, pl.a3, fn2_i, bov_i, pl.alpha, pl.offd, pl.omega,
                                           pl.st, pl.flags, ncols - 1, pl.seg0, pl.m, pl.thresh, pl.eps1);
                 if (t < PRO_PUB)
                     __hip_atomic_store(pl.pub + PRO_PUB_STRIDE * t, d ? 2u : 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                PRO_STAMP(2);
+                PRO_DECISION(d ? 2 : 1);
             }
+            PRO_STAMP(4);
             return;
         }
         orig -= 8;
@@ -461,16 +488,20 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 const int blk = orig - nproj, tot = ncols + has_u0;
                 unsigned* done = pl.pub + PRO_PUB_STRIDE * PRO_PUB;
                 __shared__ int s_ud;
+                PRO_ROLE(5);
                 if (t == 0) s_ud = pro_poll(pl.pub + PRO_PUB_STRIDE * (orig % 8), &pl.st->timeouts);
+                PRO_STAMP(2);
                 __syncthreads();
                 if (s_ud == 1) {  // a skipped step: f = f'; ||f||^2 = ||f'||^2 once the norm is in
                     if (blk == 0) {
                         if (t == 0) {
                             (void)pro_wait(done, 1u, &pl.st->timeouts);
+                            PRO_STAMP(3);
                             if (fn2_fast) *fn2_fast = ld_sc1(h_out + tot);
                         }
                         if (t < 2 && ncols - 1 - t >= 0) h_out[ncols - 1 - t] = 0.0;  // (the finalize's h[i], h[i-1])
                     }
+                    PRO_STAMP(4);
                     return;
                 }
                 UpdTT tt;
@@ -485,6 +516,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 update_body<false, B32U, NT, true>(blk, ldv, V, ncols, has_u0, u0val, nreal, h_out, fp, fp, pl.npart,
                                                    nullptr, nrb, nullptr, pl.V32, pl.fb, fn2_fast, done,
                                                    unsigned(ncg + 1), tt);
+                PRO_STAMP(4);
                 return;
             }
             nwg = nproj;
@@ -506,10 +538,15 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     const int rbk = v / ncgl, j0 = (v % ncgl) * GT_COLS;
     __shared__ int s_dec;
     if constexpr (PROI) {
+        PRO_ROLE(j0 == 0 ? 3 : 4);
         if (j0 != 0) {
             if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd, &pl.st->timeouts);
+            PRO_STAMP(2);
             __syncthreads();
-            if (s_dec == 1) return;
+            if (s_dec == 1) {
+                PRO_STAMP(4);
+                return;
+            }
         }
     }
     // (PROI: the basis tile is loaded after f' is formed, at one place for
@@ -604,8 +641,10 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     if constexpr (PROI) {
         if (j0 == 0) {
             // ||f'||^2 (both outcomes need it): its hand-off before the decision
+            PRO_STAMP(2);
             gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out, MRG ? nullptr : fn2_fast,
                             false, MRG ? pl.pub + PRO_PUB_STRIDE * PRO_PUB : nullptr);
+            PRO_STAMP(3);
             if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd, &pl.st->timeouts);
             __syncthreads();
             skip = s_dec == 1;
@@ -616,7 +655,10 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                         *reinterpret_cast<double2*>(fp + size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t)) = xs[k];
                 }
             }
-            if (skip) return;
+            if (skip) {
+                PRO_STAMP(4);
+                return;
+            }
         }
     }
     if (skip) {
@@ -736,6 +778,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     }
     if (t < GT_SUB + 1) ctr[t * 64] = 0u;  // re-armed for the next launch (visible at the kernel boundary)
     }  // tiles
+    if constexpr (PROI) PRO_STAMP(4);
 }
 
 #define EK_GEMVT_PARAMS                                                                                               \
@@ -1667,6 +1710,30 @@ void pro_step(hipStream_t s, const double* apart, const double* wpart, int npart
                        flags, i, seg0, m, thresh, eps1);
 }
 
+// The mid-cycle convergence check's operands in ONE launch straight into the
+// host's pinned slot (device-accessible host memory): alpha[0:b), offd[0:b),
+// fn2[0:b) (and the sharded step's cancellation flags) at the slot's m-based
+// offsets — instead of one DMA blit per array
+__global__ __launch_bounds__(256) void k_chk_gather(const double* __restrict__ alpha, const double* __restrict__ offd,
+                                                    const double* __restrict__ fn2, const double* __restrict__ flags,
+                                                    int b, int bf, int m, size_t flags_off,
+                                                    double* __restrict__ dst) {
+    for (int i = int(threadIdx.x); i < bf; i += 256) {
+        if (i < b) {
+            dst[i] = alpha[i];
+            dst[m + i] = offd[i];
+            if (flags) dst[flags_off + size_t(i)] = flags[i];
+        }
+        dst[2 * m + i] = fn2[i];
+    }
+}
+
+void chk_gather(hipStream_t s, const double* alpha, const double* offd, const double* fn2, const double* flags, int b,
+                int m, size_t flags_off, double* dst, int bf) {
+    hipLaunchKernelGGL(k_chk_gather, dim3(1), dim3(256), 0, s, alpha, offd, fn2, flags, b, bf < 0 ? b : bf, m,
+                       flags_off, dst);
+}
+
 void sum_pair(hipStream_t s, const double* a, const double* b, int n, double* out) {
     hipLaunchKernelGGL(k_sum_pair, dim3(1), dim3(256), 0, s, a, b, n, out);
 }
@@ -1775,3 +1842,15 @@ void scale_sub_mean(hipStream_t s, int ldv, double* x, int nreal, const double* 
 
 }  // namespace dev
 }  // namespace ek
+
+#ifdef EK_PRO_STAMPS
+// lab (tools/pro_stamps.py): the stamp table, [step - 20][workgroup][6] u64
+extern "C" int ek_lab_pro_stamps(unsigned long long* out, long long count) {
+    const long long cap = (long long)(sizeof(ek::dev::g_pro_stamps) / sizeof(unsigned long long));
+    if (count > cap) count = cap;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(ek::dev::g_pro_stamps), size_t(count) * 8, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? int(count)
+               : -1;
+}
+#endif
