@@ -45,6 +45,16 @@ __device__ __forceinline__ void pro_stamp(int step, int slot, unsigned long long
 #define PRO_DECISION(v) ((void)0)
 #endif
 
+// projection slots of one column-group phase of the in-launch-decision
+// launch: nrb rounded up to the 8 XCDs (gemvt_body's column-group-0-first map)
+#ifndef EK_PRO_CG0_FIRST
+#define EK_PRO_CG0_FIRST 1
+#endif
+#ifndef EK_PRO_NORM_DIRECT  // the merged fp32-shadow form: the norm hand-off writes ||f||^2 for a skipped step
+#define EK_PRO_NORM_DIRECT 1
+#endif
+__host__ __device__ constexpr int pro_slots(int nrb) { return EK_PRO_CG0_FIRST ? (nrb + 7) / 8 * 8 : nrb; }
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -363,6 +373,10 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
         if (t == 0) {
             if (done) {  // (merged: the update in this launch reads it; write-through, then the signal)
                 st_sc1(h_out + tot, a);
+                // (fn2_fast here: ||f||^2 = ||f'||^2 for the next SpMV if the
+                // step skips; a projecting step's update overwrites it after
+                // this signal)
+                if (fn2_fast) st_sc1(fn2_fast, a);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
@@ -483,7 +497,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         if constexpr (MRG) {
             // the update's workgroups, after every projection workgroup (so
             // they wait only on workgroups dispatched before them)
-            const int nproj = nrb * ncgl;
+            const int nproj = pro_slots(nrb) * ncgl;
             if (orig >= nproj) {
                 const int blk = orig - nproj, tot = ncols + has_u0;
                 unsigned* done = pl.pub + PRO_PUB_STRIDE * PRO_PUB;
@@ -494,7 +508,10 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 __syncthreads();
                 if (s_ud == 1) {  // a skipped step: f = f'; ||f||^2 = ||f'||^2 once the norm is in
                     if (blk == 0) {
-                        if (t == 0) {
+                        // (B32U: the norm's hand-off wrote ||f||^2 itself,
+                        // one round trip sooner; the !B32U update writes NaN
+                        // to it at its start, which would race with that)
+                        if (t == 0 && !(B32U && EK_PRO_NORM_DIRECT)) {
                             (void)pro_wait(done, 1u, &pl.st->timeouts);
                             PRO_STAMP(3);
                             if (fn2_fast) *fn2_fast = ld_sc1(h_out + tot);
@@ -522,7 +539,8 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
             nwg = nproj;
         }
     }
-    const int xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+    int xcd = orig % 8;
+    const int q = nwg / 8, rr = nwg % 8;
     // partial reorthogonalisation (k_pro's decision for this step, uniform
     // over the launch): a step that does not project only forms f' and its
     // ||f'||^2 partials (column group 0); the other column groups have no
@@ -534,8 +552,27 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     // f' first.  skip is uniform over the workgroup in every form
     bool skip = !PROI && flag && *flag == 0;
     if (skip && orig >= nrb) return;
-    const int v = skip ? orig * ncgl : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-    const int rbk = v / ncgl, j0 = (v % ncgl) * GT_COLS;
+    int rbk, j0;
+    if (PROI && EK_PRO_CG0_FIRST) {
+        // column group 0 first: its workgroups form f' and ||f'||^2, the
+        // chain a skipped step waits on, so they are dispatched right after
+        // the decider instead of spread over the whole projection (the last
+        // of them entered ~3 us into the launch: tools/pro_stamps.py,
+        // profiles/r05/pro_stamps_*.txt).  Phase p of ncgl holds column group
+        // p of every row block; in each phase XCD x takes the same row blocks
+        // (its contiguous share of nrb), so the tiles of a row block share an
+        // L2 as before.  Slots past an XCD's share are empty.
+        const int P1 = pro_slots(nrb), ph = orig / P1, o = orig % P1, idx = o / 8;
+        xcd = o % 8;
+        const int b8 = nrb / 8, e8 = nrb % 8;
+        if (idx >= b8 + (xcd < e8 ? 1 : 0)) return;
+        rbk = xcd * b8 + min(xcd, e8) + idx;
+        j0 = ph * GT_COLS;
+    } else {
+        const int v = skip ? orig * ncgl : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+        rbk = v / ncgl;
+        j0 = (v % ncgl) * GT_COLS;
+    }
     __shared__ int s_dec;
     if constexpr (PROI) {
         PRO_ROLE(j0 == 0 ? 3 : 4);
@@ -642,8 +679,9 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
         if (j0 == 0) {
             // ||f'||^2 (both outcomes need it): its hand-off before the decision
             PRO_STAMP(2);
-            gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out, MRG ? nullptr : fn2_fast,
-                            false, MRG ? pl.pub + PRO_PUB_STRIDE * PRO_PUB : nullptr);
+            gemvt_skip_tail(ncols, has_u0, nrb, rbk, t, part, nred, gctr + GT_NORM_CTR, h_out,
+                            MRG && !(B32U && EK_PRO_NORM_DIRECT) ? nullptr : fn2_fast, false,
+                            MRG ? pl.pub + PRO_PUB_STRIDE * PRO_PUB : nullptr);
             PRO_STAMP(3);
             if (t == 0) s_dec = pro_poll(pl.pub + PRO_PUB_STRIDE * xcd, &pl.st->timeouts);
             __syncthreads();
@@ -1598,7 +1636,7 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
     const int cols = ncols + has_u0;
     const bool mrg = pl && pl->merged;
     const int ncg = (cols + GT_COLS - 1) / GT_COLS, ncgl = pl && pl->cgw > 0 ? std::min(ncg, pl->cgw) : ncg;
-    const dim3 g(nrb * ncgl + (pl ? 8 : 0) + (mrg ? ldv / UPD_ROWS : 0));
+    const dim3 g((pl && EK_PRO_CG0_FIRST ? pro_slots(nrb) : nrb) * ncgl + (pl ? 8 : 0) + (mrg ? ldv / UPD_ROWS : 0));
     // pl (PROI): the decision in this launch (8 more workgroups); alpha reduced by every
     // workgroup from apart (required) and published to pl->a3
     const ProLaunch pv = pl ? *pl : ProLaunch{};

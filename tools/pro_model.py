@@ -23,8 +23,13 @@ EPS = np.finfo(float).eps
 
 
 def lanczos(A, n, thresh=None, m=100, tol=1e-10, keep_min=20, check=9, seed=1, est_beta=True, trace=False,
-            restart_proj=False):
-    """thresh None: full CGS every step; else partial reorthogonalisation."""
+            restart_proj=False, eta=None):
+    """thresh None: full CGS every step; else partial reorthogonalisation.
+    eta: PROPACK's selective form (compute_int): a triggered step and its
+    pair partner project only against the columns in the intervals around
+    every |omega_j| > thresh where |omega| > eta (u0 when its omega > eta);
+    the rule-forced steps (a run's first, the cycle's last, a lost estimate)
+    against all.  Counts the column passes (cols_projected / cols_full)."""
     u0 = np.full(n, 1.0 / np.sqrt(n))
     rng = np.random.default_rng(seed)
     f = rng.random(n) - 0.5
@@ -43,6 +48,8 @@ def lanczos(A, n, thresh=None, m=100, tol=1e-10, keep_min=20, check=9, seed=1, e
     matvecs = projected = restarts = 0
     ortho = []
     eps1 = EPS * np.sqrt(n)
+    cols_projected = cols_full = 0
+    sel_prev = None  # the interval set of a triggered step, for its pair partner
     while True:
         from_ = k
         conv_j = None
@@ -77,17 +84,64 @@ def lanczos(A, n, thresh=None, m=100, tol=1e-10, keep_min=20, check=9, seed=1, e
                     new[m] = (t + np.copysign(eps1 * anorm_est, t)) / bn
                     new[i] = eps1  # v_{i+1} vs v_i: local rounding
                 forced = force
-                do = force or bn == 0.0 or i == m - 1 or np.max(np.abs(new)) > thresh
+                rule = bn == 0.0 or i == m - 1 or i == from_
+                trig = np.max(np.abs(new)) > thresh
+                do = force or rule or trig
                 force = False
+            sel = None  # None: every column
+            if do and thresh is not None and eta is not None and not rule:
+                if trig:
+                    om = np.abs(new[: i + 1])
+                    sel = np.zeros(i + 1, bool)
+                    for j in np.nonzero(om > thresh)[0]:
+                        lo = j
+                        while lo > 0 and om[lo - 1] > eta:
+                            lo -= 1
+                        hi = j
+                        while hi < i and om[hi + 1] > eta:
+                            hi += 1
+                        sel[lo: hi + 1] = True
+                    sel_u0 = abs(new[m]) > eta
+                    if forced and sel_prev is not None:  # a pair partner also triggered: the union
+                        ps, pu = sel_prev
+                        sel[: len(ps)] |= ps
+                        sel_u0 = sel_u0 or pu
+                    sel = (sel, sel_u0)
+                elif sel_prev is not None:  # the pair partner: the same intervals
+                    ps, pu = sel_prev
+                    s2 = np.zeros(i + 1, bool)
+                    s2[: len(ps)] = ps
+                    sel = (s2, pu)
             if do:
-                B = np.column_stack([V[:, : i + 1], u0])
-                h = B.T @ fp
-                fp = fp - B @ h
-                alpha[i] += h[i]
+                if sel is None:
+                    B = np.column_stack([V[:, : i + 1], u0])
+                    h = B.T @ fp
+                    fp = fp - B @ h
+                    alpha[i] += h[i]
+                    cols_projected += i + 2
+                else:
+                    cs, cu = sel
+                    idx = np.nonzero(cs)[0]
+                    B = np.column_stack([V[:, idx]] + ([u0] if cu else []))
+                    h = B.T @ fp
+                    fp = fp - B @ h
+                    hi_ = dict(zip(idx.tolist(), h[: len(idx)].tolist()))
+                    alpha[i] += hi_.get(i, 0.0)
+                    cols_projected += len(idx) + (1 if cu else 0)
                 projected += 1
                 if thresh is not None:
                     force = not forced  # the next step too (a triggered step starts a pair)
-                    new = np.full(m + 1, eps1)
+                    if sel is None:
+                        new = np.full(m + 1, eps1)
+                        sel_prev = None
+                    else:
+                        cs, cu = sel
+                        new[: i + 1][cs] = eps1
+                        if cu:
+                            new[m] = eps1
+                        new[i] = eps1
+                        sel_prev = sel if not forced else None
+            cols_full += i + 2
             f = fp
             beta[i + 1] = np.linalg.norm(f)
             if thresh is not None:
@@ -152,6 +206,7 @@ def lanczos(A, n, thresh=None, m=100, tol=1e-10, keep_min=20, check=9, seed=1, e
     x /= np.linalg.norm(x)
     lam = th[0]
     return dict(lam=lam, x=x, matvecs=matvecs, projected=projected, restarts=restarts,
+                cols_projected=cols_projected, cols_full=cols_full,
                 ortho_max=max(ortho) if ortho else 0.0, resid=float(np.linalg.norm(A @ x - lam * x)))
 
 
@@ -172,14 +227,22 @@ def main():
     L = h.laplacian()
     n = h.nodes
     A = sp.csr_matrix((L.val, L.col, L.rowptr), shape=(n, n))
-    threshes = [None] + [float(t) for t in sys.argv[2:]] if len(sys.argv) > 2 else [None, np.sqrt(EPS), 1e-9]
+    # thresholds, or thresh:eta for the selective form
+    specs = [None] + sys.argv[2:] if len(sys.argv) > 2 else [None, "1e-10", "1e-10:1.8e-12"]
     ref = None
-    for th in threshes:
-        r = lanczos(A, n, th, trace=True)
+    for spec in specs:
+        th = eta = None
+        if spec is not None:
+            th, *e = spec.split(":")
+            th = float(th)
+            eta = float(e[0]) if e else None
+        r = lanczos(A, n, th, trace=True, eta=eta)
         x = r["x"] * np.sign(r["x"][np.argmax(np.abs(r["x"]))])
         med, bits = ek.median_split(x)
         if ref is None:
             ref = (r["lam"], x, bits)
+        print(f"thresh {spec}: column passes {r['cols_projected']} of {r['cols_full']} "
+              f"({r['cols_projected'] / r['cols_full']:.3f})")
         print(f"thresh {th}: lambda {r['lam']!r} (d {r['lam'] - ref[0]:.2e}), matvecs {r['matvecs']}, projected "
               f"{r['projected']} ({r['projected'] / r['matvecs']:.2f}), restarts {r['restarts']}, max|V^TV-I| "
               f"{r['ortho_max']:.2e}, resid {r['resid']:.2e}, max|dx| {np.abs(x - ref[1]).max():.2e}, split diff "

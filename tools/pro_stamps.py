@@ -24,23 +24,28 @@ spec.loader.exec_module(ek)
 LO, NS, WG, W = 20, 80, 2048, 6
 ROLES = {1: "decider", 2: "decider-slot", 3: "cg0", 4: "cg>0", 5: "update"}
 
-a, sd = (sys.argv[1:3] + ["1.15lcc", "1"][len(sys.argv[1:3]):])[:2]
-lcc = a.endswith("lcc")
-h = ek.Hypergraph.generate(float(a[:-3] if lcc else a), int(sd))
-if lcc:
-    h, _ = h.largest_component()
-c = ek.Context(0)
-c.spmv_setup_pins(h)
-for _ in range(2):
-    lam, v, st = c.lanczos_fiedler()
-print({k: st[k] for k in ("matvecs", "restarts", "projected_steps", "total_ms")}, flush=True)
-fn = ek._lib.ek_lab_pro_stamps
-fn.restype = ctypes.c_int
-fn.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
-buf = np.zeros(NS * WG * W, dtype=np.uint64)
-assert fn(buf.ctypes.data, buf.size) == buf.size
-c.close()
-S = buf.reshape(NS, WG, W).astype(np.int64)
+if sys.argv[1:2] == ["--from"]:
+    S = np.load(sys.argv[2])
+else:
+    a, sd = (sys.argv[1:3] + ["1.15lcc", "1"][len(sys.argv[1:3]):])[:2]
+    lcc = a.endswith("lcc")
+    h = ek.Hypergraph.generate(float(a[:-3] if lcc else a), int(sd))
+    if lcc:
+        h, _ = h.largest_component()
+    c = ek.Context(0)
+    c.spmv_setup_pins(h)
+    for _ in range(2):
+        lam, v, st = c.lanczos_fiedler()
+    print({k: st[k] for k in ("matvecs", "restarts", "projected_steps", "total_ms")}, flush=True)
+    fn = ek._lib.ek_lab_pro_stamps
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    buf = np.zeros(NS * WG * W, dtype=np.uint64)
+    assert fn(buf.ctypes.data, buf.size) == buf.size
+    c.close()
+    S = buf.reshape(NS, WG, W).astype(np.int64)
+if os.environ.get("EK_STAMPS_OUT"):  # the raw table, for offline looks (tools/pro_stamps.py --from FILE)
+    np.save(os.environ["EK_STAMPS_OUT"], S)
 
 rows = {1: [], 2: []}
 for k in range(NS):
@@ -64,6 +69,9 @@ for k in range(NS):
          "dispatch_span": rel(s[:, 1].max()),
          "decider_entry": rel(d[0, 1]), "decider_publish": rel(d[0, 2]),
          "cg0_entry_med": rel(np.median(cg0[:, 1])), "cg0_fprime_med": rel(np.median(cg0[:, 2])),
+         "cg0_entry_max": rel(cg0[:, 1].max()), "cg0_fprime_p90": rel(np.percentile(cg0[:, 2], 90)),
+         "cg0_fprime_max": rel(cg0[:, 2].max()),
+         "cg0_tail_nonlast_med": float(np.median(np.sort(cg0[:, 3] - cg0[:, 2])[:-1])) / 100.0,
          "cg0_norm_handoff_max": rel(cg0[:, 3].max()),
          "cgx_seen_med": rel(np.median(cgx[:, 2])) if len(cgx) else 0.0,
          "upd_entry_med": rel(np.median(up[:, 1])) if len(up) else 0.0,
