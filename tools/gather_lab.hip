@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
     // per workgroup an equal share, bucketed by panel (counting sort), random order inside a bucket
     const long long per = (nnz + G - 1) / G;
     std::vector<unsigned> wA(static_cast<size_t>(nnz)), wB(static_cast<size_t>(nnz));
-    std::vector<long long> stA(size_t(G) * (P + 1)), stB(size_t(G) * (P + 1));
+    std::vector<long long> stA(size_t(G) * (P + 1)), stB(size_t(G) * 2);
     for (int w = 0; w < G; ++w) {
         const long long e0 = std::min(nnz, w * per), e1 = std::min(nnz, (w + 1) * per);
         std::vector<long long> cnt(size_t(P) + 1, 0);
@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
         for (int p = 0; p < P; ++p) cnt[size_t(p) + 1] += cnt[size_t(p)];
         for (int p = 0; p <= P; ++p) {
             stA[size_t(w) * (P + 1) + p] = e0 + cnt[size_t(p)];
-            stB[size_t(w) * (P + 1) + p] = p == 0 ? e0 : e1;  // B: one "panel" holding everything
+            if (p < 2) stB[size_t(w) * 2 + p] = p == 0 ? e0 : e1;  // B: one "panel" holding everything (stride 2)
         }
         std::vector<long long> cur(cnt.begin(), cnt.end() - 1);
         for (long long e = e0; e < e1; ++e) wA[size_t(e0 + cur[size_t(cols[size_t(e)] >> pb)]++)] = cols[size_t(e)];
