@@ -2046,8 +2046,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // then dispatches ~850 + 422 workgroups instead of up to ~3,100 (headline
     // Lanczos 20.4 -> 19.4 ms; ibm10 and ibm01 lost 3-10 % at 3-4 per row
     // block: too few workgroups for the projecting steps;
-    // profiles/r04/cgw/).  EK_PRO_CGW overrides (0: one workgroup per tile)
-    L.pro_cgw = std::max(3, 850 / std::max(1, L.nrb));
+    // profiles/r04/cgw/).  Round 5: with column group 0 dispatched first the
+    // other groups' workgroups cost a skipped step little (they read the
+    // decision and return), so more of them, which a projecting step uses,
+    // pay: at least 8 per row block (headline Lanczos 17.93-18.05 ms at 4,
+    // 17.67-17.72 at 6, 17.53-17.61 at 8, 17.66-17.70 at one per tile;
+    // profiles/r05/pro/cgw_ab*.txt).  EK_PRO_CGW overrides (0: one workgroup
+    // per tile)
+    L.pro_cgw = std::max(8, 850 / std::max(1, L.nrb));
     if (const char* e = std::getenv("EK_PRO_CGW"); e && e[0]) L.pro_cgw = std::atoi(e);
 
     const size_t ldv = size_t(L.ldv);
