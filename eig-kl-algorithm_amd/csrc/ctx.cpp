@@ -1995,15 +1995,20 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // ncv: the reference's min(100, n/2) (cEIG.cpp:195) for the full and CGS2
     // passes.  Under partial reorthogonalisation (reorth 3, the default) a
     // step costs ~ncv only when it projects, and a restart's host QL and QR
-    // shifts cost ~ncv^2 with the GPU idle, so a smaller basis pays: min(80,
+    // shifts cost ~ncv^2 with the GPU idle, so below a million rows, where a
+    // restart weighs most against the steps, a smaller basis pays: min(80,
     // n/2) (round 5, tools/ncv_ab.py, profiles/r05/ncv_ab_r05*.txt: headline
-    // 17.6 -> 16.7 ms, ibm10 38.7 -> 37.7, the 2x LCC 36.8 -> 35.2, ibm01
-    // 7.6 -> 6.9; industry2 9.85 -> 9.5; 64-72 lose on ibm10)
+    // 17.6 -> 16.7 ms, ibm10 38.7 -> 37.7, the 2x LCC 36.8 -> 35.2, the 5x
+    // LCC 54.0 -> 51.2, ibm01 7.6 -> 6.9; 64-72 lose on ibm10).  Above it
+    // the steps dominate and the basis's convergence decides: the 10x
+    // synthetic (disconnected: its null space) took 838 matvecs at 80 against
+    // 394 at 100 (tools/ncv10_lab.py, profiles/r05/ncv10.txt)
     const int ro_dflt = [&] {
         const char* e = std::getenv("EK_REORTH");
         return e && e[0] ? std::atoi(e) : o.reorth;
     }();
-    int m = o.ncv > 0 ? o.ncv : int(std::min<int64_t>(ro_dflt == 3 ? 80 : 100, n / 2));
+    const int ncv_dflt = ro_dflt == 3 && n < 1000000 ? 80 : 100;
+    int m = o.ncv > 0 ? o.ncv : int(std::min<int64_t>(ncv_dflt, n / 2));
     m = int(std::min<int64_t>(m, n - (deflate ? 1 : 0)));
     if (m > ek::dev::MAX_NCV) ek::fail(EK_EINVAL, "ncv %d exceeds %d", m, ek::dev::MAX_NCV);
     if (m <= nev) ek::fail(EK_EINVAL, "graph too small for ncv=%d (n=%lld)", m, (long long)n);

@@ -211,7 +211,8 @@ int ek_spmv_bench(ek_ctx* ctx, int iters, int fused, double* avg_us);
 /* ------------------------------------------------------------------ */
 typedef struct {
     int32_t ncv;        /* <= 0: min(80, n/2) under partial reorthogonalisation
-                           (reorth 3, the default), else min(100, n/2) (cEIG.cpp:195) */
+                           (reorth 3, the default) below 1M rows, else
+                           min(100, n/2) (cEIG.cpp:195) */
     int32_t maxit;      /* restarts; <= 0: 1000 (Spectra default) */
     double tol;         /* <= 0: 1e-10 (Spectra default) */
     int32_t deflate;    /* 1 (default): deflate the constant null vector, nev=1;
