@@ -2003,11 +2003,12 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // the steps dominate and the basis's convergence decides: the 10x
     // synthetic (disconnected: its null space) took 838 matvecs at 80 against
     // 394 at 100 (tools/ncv10_lab.py, profiles/r05/ncv10.txt)
-    const int ro_dflt = [&] {
-        const char* e = std::getenv("EK_REORTH");
-        return e && e[0] ? std::atoi(e) : o.reorth;
-    }();
-    const int ncv_dflt = ro_dflt == 3 && n < 1000000 ? 80 : 100;
+    // reorth 3: partial reorthogonalisation, on the single-context step and
+    // on the sharded one (factorize_mr_pro; the CGS2 step always projects).
+    // EK_REORTH=1|3 overrides (A/B).
+    int reorth_mode = o.reorth;
+    if (const char* e = std::getenv("EK_REORTH"); e && e[0]) reorth_mode = std::atoi(e);
+    const int ncv_dflt = reorth_mode == 3 && n < 1000000 ? 80 : 100;
     int m = o.ncv > 0 ? o.ncv : int(std::min<int64_t>(ncv_dflt, n / 2));
     m = int(std::min<int64_t>(m, n - (deflate ? 1 : 0)));
     if (m > ek::dev::MAX_NCV) ek::fail(EK_EINVAL, "ncv %d exceeds %d", m, ek::dev::MAX_NCV);
@@ -2032,11 +2033,6 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     L.time_spmv = o.time_spmv != 0;
     L.reorth = o.reorth == 2 ? 2 : 1;
     hipStream_t s = c->stream;
-    // reorth 3: partial reorthogonalisation, on the single-context step and
-    // on the sharded one (factorize_mr_pro; the CGS2 step always projects).
-    // EK_REORTH=1|3 overrides (A/B).
-    int reorth_mode = o.reorth;
-    if (const char* e = std::getenv("EK_REORTH"); e && e[0]) reorth_mode = std::atoi(e);
     L.pro = reorth_mode == 3 && L.reorth == 1 && std::getenv("EK_LANCZOS_UNFUSED") == nullptr;
     // threshold 1e-10, not Simon's sqrt(eps): across implicit restarts the
     // kept Ritz block carries the basis's loss of orthogonality into the next
