@@ -105,9 +105,11 @@ int host_threads() {
 
 // The host worker pool behind run_threads / parallel_for: workers are
 // created once and woken per parallel region (spawning 16 threads per region
-// cost ~0.3 ms, several times per solve).  One caller at a time; a second
-// concurrent caller (the KL graph thread beside the solve's thread) gets
-// spawned threads.  Workers run with exceptions unhandled, as std::thread's.
+// cost ~0.3 ms, several times per solve).  Two pools, one caller each: the
+// KL graph thread's regions run beside the solve's thread (its Laplacian
+// build) on the second pool instead of spawning threads for every region; a
+// third concurrent caller gets spawned threads.  Workers run with exceptions
+// unhandled, as std::thread's.
 namespace {
 struct Pool {
     std::mutex run_mu;  // held by the caller of the current region
@@ -137,8 +139,13 @@ struct Pool {
 }  // namespace
 
 void pool_run(int T, void (*fn)(void*, int), void* ctx) {
-    static Pool* P = new Pool;  // never destroyed: workers stay blocked until the process exits
+    static Pool* pools = new Pool[2];  // never destroyed: workers stay blocked until the process exits
+    Pool* P = &pools[0];
     std::unique_lock<std::mutex> rl(P->run_mu, std::try_to_lock);
+    if (!rl.owns_lock()) {
+        P = &pools[1];
+        rl = std::unique_lock<std::mutex>(P->run_mu, std::try_to_lock);
+    }
     if (!rl.owns_lock()) {
         std::vector<std::thread> th;
         th.reserve(size_t(T - 1));
@@ -151,7 +158,7 @@ void pool_run(int T, void (*fn)(void*, int), void* ctx) {
         std::lock_guard<std::mutex> lk(P->mu);
         while (int(P->th.size()) < T - 1) {
             const int w = int(P->th.size()) + 1;
-            P->th.emplace_back([w] { P->loop(w); });
+            P->th.emplace_back([P, w] { P->loop(w); });
             P->th.back().detach();
         }
         P->fn = fn;
