@@ -42,6 +42,13 @@
 #ifndef EK_KL_PREFETCH
 #define EK_KL_PREFETCH 1  // provisional next pair's rows touched into L2 across barrier 2 (0: off, for A/B)
 #endif
+#ifndef EK_KL_NEXT
+// 1: P selects the next pair exactly between the barriers and publishes it;
+// the waves read it after barrier 2 instead of selecting.  Same swap logs,
+// but 2.26 against 1.96 us/swap (profiles/r05/kl/kl_ab_next.txt): P's
+// resolve holds barrier 2 back more than the selection it saves.
+#define EK_KL_NEXT 0
+#endif
 #ifndef EK_E_TWO_TRIPS
 #define EK_E_TWO_TRIPS 1  // early rescans: gains, then the winner's descriptor (0: both in one trip, A/B; 2.03 vs 2.00 us/swap)
 #endif
@@ -327,9 +334,9 @@ size_t kl_loop_lds_bytes(const KLDev& d) {
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
     // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * 2 (early rescans), as carved by the kernel
     constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
-    const size_t b = (nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
-                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP) * 8 +
-                     (2 * nck + KL_ITEM_CAP + 4 + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
+    const size_t b = (nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2 + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
+                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2) * 8 +
+                     (2 * nck + KL_ITEM_CAP + 4 + 4 + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
     return b <= 152 * 1024 ? b : 0;
 }
 
@@ -472,7 +479,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
     KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2][E_PARTS] early-rescan winners
     KLInfo* ab_info = er_info + 2 * E_PARTS;  // [2][KL_AB_CAP] updated rows in node1's / node2's chunk
-    int4* sg_stage = reinterpret_cast<int4*>(ab_info + 2 * KL_AB_CAP);  // [NG][KL_STAGE_ROWS][KL_STAGE_ROW] G1 staging
+    KLInfo* nx_info = ab_info + 2 * KL_AB_CAP;  // [2] the next pair's descriptors, published by P (EK_KL_NEXT)
+    int4* sg_stage = reinterpret_cast<int4*>(nx_info + 2);  // [NG][KL_STAGE_ROWS][KL_STAGE_ROW] G1 staging
     u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * KL_STAGE_ROWS * KL_STAGE_ROW);  // chunk keys (zero-padded to nsel)
     u64* ck1 = ck0 + nsel;
     u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
@@ -480,14 +488,20 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     u64* it_key = ckn1 + d.nck1;           // per updated row: its new key
     u64* er_key = it_key + KL_ITEM_CAP;     // [2][E_PARTS] early-rescan keys
     u64* ab_key = er_key + 2 * E_PARTS;     // [2][KL_AB_CAP] their new keys
-    int* dtag0 = reinterpret_cast<int*>(ab_key + 2 * KL_AB_CAP);  // iteration that tagged a late rescan
+    u64* nx_key = ab_key + 2 * KL_AB_CAP;   // [2] the next pair's keys, published by P
+    int* dtag0 = reinterpret_cast<int*>(nx_key + 2);  // iteration that tagged a late rescan
     int* dtag1 = dtag0 + d.nck0;
     int* ctag0 = dtag1 + d.nck1;  // iteration that claimed it
     int* ctag1 = ctag0 + d.nck0;
     int* it_cs = ctag1 + d.nck1;  // per updated row: list << 31 | chunk (-1: locked)
     int* s_stop = it_cs + KL_ITEM_CAP;  // [4], by iteration parity
-    int* ab_cnt = s_stop + 4;  // [2] (+2 pad): rows appended to ab_* this swap, reset by G2a
-    uint32_t* s_side = reinterpret_cast<uint32_t*>(ab_cnt + 4);
+    // rows appended to ab_* by this swap's G1, per list: [0..1], reset by
+    // G2a after its read.  With EK_KL_NEXT, [2][2] by iteration parity: G2a
+    // (and P) read this swap's pair and G2a zeroes the other, which the next
+    // swap's G1 fills (so P never reads a reset count)
+    int* ab_cnt = s_stop + 4;
+    int* nx_ok = ab_cnt + 4;  // [4]: [0] = 1 when P published the next pair
+    uint32_t* s_side = reinterpret_cast<uint32_t*>(nx_ok + 4);
     uint32_t* s_lock = s_side + words;
     float* s_wd = reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
     if constexpr (SEGC)
@@ -512,6 +526,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     }
     if (tid < 4) s_stop[tid] = tid == 3 ? -1 : 0;
     if (tid < 4) ab_cnt[tid] = 0;
+    if (tid < 4) nx_ok[tid] = 0;  // the first swap selects
     __syncthreads();
     float cut = *d.cut0, best = cut;  // loop-carried scalars: the W wave's lane 0 only
     long long best_it = 0, it = 0;
@@ -566,10 +581,28 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 }
             }
         }
-        // S. selection (cKL.cpp:341-355): lanes 0-31 reduce remain[0]'s keys,
+        // S. selection (cKL.cpp:341-355): the pair P published before barrier
+        // 2 (one LDS round trip), or else lanes 0-31 reduce remain[0]'s keys,
         // 32-63 remain[1]'s; identical in every wave
-        u64 k = 0ull;
-        {
+        u64 k0 = 0ull, k1 = 0ull;
+        v4i dA = v4i{0, 0, 0, 0}, dB = v4i{0, 0, 0, 0};
+        bool sel = true;
+        if constexpr (EK_KL_NEXT) {
+            const int ok = nx_ok[0];
+            const u64 nk0 = nx_key[0], nk1 = nx_key[1];
+            const v4i ni0 = *reinterpret_cast<const v4i*>(nx_info), ni1 = *reinterpret_cast<const v4i*>(nx_info + 1);
+            if (__builtin_amdgcn_readfirstlane(ok)) {
+                sel = false;
+                k0 = readlane_u64(nk0, 0);
+                k1 = readlane_u64(nk1, 0);
+                dA = v4i{__builtin_amdgcn_readfirstlane(ni0.x), __builtin_amdgcn_readfirstlane(ni0.y),
+                         __builtin_amdgcn_readfirstlane(ni0.z), 0};
+                dB = v4i{__builtin_amdgcn_readfirstlane(ni1.x), __builtin_amdgcn_readfirstlane(ni1.y),
+                         __builtin_amdgcn_readfirstlane(ni1.z), 0};
+            }
+        }
+        if (sel) {
+            u64 k = 0ull;
             // 8 keys per lane read together (clamped index: duplicates do not
             // change a max); one read per trip waited for each LDS round trip
             const u64* ck = half ? ck1 : ck0;
@@ -589,13 +622,17 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 }
             }
             k = half_max_u64(k);
+            k0 = readlane_u64(k, 0);
+            k1 = readlane_u64(k, 32);
         }
-        const u64 k0 = readlane_u64(k, 0), k1 = readlane_u64(k, 32);
         if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
         const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
         const int cA = posA / KL_CHUNK, cB = posB / KL_CHUNK;
-        const KLInfo ia = ci0[cA], ib = ci1[cB];
-        const int A = ia.a, pa = ia.b, la = ia.c, B = ib.a, pb = ib.b, lb = ib.c;
+        if (sel) {
+            dA = *reinterpret_cast<const v4i*>(ci0 + cA);
+            dB = *reinterpret_cast<const v4i*>(ci1 + cB);
+        }
+        const int A = dA.x, pa = dA.y, la = dA.z, B = dB.x, pb = dB.y, lb = dB.z;
         if constexpr (PROF && EK_KL_PREFETCH) {  // how often the provisional pair was the pair
             if (wv == W_PF) {
                 pf_hit_a += __builtin_amdgcn_readlane(pf_inf.x, 0) == A && __builtin_amdgcn_readlane(pf_inf.z, 0) > 0;
@@ -617,6 +654,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         auto locked_now = [&](int x) -> bool { return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B; };
         const int tot = la + lb;
         const int tag = int(it);
+        const int abp = EK_KL_NEXT ? (tag & 1) * 2 : 0;  // this swap's short-list counts (ab_cnt)
         if (wv == W_W) {
             // W. w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
             float gA = 0.f, gB = 0.f;
@@ -841,7 +879,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     (s ? d.gp1 : d.gp0)[pp] = g;
                     kn = key_max(s ? -g : g, pp);  // = key_min(g, pp) for list 1, without a branch
                     if (ab) {  // node1's / node2's chunk: resolved by G2a from this short list
-                        const int slot = atomicAdd(&ab_cnt[s], 1);
+                        const int slot = atomicAdd(&ab_cnt[abp + s], 1);
                         if (slot < KL_AB_CAP) {
                             ab_key[s * KL_AB_CAP + slot] = kn;
                             ab_info[s * KL_AB_CAP + slot] = KLInfo{u, rp, len, pp};
@@ -890,13 +928,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
             // (the list entries are read whatever the count, so all of it is one
             // round trip; slots beyond the count hold stale rows and are masked)
-            const int cnt = ab_cnt[s];
+            const int cnt = ab_cnt[abp + s];
             const int hs = hl < KL_AB_CAP ? hl : KL_AB_CAP - 1;
             const u64 bk_raw = ab_key[s * KL_AB_CAP + hs];
             const v4i bf = *reinterpret_cast<const v4i*>(ab_info + s * KL_AB_CAP + hs);
             const bool have = hl < cnt && hl < KL_AB_CAP;
             const u64 bk = have ? bk_raw : 0ull;
-            if (hl == 0) ab_cnt[s] = 0;  // after the read (in order within the wave); G1 appends after barrier 2
+            if (hl == 0) ab_cnt[(EK_KL_NEXT ? 2 - abp : 0) + s] = 0;  // after the read (in order within the wave), or the next swap's pair; G1 appends after barrier 2
             u64 R = rk[0];  // the early rescan's key: the best of its parts
             v4i Rf = rf[0];
 #pragma unroll
@@ -962,7 +1000,99 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             atomicOr(&s_lock[A >> 5], 1u << (A & 31));
             atomicOr(&s_lock[B >> 5], 1u << (B & 31));
         }
-        if constexpr (EK_KL_PREFETCH) {
+        if constexpr (EK_KL_NEXT) {
+            if (wv == W_PF) {
+                // P. the next pair, exactly, from the state G2 is publishing
+                // (beside it): per list the best of
+                //  * the shadow keys of the chunks other than node1's /
+                //    node2's: an untagged chunk's key IS its shadow key (G2b
+                //    copies it), as every raise was merged into it by G1;
+                //  * node1's / node2's chunk resolved as G2a resolves it: the
+                //    early rescan against the updated rows in the chunk.
+                // The winner's descriptor: the updated row holding the winning
+                // key (the one G2b publishes), else the early rescan's winner,
+                // else the chunk table's entry (neither G2a nor G2b writes it
+                // this swap).  A tagged chunk, a stale early rescan, an
+                // overflowing short list or more than 64 updated rows: nothing
+                // published, the waves select after barrier 2.
+                const int s = half, cS = s ? cB : cA, nck = s ? d.nck1 : d.nck0;
+                const u64* ckn = s ? ckn1 : ckn0;
+                u64 k = 0ull;
+                for (int c0 = hl; c0 < nck; c0 += 4 * 32) {
+                    u64 kv[4];  // all four reads in flight, then masked (no per-read branch)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) kv[u] = ckn[min(c0 + 32 * u, nck - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const u64 v = kv[u] & (min(c0 + 32 * u, nck - 1) == cS ? 0ull : ~0ull);
+                        k = v > k ? v : k;
+                    }
+                }
+                // the same round trip: the early rescan's parts, the short
+                // list and its count, the updated rows (lane l: row l)
+                u64 rk[E_PARTS];
+                v4i rf[E_PARTS];
+#pragma unroll
+                for (int q = 0; q < E_PARTS; ++q) {
+                    rk[q] = er_key[s * E_PARTS + q];
+                    rf[q] = *reinterpret_cast<const v4i*>(er_info + s * E_PARTS + q);
+                }
+                const int cnt = ab_cnt[abp + s];
+                const int hs = hl < KL_AB_CAP ? hl : KL_AB_CAP - 1;
+                const u64 bk_raw = ab_key[s * KL_AB_CAP + hs];
+                const v4i bf = *reinterpret_cast<const v4i*>(ab_info + s * KL_AB_CAP + hs);
+                const int il = lane < tot ? lane : 0;
+                const u64 ik = it_key[il];
+                const int ics = it_cs[il];
+                const v4i iinf = *reinterpret_cast<const v4i*>(it_info + il);
+                const bool have = hl < cnt && hl < KL_AB_CAP;
+                const u64 bk = have ? bk_raw : 0ull;
+                u64 R = rk[0];
+                v4i Rf = rf[0];
+#pragma unroll
+                for (int q = 1; q < E_PARTS; ++q) {
+                    const bool b = rk[q] > R;
+                    R = b ? rk[q] : R;
+                    Rf.x = b ? rf[q].x : Rf.x;
+                    Rf.y = b ? rf[q].y : Rf.y;
+                    Rf.z = b ? rf[q].z : Rf.z;
+                    Rf.w = b ? rf[q].w : Rf.w;
+                }
+                const int Rpos = int(~uint32_t(R & 0xffffffffull));
+                const bool stale = have && R != 0ull && bf.w == Rpos && bk < R;
+                const bool bad = any_tag || tot > 64 || __ballot(stale || cnt > KL_AB_CAP) != 0ull;
+                const u64 m = __ballot(cnt > 0) ? half_max_u64(bk) : 0ull;
+                const u64 kS = m > R ? m : R;
+                k = kS > k ? kS : k;
+                k = half_max_u64(k);
+                const u64 kA = readlane_u64(k, 0), kB = readlane_u64(k, 32);
+                // list-1 rows have bit 31 of it_cs set; -1 is a locked row
+                const bool own = lane < tot && ics != -1;
+                const u64 mA = __ballot(own && ics >= 0 && ik == kA), mB = __ballot(own && ics < 0 && ik == kB);
+                const u64 mS = s ? mB : mA;
+                v4i desc = Rf;
+                if (mA) {
+                    const int l = __ffsll((long long)mA) - 1;
+                    const v4i t = v4i{__builtin_amdgcn_readlane(iinf.x, l), __builtin_amdgcn_readlane(iinf.y, l),
+                                      __builtin_amdgcn_readlane(iinf.z, l), 0};
+                    if (!s) desc = t;
+                }
+                if (mB) {
+                    const int l = __ffsll((long long)mB) - 1;
+                    const v4i t = v4i{__builtin_amdgcn_readlane(iinf.x, l), __builtin_amdgcn_readlane(iinf.y, l),
+                                      __builtin_amdgcn_readlane(iinf.z, l), 0};
+                    if (s) desc = t;
+                }
+                if (!mS && k != R && k != 0ull)  // an unchanged chunk's winner
+                    desc = *reinterpret_cast<const v4i*>((s ? ci1 : ci0) + int(~uint32_t(k & 0xffffffffull)) / KL_CHUNK);
+                if (hl == 0) {
+                    nx_key[s] = k;
+                    *reinterpret_cast<v4i*>(nx_info + s) = desc;
+                }
+                if (lane == 0) nx_ok[0] = bad ? 0 : 1;
+                if constexpr (EK_KL_PREFETCH) pf_inf = make_int4(desc.x, desc.y, desc.z, 0);
+            }
+        } else if constexpr (EK_KL_PREFETCH) {
             if (wv == W_PF) {
                 // P. provisional next pair (a prefetch hint, never a result):
                 // per list the best shadow key outside node1's / node2's chunk
