@@ -3004,13 +3004,6 @@ ek::dev::KLDev kl_dev(ek_ctx* c) {
     return d;
 }
 
-int64_t net_cut_of(ek_ctx* c, const uint8_t* side_dev, unsigned long long* cnt_dev, hipStream_t s) {
-    if (!c->kl_nets) return -1;
-    HIPCHK(hipMemsetAsync(cnt_dev, 0, 8, s));
-    ek::dev::net_cut(s, c->kl_nets, c->kl_netptr.as<int64_t>(), c->kl_pins.as<int32_t>(), side_dev, cnt_dev);
-    return 0;
-}
-
 }  // namespace
 
 extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap, ek_kl_result* res) {
@@ -3046,12 +3039,12 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
     // integer net cuts: initial, best prefix, final
     auto* cnt = c->kl_count.as<unsigned long long>();
     const bool nets = c->kl_nets > 0;
-    if (nets) {
-        net_cut_of(c, c->kl_side_init.as<uint8_t>(), cnt + 0, s);
-        net_cut_of(c, c->kl_side.as<uint8_t>(), cnt + 2, s);
+    if (nets) {  // one pass over the pins for all three
         ek::dev::kl_replay(s, int(n), c->kl_side_init.as<uint8_t>(), c->kl_log.as<ek_swap>(), &out->best_iter, dcap,
                            c->kl_sides_tmp.as<uint8_t>());
-        net_cut_of(c, c->kl_sides_tmp.as<uint8_t>(), cnt + 1, s);
+        HIPCHK(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), s));
+        ek::dev::net_cut(s, c->kl_nets, c->kl_netptr.as<int64_t>(), c->kl_pins.as<int32_t>(),
+                         c->kl_side_init.as<uint8_t>(), c->kl_sides_tmp.as<uint8_t>(), c->kl_side.as<uint8_t>(), cnt);
     }
     ek::dev::KLOut ho{};
     unsigned long long hc[3] = {0, 0, 0};

@@ -1389,21 +1389,40 @@ __global__ __launch_bounds__(256) void k_replay_swaps(const ek_swap* __restrict_
     }
 }
 
-// integer hyperedge cut: nets whose pins are not all on one side
+// integer hyperedge cuts of three partitions at once (initial, best prefix,
+// final): nets whose pins are not all on one side.  One thread per net; its
+// pins' ids are loaded four at a time, then their three sides, so a net costs
+// one dependent round trip per four pins instead of per pin
 __global__ __launch_bounds__(256) void k_net_cut(long long nets, const int64_t* __restrict__ net_ptr,
-                                                 const int32_t* __restrict__ pins, const uint8_t* __restrict__ side,
+                                                 const int32_t* __restrict__ pins, const uint8_t* __restrict__ sa,
+                                                 const uint8_t* __restrict__ sb, const uint8_t* __restrict__ sc,
                                                  unsigned long long* __restrict__ count) {
     const long long e = blockIdx.x * 256ll + threadIdx.x;
-    bool cut = false;
+    bool ca = false, cb = false, cc = false;
     if (e < nets) {
         const int64_t p0 = net_ptr[e], p1 = net_ptr[e + 1];
         if (p1 - p0 >= 2) {
-            const uint8_t s0 = side[pins[p0]];
-            for (int64_t p = p0 + 1; p < p1 && !cut; ++p) cut = side[pins[p]] != s0;
+            const int v0 = pins[p0];
+            const uint8_t a0 = sa[v0], b0 = sb[v0], c0 = sc[v0];
+            for (int64_t p = p0 + 1; p < p1 && !(ca && cb && cc); p += 4) {
+                int v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = p + u < p1 ? pins[p + u] : v0;  // past the net: the first pin
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    ca |= sa[v[u]] != a0;
+                    cb |= sb[v[u]] != b0;
+                    cc |= sc[v[u]] != c0;
+                }
+            }
         }
     }
-    const u64 m = __ballot(cut);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+    const u64 ma = __ballot(ca), mb = __ballot(cb), mc = __ballot(cc);
+    if ((threadIdx.x & 63) == 0) {
+        if (ma) atomicAdd(count + 0, (unsigned long long)__popcll(ma));
+        if (mb) atomicAdd(count + 1, (unsigned long long)__popcll(mb));
+        if (mc) atomicAdd(count + 2, (unsigned long long)__popcll(mc));
+    }
 }
 
 __global__ __launch_bounds__(256) void k_build_aux(long long nnz, const int32_t* __restrict__ col,
@@ -1644,11 +1663,11 @@ void kl_replay(hipStream_t s, int n, const uint8_t* side_init, const ek_swap* lo
     hipLaunchKernelGGL(k_replay_swaps, dim3(64), dim3(256), 0, s, log, count, cap, sides_out);
 }
 
-void net_cut(hipStream_t s, int64_t nets, const int64_t* net_ptr, const int32_t* pins, const uint8_t* side,
-             unsigned long long* count) {
+void net_cut(hipStream_t s, int64_t nets, const int64_t* net_ptr, const int32_t* pins, const uint8_t* side_a,
+             const uint8_t* side_b, const uint8_t* side_c, unsigned long long* count) {
     if (nets <= 0) return;
     hipLaunchKernelGGL(k_net_cut, dim3(unsigned((nets + 255) / 256)), dim3(256), 0, s, (long long)nets, net_ptr, pins,
-                       side, count);
+                       side_a, side_b, side_c, count);
 }
 
 
