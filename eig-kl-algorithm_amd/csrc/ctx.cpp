@@ -2818,6 +2818,7 @@ int ek_kl_nets_setup(ek_ctx* c, int64_t nets, const int64_t* net_ptr, const int3
     Uploader up(c, c->kstream, (size_t(nets) + 1) * 8 + size_t(net_ptr[nets]) * 4);
     up.put(c->kl_netptr, net_ptr, size_t(nets) + 1);
     up.put(c->kl_pins, pins, size_t(net_ptr[nets]));
+    c->kl_count.ensure(size_t(3) * size_t(ek::dev::net_cut_blocks(nets)) * sizeof(unsigned));  // ek_kl_run's cut partials
     HIPCHK(hipStreamSynchronize(c->kstream));
     return EK_OK;
     EK_CATCH
@@ -3037,20 +3038,24 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e2, s));
     // integer net cuts: initial, best prefix, final
-    auto* cnt = c->kl_count.as<unsigned long long>();
     const bool nets = c->kl_nets > 0;
-    if (nets) {  // one pass over the pins for all three
+    const int ncb = nets ? ek::dev::net_cut_blocks(c->kl_nets) : 0;
+    std::vector<unsigned> cparts(size_t(3) * size_t(ncb));
+    if (nets) {  // one pass over the pins for all three; per-workgroup counts, added here
         ek::dev::kl_replay(s, int(n), c->kl_side_init.as<uint8_t>(), c->kl_log.as<ek_swap>(), &out->best_iter, dcap,
                            c->kl_sides_tmp.as<uint8_t>());
-        HIPCHK(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), s));
         ek::dev::net_cut(s, c->kl_nets, c->kl_netptr.as<int64_t>(), c->kl_pins.as<int32_t>(),
-                         c->kl_side_init.as<uint8_t>(), c->kl_sides_tmp.as<uint8_t>(), c->kl_side.as<uint8_t>(), cnt);
+                         c->kl_side_init.as<uint8_t>(), c->kl_sides_tmp.as<uint8_t>(), c->kl_side.as<uint8_t>(),
+                         c->kl_count.as<unsigned>());
     }
     ek::dev::KLOut ho{};
-    unsigned long long hc[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(&ho, out, sizeof ho, hipMemcpyDeviceToHost, s));
-    if (nets) HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
+    if (nets)
+        HIPCHK(hipMemcpyAsync(cparts.data(), c->kl_count.p, cparts.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    unsigned long long hc[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k)
+        for (int b = 0; b < ncb; ++b) hc[k] += cparts[size_t(k) * size_t(ncb) + size_t(b)];
     if (log_out && cap > 0) {
         const int64_t k = std::min<int64_t>(cap, ho.iterations);
         if (k) HIPCHK(hipMemcpy(log_out, c->kl_log.p, size_t(k) * sizeof(ek_swap), hipMemcpyDeviceToHost));

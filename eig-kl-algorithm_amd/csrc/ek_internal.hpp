@@ -591,9 +591,11 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
 // sides_out = side_init with the first `count` swaps of `log` applied (count on device: *best or *iters)
 void kl_replay(hipStream_t s, int n, const uint8_t* side_init, const ek_swap* log, const long long* count,
                long long cap, uint8_t* sides_out);
-// count[0..2] += the net cuts of the three sides (counts zeroed by the caller)
+// the net cuts of the three sides as per-workgroup partials: the cut of
+// side k is the sum of part[k * net_cut_blocks(nets) + b] over b
+int net_cut_blocks(int64_t nets);
 void net_cut(hipStream_t s, int64_t nets, const int64_t* net_ptr, const int32_t* pins, const uint8_t* side_a,
-             const uint8_t* side_b, const uint8_t* side_c, unsigned long long* count);
+             const uint8_t* side_b, const uint8_t* side_c, unsigned* part);
 
 }  // namespace dev
 }  // namespace ek
