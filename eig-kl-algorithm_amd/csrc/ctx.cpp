@@ -2250,9 +2250,13 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         const char* e = std::getenv("EK_CHK_KERNEL");
         return !(e && e[0] == '0');
     }();
+    bool cycle_reset = false;  // the restart already queued the resets below
     for (;;) {
-        HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
-        if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));
+        if (!cycle_reset) {
+            HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
+            if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));
+        }
+        cycle_reset = false;
         const auto tc = std::chrono::steady_clock::now();
         int cycle_breakdowns = 0;  // bounded per cycle: each one moves the factorisation forward
         int from = k;
@@ -2491,21 +2495,13 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
         HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
-        const double hk = ee[size_t(knew - 1)];  // H(knew, knew-1)
-        ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>(),
-                         L.b32 ? c->Vn32.as<float>() : nullptr);
-        ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
-                            c->npart.as<double>());
-        L.reduce_scalar(c->fn2.as<double>() + knew);
-        HIPCHK(hipMemcpyAsync(&fn2_k, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
-        std::swap(c->V.p, c->Vn.p);
-        std::swap(c->V.bytes, c->Vn.bytes);
-        if (L.b32) {
-            std::swap(c->V32.p, c->Vn32.p);
-            std::swap(c->V32.bytes, c->Vn32.bytes);
-        }
+        // the restart's small transfers and the next cycle's resets are queued
+        // with the GEMM, all from pinned staging, so the one synchronisation
+        // below waits for the device work alone (as pageable copies between
+        // host wake-ups they left the GPU idle ~40 us a restart)
+        double* kp = c->q_pin + size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1);
+        double* fn2_pin = kp + 2 * (ek::dev::MAX_NCV + 2) - 1;  // (kp uses [0, 2 knew))
         if (L.pro) {  // the kept projected matrix, for k_pro's omega recurrence (alpha[j], offd[j] of j < knew)
-            double* kp = c->q_pin + size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1);
             for (int i = 0; i < knew; ++i) kp[i] = dd[size_t(i)];
             for (int i = 1; i < knew; ++i) kp[knew + i] = ee[size_t(i - 1)];
             HIPCHK(hipMemcpyAsync(c->alpha.p, kp, size_t(knew) * 8, hipMemcpyHostToDevice, s));
@@ -2513,8 +2509,26 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                 HIPCHK(hipMemcpyAsync(c->offd.as<double>() + 1, kp + knew + 1, size_t(knew - 1) * 8,
                                       hipMemcpyHostToDevice, s));
         }
+        const double hk = ee[size_t(knew - 1)];  // H(knew, knew-1)
+        ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>(),
+                         L.b32 ? c->Vn32.as<float>() : nullptr);
+        ek::dev::axpby_norm(s, L.ldv, c->f.as<double>(), sigma, c->Vn.as<double>() + size_t(knew) * ldv, hk,
+                            c->npart.as<double>());
+        L.reduce_scalar(c->fn2.as<double>() + knew);
+        HIPCHK(hipMemcpyAsync(fn2_pin, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
+        // the next cycle's resets (after every read of this cycle's values)
+        HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
+        if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));
+        cycle_reset = true;
+        std::swap(c->V.p, c->Vn.p);
+        std::swap(c->V.bytes, c->Vn.bytes);
+        if (L.b32) {
+            std::swap(c->V32.p, c->Vn32.p);
+            std::swap(c->V32.bytes, c->Vn32.bytes);
+        }
         const auto tsy = std::chrono::steady_clock::now();
         HIPCHK(hipStreamSynchronize(s));  // Q upload buffer reused next restart; fn2_k read (and k_pro's staging)
+        fn2_k = *fn2_pin;
         restart_sync_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tsy).count();
         if (L.pro && std::getenv("EK_PRO_TRACE")) {  // (lab: the cycle's per-step decisions)
             std::vector<int> fl(static_cast<size_t>(m));
