@@ -2493,22 +2493,22 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         double* Q = c->q_pin;  // pinned: the upload below is a plain DMA
         ek::accumulate_q(m, rots, knew + 1, Q, qscratch);
         const double sigma = Q[size_t(knew - 1) * m + size_t(m - 1)];  // Q(m-1, knew-1)
-        HIPCHK(hipMemcpyAsync(c->Qd.p, Q, size_t(m) * size_t(knew + 1) * 8, hipMemcpyHostToDevice, s));
         host_qr_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count();
-        // the restart's small transfers and the next cycle's resets are queued
-        // with the GEMM, all from pinned staging, so the one synchronisation
+        // the restart's transfers and the next cycle's resets are queued with
+        // the GEMM, all through pinned staging, so the one synchronisation
         // below waits for the device work alone (as pageable copies between
-        // host wake-ups they left the GPU idle ~40 us a restart)
+        // host wake-ups they left the GPU idle ~30 us a restart): Q, the kept
+        // projected matrix and the beta-override reset in one launch that
+        // reads the staging directly (three blits and a fill before)
         double* kp = c->q_pin + size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1);
         double* fn2_pin = kp + 2 * (ek::dev::MAX_NCV + 2) - 1;  // (kp uses [0, 2 knew))
         if (L.pro) {  // the kept projected matrix, for k_pro's omega recurrence (alpha[j], offd[j] of j < knew)
             for (int i = 0; i < knew; ++i) kp[i] = dd[size_t(i)];
             for (int i = 1; i < knew; ++i) kp[knew + i] = ee[size_t(i - 1)];
-            HIPCHK(hipMemcpyAsync(c->alpha.p, kp, size_t(knew) * 8, hipMemcpyHostToDevice, s));
-            if (knew > 1)
-                HIPCHK(hipMemcpyAsync(c->offd.as<double>() + 1, kp + knew + 1, size_t(knew - 1) * 8,
-                                      hipMemcpyHostToDevice, s));
         }
+        ek::dev::restart_upload(s, Q, m * (knew + 1), c->Qd.as<double>(), L.pro ? kp : nullptr, knew,
+                                c->alpha.as<double>(), c->offd.as<double>(), c->bov.as<double>(),
+                                int(c->bov.bytes / 8));
         const double hk = ee[size_t(knew - 1)];  // H(knew, knew-1)
         ek::dev::gemm_vq(s, L.ldv, L.V(), m, c->Qd.as<double>(), knew + 1, c->Vn.as<double>(),
                          L.b32 ? c->Vn32.as<float>() : nullptr);
@@ -2516,9 +2516,7 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                             c->npart.as<double>());
         L.reduce_scalar(c->fn2.as<double>() + knew);
         HIPCHK(hipMemcpyAsync(fn2_pin, c->fn2.as<double>() + knew, 8, hipMemcpyDeviceToHost, s));
-        // the next cycle's resets (after every read of this cycle's values)
-        HIPCHK(hipMemsetAsync(c->bov.p, 0xFF, c->bov.bytes, s));  // NaN: no beta override
-        if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));
+        if (mr_step) HIPCHK(hipMemsetAsync(c->cflag.p, 0, c->cflag.bytes, s));  // the next cycle's flags
         cycle_reset = true;
         std::swap(c->V.p, c->Vn.p);
         std::swap(c->V.bytes, c->Vn.bytes);

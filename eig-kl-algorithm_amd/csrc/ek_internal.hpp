@@ -433,6 +433,11 @@ struct ProState {
 // copy, one launch into pinned host memory
 void chk_gather(hipStream_t s, const double* alpha, const double* offd, const double* fn2, const double* flags, int b,
                 int m, size_t flags_off, double* dst, int bf = -1);
+// the implicit restart's uploads from pinned host staging in one launch:
+// qd[0:nq) = q_src, alpha[0:na) = kp[0:na) and offd[1:na) = kp[na+1:2na) when
+// kp != null, bov[0:nbov) = NaN (all-ones bits)
+void restart_upload(hipStream_t s, const double* q_src, int nq, double* qd, const double* kp, int na, double* alpha,
+                    double* offd, double* bov, int nbov);
 // out[0..1] = the sums of a[0:n) and b[0:n) (one workgroup; pro_decide's order)
 void sum_pair(hipStream_t s, const double* a, const double* b, int n, double* out);
 void pro_step(hipStream_t s, const double* apart, const double* wpart, int nparts, double* a3, const double* fn2_i,

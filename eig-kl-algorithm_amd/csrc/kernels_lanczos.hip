@@ -1772,6 +1772,30 @@ void chk_gather(hipStream_t s, const double* alpha, const double* offd, const do
                        flags_off, dst);
 }
 
+// The implicit restart's uploads in ONE launch straight from the host's
+// pinned staging (device-accessible host memory, like k_chk_gather's slot):
+// Q, the kept projected matrix for k_pro's omega recurrence (alpha[0:na) =
+// kp[0:na), offd[1:na) = kp[na+1:2na)) and the next cycle's beta overrides
+// reset (all-ones bits: the NaN hipMemsetAsync(0xFF) wrote) — instead of three
+// DMA blits and a fill, ~4 us each at these sizes
+__global__ __launch_bounds__(256) void k_restart_upload(const double* __restrict__ q_src, int nq, double* __restrict__ qd,
+                                                        const double* __restrict__ kp, int na, double* __restrict__ alpha,
+                                                        double* __restrict__ offd, double* __restrict__ bov, int nbov) {
+    const int t = int(blockIdx.x * 256 + threadIdx.x), stride = int(gridDim.x * 256);
+    for (int i = t; i < nq; i += stride) qd[i] = q_src[i];
+    if (kp) {
+        for (int i = t; i < na; i += stride) alpha[i] = kp[i];
+        for (int i = t + 1; i < na; i += stride) offd[i] = kp[na + i];
+    }
+    for (int i = t; i < nbov; i += stride) bov[i] = __longlong_as_double(-1ll);
+}
+
+void restart_upload(hipStream_t s, const double* q_src, int nq, double* qd, const double* kp, int na, double* alpha,
+                    double* offd, double* bov, int nbov) {
+    const int nb = std::max(1, std::min(32, (std::max(nq, nbov) + 255) / 256));
+    hipLaunchKernelGGL(k_restart_upload, dim3(nb), dim3(256), 0, s, q_src, nq, qd, kp, na, alpha, offd, bov, nbov);
+}
+
 void sum_pair(hipStream_t s, const double* a, const double* b, int n, double* out) {
     hipLaunchKernelGGL(k_sum_pair, dim3(1), dim3(256), 0, s, a, b, n, out);
 }
