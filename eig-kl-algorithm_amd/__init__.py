@@ -40,13 +40,23 @@ SWAP_DTYPE = np.dtype([("iter", "<u4"), ("node_left", "<u4"), ("node_right", "<u
                        ("cut", "<f4"), ("pad", "<u4")])
 
 
-class LanczosOpts(ctypes.Structure):
+class _AbiStruct(ctypes.Structure):
+    """A mirror of an eigkl.h struct (layout ABI_VERSION): refused against a
+    library that cannot state its ABI (an older EK_LIB_PATH lab build)."""
+
+    def __init__(self, *a, **k):
+        if not _ABI_CHECKED:
+            raise RuntimeError(f"{type(self).__name__}: {_lib._name} has no ek_abi_version, its layout is unknown")
+        super().__init__(*a, **k)
+
+
+class LanczosOpts(_AbiStruct):
     _fields_ = [("ncv", _I32), ("maxit", _I32), ("tol", ctypes.c_double), ("deflate", _I32),
                 ("time_spmv", _I32), ("reorth", _I32), ("check_every", _I32), ("basis32", _I32),
                 ("alpha_last", _I32), ("keep_min", _I32), ("reorth_thresh", ctypes.c_double)]
 
 
-class LanczosStats(ctypes.Structure):
+class LanczosStats(_AbiStruct):
     _fields_ = [("restarts", _I32), ("matvecs", _I32), ("converged", _I32), ("residual", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double), ("spmv_timed", _I32),
                 ("comm_ms", ctypes.c_double), ("allgathers", _I32), ("allreduces", _I32),
@@ -54,14 +64,14 @@ class LanczosStats(ctypes.Structure):
                 ("reprojected", _I32), ("ortho_max", ctypes.c_double)]
 
 
-class KLResult(ctypes.Structure):
+class KLResult(_AbiStruct):
     _fields_ = [("iterations", _I64), ("initial_cut", ctypes.c_float), ("best_cut", ctypes.c_float),
                 ("final_cut", ctypes.c_float), ("best_iter", _I64), ("net_cut_initial", _I64),
                 ("net_cut_best", _I64), ("net_cut_final", _I64), ("loop_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double)]
 
 
-class SolveOpts(ctypes.Structure):
+class SolveOpts(_AbiStruct):
     _fields_ = [("eig", _I32), ("seed", ctypes.c_uint32), ("write_results", _I32), ("limit", _I32),
                 ("out_dir", ctypes.c_char_p), ("sign_ref", ctypes.c_char_p), ("lanczos", LanczosOpts)]
 
@@ -70,7 +80,7 @@ _SOLVE_TIMES = ("t_read", "t_laplacian", "t_lanczos", "t_split", "t_kl_graph_wai
                 "t_write", "t_total", "t_spmv_setup")
 
 
-class SolveResult(ctypes.Structure):
+class SolveResult(_AbiStruct):
     _fields_ = ([("nets", _I64), ("nodes", _I64), ("pins", _I64), ("lambda_", ctypes.c_double),
                  ("median", ctypes.c_double), ("lanczos", LanczosStats), ("kl", KLResult)]
                 + [(k, ctypes.c_double) for k in _SOLVE_TIMES])
@@ -99,6 +109,13 @@ ABI_VERSION = 4  # eigkl.h EIGKL_ABI_VERSION: the ctypes struct mirrors below fo
 if _sig("ek_abi_version", ctypes.c_int) is not None:
     if _lib.ek_abi_version() != ABI_VERSION:
         raise ImportError(f"libeigkl_hip ABI {_lib.ek_abi_version()} != the {ABI_VERSION} these bindings mirror: rebuild")
+    _ABI_CHECKED = True
+else:
+    # an EK_LIB_PATH lab build older than the ABI query: its struct layouts are
+    # unknown, so every entry that takes one of the mirrors below refuses
+    import warnings
+    warnings.warn(f"{_lib._name} has no ek_abi_version: calls passing ABI-{ABI_VERSION} structs are refused")
+    _ABI_CHECKED = False
 _sig("ek_hgr_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_P))
 _sig("ek_hgr_generate", ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.POINTER(_P))
 _sig("ek_hgr_from_pins", ctypes.c_int, _I64, _I64, _P, _P, ctypes.POINTER(_P))

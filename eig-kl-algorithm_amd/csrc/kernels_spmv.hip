@@ -340,7 +340,9 @@ void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const dou
         else EK_SPMV_LAUNCH_K((k_spmv_adaptive<SPMV_SEG_NNZ, true, false, false>));
     } else {
         if (m.block_nnz == SPMV_SEG_NNZ) {
-            if (m.has_long) EK_SPMV_LAUNCH(SPMV_SEG_NNZ, false);
+            // the <.., false, false> variant compiles out the ALAST hand-off,
+            // so a caller asking for alpha_out needs the full one
+            if (m.has_long || alpha_out) EK_SPMV_LAUNCH(SPMV_SEG_NNZ, false);
             else EK_SPMV_LAUNCH_K((k_spmv_adaptive<SPMV_SEG_NNZ, false, false, false>));
         } else {
             switch (m.block_nnz) {

@@ -397,7 +397,8 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
 
 
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25", "syn2"])
-@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_ALPHA_LAST=1", "EK_UPD_RED=0", "EK_UPD_RED=1",
+@pytest.mark.parametrize("switch", ["EK_LANCZOS_TT=0", "EK_ALPHA_LAST=1", "plain:EK_ALPHA_LAST=1", "EK_UPD_RED=0",
+                                    "EK_UPD_RED=1",
                                     "EK_UPD_RED=2", "EK_V_NT=1", "pro:EK_UPD_RED=0", "pro:EK_UPD_RED=2",
                                     "pro:EK_V_NT=1", "pro:EK_PRO_INLAUNCH=0", "pro:EK_PRO_MERGE=0",
                                     "pro:EK_PRO_CGW=0", "pro:EK_PRO_CGW=1", "pro:EK_VQ_IB=8",
@@ -426,7 +427,9 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
       fence (EK_CHK_FENCE=0) against the device-scope default.
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses.  These run the full
-    reorthogonalisation (EK_REORTH=1); "pro:" switches hold the partial one
+    reorthogonalisation (EK_REORTH=1); "plain:" runs both sides on the plain
+    CSR SpMV (EK_SPMV_PLAIN=1, whose launcher must keep the alpha hand-off
+    when the caller asks for it); "pro:" switches hold the partial one
     (the default) to the same rule: the skipped steps' paths (the projection's
     norm-only hand-off or its zeroed partials under k_reduce_cols, the
     update's early exit) give the same bits whichever form runs."""
@@ -445,6 +448,9 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
         env["EK_REORTH"] = "3"
     else:
         env["EK_REORTH"] = "1"
+    if switch.startswith("plain:"):
+        switch = switch[6:]
+        env["EK_SPMV_PLAIN"] = "1"
     a, b = str(tmp_path / "new.npy"), str(tmp_path / "old.npy")
     subprocess.run([sys.executable, "-c", code, a], check=True, timeout=180, env=env)
     k, v = switch.split("=")
