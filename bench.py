@@ -450,6 +450,7 @@ def main():
             c10.synchronize()
             barrier()
             tt.append(max_over_ranks(time.time() - t))
+        cs10 = c10.comm_stats()  # the timed solve's collectives (time_spmv on the last one)
         b10 = c10.spmv_bytes(fused=False)
         us10 = 1e3 * st10["spmv_ms"] / max(1, st10["spmv_timed"])
         us10_max = max_over_ranks(us10)
@@ -467,6 +468,23 @@ def main():
                               "recv_MB_per_step_rank0": round(8 * rv10 / 1e6, 3),
                               "send_MB_per_step_rank0": round(8 * sd10 / 1e6, 3)},
                  "projected_steps": st10["projected_steps"]}
+        if world > 1:
+            # per rank, the timed solve's exchange of f and its all-reduces
+            # separately (RCCL: HIP events around each on its stream, waits for
+            # the peers included), the max over ranks; messages per exchange
+            xs = 1e3 * cs10["exchange_ms"] / max(1, cs10["exchanges_timed"])
+            ars = 1e3 * cs10["allreduce_ms"] / max(1, cs10["allreduces_timed"])
+            syn10["collectives"] = {
+                "exchange_us_avg_max_rank": round(max_over_ranks(xs), 2),
+                "allreduce_us_avg_max_rank": round(max_over_ranks(ars), 2),
+                "exchange_ms_per_solve_max_rank": round(max_over_ranks(cs10["exchange_ms"]), 3),
+                "allreduce_ms_per_solve_max_rank": round(max_over_ranks(cs10["allreduce_ms"]), 3),
+                "exchanges_timed": cs10["exchanges_timed"], "allreduces_timed": cs10["allreduces_timed"],
+                "messages_per_exchange_rank0": {
+                    "sends": round(cs10["sends"] / max(1, cs10["exchanges"]), 3),
+                    "recvs": round(cs10["recvs"] / max(1, cs10["exchanges"]), 3)},
+                "timing": ("HIP events around each RCCL collective on its stream" if comm == "rccl" else
+                           "host clock around each host-staged collective")}
         calls10, us10_rp = kernel_avg_us(prof.get("trace10"), "k_spmv")
         if us10_rp:  # the rocprofv3 kernel trace (a child pass before this process touched the GPU)
             syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,

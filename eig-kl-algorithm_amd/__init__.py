@@ -153,6 +153,8 @@ _sig("ek_spmv_bytes", _I64, _P)
 _sig("ek_spmv_dims", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("ek_spmv_format", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64))
 _sig("ek_spmv_exchange", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
+_sig("ek_comm_stats", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64))
 _sig("ek_spmv_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
 _sig("ek_lanczos_fiedler", ctypes.c_int, _P, ctypes.POINTER(LanczosOpts), ctypes.POINTER(ctypes.c_double), _P,
@@ -476,6 +478,18 @@ class Context:
         hl, rv, sd = ctypes.c_int32(0), _I64(0), _I64(0)
         _chk(_lib.ek_spmv_exchange(self._c, ctypes.byref(hl), ctypes.byref(rv), ctypes.byref(sd)), "ek_spmv_exchange")
         return bool(hl.value), int(rv.value), int(sd.value)
+
+    def comm_stats(self):
+        """The sharded solves' exchange accounting since the last setup (ek_comm_stats):
+        exchanges of f, point-to-point messages sent / received, and the last timed
+        (time_spmv) solve's exchange and all-reduce milliseconds with their counts."""
+        e, sd, rv, xt, at = _I64(0), _I64(0), _I64(0), _I64(0), _I64(0)
+        xm, am = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        _chk(_lib.ek_comm_stats(self._c, ctypes.byref(e), ctypes.byref(sd), ctypes.byref(rv), ctypes.byref(xm),
+                                ctypes.byref(xt), ctypes.byref(am), ctypes.byref(at)), "ek_comm_stats")
+        return {"exchanges": int(e.value), "sends": int(sd.value), "recvs": int(rv.value),
+                "exchange_ms": xm.value, "exchanges_timed": int(xt.value), "allreduce_ms": am.value,
+                "allreduces_timed": int(at.value)}
 
     def spmv_bench(self, iters=200, fused=True):
         """Average microseconds per back-to-back SpMV launch on resident buffers."""

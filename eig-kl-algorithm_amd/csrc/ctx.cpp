@@ -22,8 +22,10 @@
 #define HIPCHK(call)                                                                                 \
     do {                                                                                             \
         const hipError_t e_ = (call);                                                                \
-        if (e_ != hipSuccess) ek::fail(EK_EHIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
-                                       __FILE__, __LINE__);                                          \
+        if (e_ != hipSuccess) {                                                                      \
+            (void)hipGetLastError(); /* a failed call leaves no sticky error for the next entry */    \
+            ek::fail(EK_EHIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__); \
+        }                                                                                            \
     } while (0)
 #define NCCLCHK(call)                                                                                 \
     do {                                                                                              \
@@ -131,19 +133,32 @@ struct ek_ctx {
     // The halo exchange of the sharded step (halo_build): instead of every
     // rank's whole slot, each rank receives only the rows of f its columns
     // read, into a compact x: block q (ranks in order) holds the rows of rank
-    // q this rank reads, ascending (its own block: all its rows); the ranks'
-    // ||f||^2 partials land in hx_P[q].  The columns are remapped
+    // q this rank reads, ascending (its own block: all its rows), then q's
+    // ||f||^2 partial at the block end (hx_pidx[q]): one message per peer, the
+    // sender's packed rows closed by its partial.  The columns are remapped
     // monotonically to it, so rows stay sorted and every product is summed in
     // the same order as over the slot layout: the same bits.  Used where it
     // moves fewer bytes than the all-gather (EK_MR_HALO=0/1 forces either).
     bool halo = false;
-    std::vector<int64_t> hx_base;             // nranks + 1: block q at [hx_base[q], hx_base[q+1])
-    std::vector<int64_t> hx_rcnt;             // rows received from q (own: nrows)
+    int halo_calls = 0;  // halo_build calls since the shard map was set (exactly one per setup: it is collective)
+    std::vector<int64_t> hx_base;             // nranks + 1: block q at [hx_base[q], hx_base[q+1]), its partial last
+    std::vector<int64_t> hx_rcnt;             // rows received from q (own: nrows); the block is hx_rcnt[q] + 1
     std::vector<int64_t> hx_scnt, hx_soff;    // rows sent to q, and that message's offset in hx_sbuf (+1: the partial)
     std::vector<int64_t> hx_src;              // host-staged: q's message to this rank inside q's (padded) sbuf
     std::vector<int32_t> hx_gidx_h;           // X[t]'s global row (-1: a partial slot)
     int64_t hx_nsend = 0, hx_smax = 0;
-    DBuf hx_sidx, hx_sbuf, hx_X, hx_P, hx_gidx, hx_gbuf;
+    DBuf hx_sidx, hx_sbuf, hx_X, hx_pidx, hx_gidx, hx_gbuf;
+    // exchange accounting (sharded solves): exchanges, point-to-point
+    // messages posted, and (with timing on) the exchanges' and all-reduces'
+    // durations on the device (HIP events around them on their streams) or,
+    // host-staged, as the host saw them
+    int64_t hx_exchanges = 0, hx_sends = 0, hx_recvs = 0;
+    double x_ms = 0.0, ar_ms = 0.0;
+    int64_t x_timed = 0, ar_timed = 0;
+    bool comm_time = false;
+    std::vector<hipEvent_t> cm_ev;            // event pool, reused across solves
+    std::vector<std::pair<int, int>> cm_rec;  // (kind: 0 exchange, 1 all-reduce; first event) of this solve
+    size_t cm_used = 0;
     // the owned-slot part of a sharded rank's rows (plain CSR, local column
     // ids), summed while the all-gather of the other slots runs on `gstream`
     DBuf own_rowptr, own_col, own_val, own_rb, yown;
@@ -294,11 +309,54 @@ double* stage_for(ek_ctx* c, size_t doubles) {
     return c->stage;
 }
 
-struct CommTimer {  // host-observed time of one collective
+struct CommTimer {  // host-observed time of one collective (kind 0: an exchange of f, 1: an all-reduce)
     ek_ctx* c;
+    int kind;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    ~CommTimer() { c->comm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    ~CommTimer() {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        c->comm_ms += ms;
+        if (!c->comm_time) return;
+        (kind ? c->ar_ms : c->x_ms) += ms;
+        ++(kind ? c->ar_timed : c->x_timed);
+    }
 };
+
+// Device-side timing of the RCCL collectives of a sharded solve (comm_time:
+// the solve's time_spmv): a pair of events from the context's pool around
+// one exchange (kind 0) or all-reduce (kind 1) on its stream.  Their elapsed
+// time holds the wait for the peers, i.e. what the step pays for the
+// collective.  comm_collect sums them once the solve has drained.
+int comm_mark(ek_ctx* c, hipStream_t st) {
+    if (!c->comm_time || !c->comm) return -1;
+    while (c->cm_used + 2 > c->cm_ev.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        c->cm_ev.push_back(e);
+    }
+    const int i = int(c->cm_used);
+    c->cm_used += 2;
+    HIPCHK(hipEventRecord(c->cm_ev[size_t(i)], st));
+    return i;
+}
+
+void comm_done(ek_ctx* c, int i, int kind, hipStream_t st) {
+    if (i < 0) return;
+    HIPCHK(hipEventRecord(c->cm_ev[size_t(i) + 1], st));
+    c->cm_rec.emplace_back(kind, i);
+}
+
+void comm_collect(ek_ctx* c) {
+    for (const auto& r : c->cm_rec) {
+        HIPCHK(hipEventSynchronize(c->cm_ev[size_t(r.second) + 1]));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->cm_ev[size_t(r.second)], c->cm_ev[size_t(r.second) + 1]));
+        (r.first ? c->ar_ms : c->x_ms) += double(ms);
+        ++(r.first ? c->ar_timed : c->x_timed);
+    }
+    c->cm_rec.clear();
+    c->cm_used = 0;
+}
 
 }  // namespace
 
@@ -317,10 +375,12 @@ void allreduce(ek_ctx* c, double* p, size_t count) {
     if (!c->mr || !count) return;
     ++c->n_ar;
     if (c->comm) {
+        const int e = comm_mark(c, c->stream);
         NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, c->comm, c->stream));
+        comm_done(c, e, 1, c->stream);
         return;
     }
-    CommTimer t{c};
+    CommTimer t{c, 1};
     double* h = stage_for(c, count);
     HIPCHK(hipMemcpyAsync(h, p, count * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -335,10 +395,12 @@ void allgather(ek_ctx* c, const double* send, size_t count, double* recv, hipStr
     ++c->n_ag;
     if (!st) st = c->stream;
     if (c->comm) {
+        const int e = comm_mark(c, st);
         NCCLCHK(ncclAllGather(send, recv, count, ncclDouble, c->comm, st));
+        comm_done(c, e, 0, st);
         return;
     }
-    CommTimer t{c};
+    CommTimer t{c, 0};
     const size_t tot = count * size_t(c->nranks);
     double* h = stage_for(c, count + tot);
     HIPCHK(hipMemcpyAsync(h, send, count * 8, hipMemcpyDeviceToHost, st));
@@ -414,6 +476,7 @@ void ek_destroy(ek_ctx* c) {
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto e : c->spmv_ev) (void)hipEventDestroy(e);
+    for (auto e : c->cm_ev) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {
         if (i == 0 && c->fin_ev) (void)hipEventDestroy(c->fin_ev);
         if (c->chk_done[i]) (void)hipEventDestroy(c->chk_done[i]);
@@ -519,6 +582,10 @@ void set_shard(ek_ctx* c, int64_t n, const std::vector<int64_t>& off) {
     }
     c->shard_off = off;
     c->halo = false;
+    c->halo_calls = 0;
+    c->hx_exchanges = c->hx_sends = c->hx_recvs = 0;
+    c->x_ms = c->ar_ms = 0.0;
+    c->x_timed = c->ar_timed = 0;
     c->row0 = off[size_t(c->rank)];
     c->nrows = off[size_t(c->rank) + 1] - c->row0;
     c->nloc = c->mr ? mx : n;
@@ -537,9 +604,13 @@ int64_t x_extent(const ek_ctx* c) { return c->halo ? c->hx_base.back() : c->mr ?
 // The halo layout from this rank's columns in the slot layout (col, host, nnz
 // entries; remapped in place when the halo exchange is taken).  One
 // all-gather of the request counts (every rank then takes the same decision)
-// and one of the request lists: setup only.
+// and one of the request lists: setup only.  Collective: every rank of a
+// sharded context calls it exactly once per setup, after set_shard (the host
+// rows of spmv_setup_rows, or the device build's, whichever the rank took).
 bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
     c->halo = false;
+    if (c->mr && ++c->halo_calls != 1)
+        ek::fail(EK_ESTATE, "halo_build called %d times in one setup (a collective: once per rank)", c->halo_calls);
     if (!c->mr || c->nranks > ek::dev::MAX_HALO_RANKS) return false;
     const char* env = std::getenv("EK_MR_HALO");
     if (env && env[0] == '0') return false;
@@ -621,9 +692,11 @@ bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
     c->hx_nsend = int64_t(sidx.size());
     c->hx_rcnt.assign(size_t(R), 0);
     c->hx_base.assign(size_t(R) + 1, 0);
+    std::vector<int32_t> pidx(static_cast<size_t>(R));
     for (int q = 0; q < R; ++q) {
         c->hx_rcnt[size_t(q)] = q == me ? c->nrows : Cat(me, q);
-        c->hx_base[size_t(q) + 1] = c->hx_base[size_t(q)] + c->hx_rcnt[size_t(q)];
+        pidx[size_t(q)] = int32_t(c->hx_base[size_t(q)] + c->hx_rcnt[size_t(q)]);  // q's partial: the block end
+        c->hx_base[size_t(q) + 1] = c->hx_base[size_t(q)] + c->hx_rcnt[size_t(q)] + 1;
     }
     // host-staged exchange: q's sbuf lists its messages to r = 0, 1, ... (r != q)
     c->hx_src.assign(size_t(R), 0);
@@ -657,9 +730,9 @@ bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
     if (sidx.empty()) sidx.push_back(0);  // (one forced rank: no messages; a valid upload)
     upload(c->hx_sidx, sidx.data(), sidx.size(), c->stream);
     upload(c->hx_gidx, c->hx_gidx_h.data(), c->hx_gidx_h.size(), c->stream);
+    upload(c->hx_pidx, pidx.data(), pidx.size(), c->stream);
     c->hx_sbuf.ensure(size_t(std::max(c->hx_smax, c->hx_nsend)) * 8);
     c->hx_X.ensure(size_t(std::max<int64_t>(c->hx_base.back(), 1)) * 8);
-    c->hx_P.ensure(size_t(R) * 8);
     if (!c->comm) c->hx_gbuf.ensure(size_t(c->hx_smax) * size_t(R) * 8);
     HIPCHK(hipMemsetAsync(c->hx_sbuf.p, 0, c->hx_sbuf.bytes, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -668,33 +741,36 @@ bool halo_build(ek_ctx* c, int32_t* col, int64_t nnz) {
 }
 
 // One halo exchange of src (this rank's rows, its ||f||^2 partial at
-// src[ldv]) into the compact x (c->hx_X) and the ranks' partials (c->hx_P),
-// on stream st: the pack, then RCCL point-to-point messages to and from every
-// peer in one group (the rows, then the partial: each message is closed by
-// it in sbuf), or, staged through the host, an all-gather of every rank's
-// (padded) messages of which this rank keeps its pieces.  Counted as the
-// step's one all-gather.
+// src[ldv]) into the compact x (c->hx_X), on stream st: the pack (each
+// peer's message in sbuf: the rows it reads, closed by this rank's partial;
+// the own block and partial straight into X), then ONE RCCL message to and
+// one from every peer in one group — block q of X is exactly q's message,
+// rows then partial — or, staged through the host, an all-gather of every
+// rank's (padded) messages of which this rank copies its one piece per peer
+// into the same block.  Counted as the step's one all-gather.
 void halo_exchange(ek_ctx* c, const double* src, hipStream_t st) {
     const int R = c->nranks, me = c->rank;
     double* X = c->hx_X.as<double>();
-    double* P = c->hx_P.as<double>();
     double* sb = c->hx_sbuf.as<double>();
-    ek::dev::halo_pack(st, src, int(c->slot - 64), c->hx_sidx.as<int>(), c->hx_nsend, sb, X, c->hx_base[size_t(me)],
-                       c->nrows, P + me);
+    const int64_t bme = c->hx_base[size_t(me)];
+    ek::dev::halo_pack(st, src, int(c->slot - 64), c->hx_sidx.as<int>(), c->hx_nsend, sb, X, bme, c->nrows,
+                       X + bme + c->nrows);
+    ++c->hx_exchanges;
     if (c->comm) {
         ++c->n_ag;
         if (R == 1) return;
+        const int e = comm_mark(c, st);
         NCCLCHK(ncclGroupStart());
         for (int q = 0; q < R; ++q) {
             if (q == me) continue;
             const int64_t sc = c->hx_scnt[size_t(q)], rc = c->hx_rcnt[size_t(q)];
-            double* sq = sb + c->hx_soff[size_t(q)];
-            if (sc) NCCLCHK(ncclSend(sq, size_t(sc), ncclDouble, q, c->comm, st));
-            NCCLCHK(ncclSend(sq + sc, 1, ncclDouble, q, c->comm, st));
-            if (rc) NCCLCHK(ncclRecv(X + c->hx_base[size_t(q)], size_t(rc), ncclDouble, q, c->comm, st));
-            NCCLCHK(ncclRecv(P + q, 1, ncclDouble, q, c->comm, st));
+            NCCLCHK(ncclSend(sb + c->hx_soff[size_t(q)], size_t(sc + 1), ncclDouble, q, c->comm, st));
+            NCCLCHK(ncclRecv(X + c->hx_base[size_t(q)], size_t(rc + 1), ncclDouble, q, c->comm, st));
+            ++c->hx_sends;
+            ++c->hx_recvs;
         }
         NCCLCHK(ncclGroupEnd());
+        comm_done(c, e, 0, st);
         return;
     }
     if (R == 1) {
@@ -703,12 +779,13 @@ void halo_exchange(ek_ctx* c, const double* src, hipStream_t st) {
     }
     double* g = c->hx_gbuf.as<double>();
     allgather(c, sb, size_t(c->hx_smax), g, st);
+    c->hx_sends += R - 1;  // (this rank's messages ride in its all-gather block)
     for (int q = 0; q < R; ++q)
         if (q != me) {
             const double* m = g + size_t(q) * size_t(c->hx_smax) + c->hx_src[size_t(q)];
-            const int64_t rc = c->hx_rcnt[size_t(q)];
-            if (rc) HIPCHK(hipMemcpyAsync(X + c->hx_base[size_t(q)], m, size_t(rc) * 8, hipMemcpyDeviceToDevice, st));
-            HIPCHK(hipMemcpyAsync(P + q, m + rc, 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(X + c->hx_base[size_t(q)], m, size_t(c->hx_rcnt[size_t(q)] + 1) * 8,
+                                  hipMemcpyDeviceToDevice, st));
+            ++c->hx_recvs;
         }
 }
 
@@ -842,8 +919,12 @@ void own_build_dev(ek_ctx* c, hipStream_t s, long long* tiles) {
     own_finish(c, orp);
 }
 
-// ek_spmv_setup's body, the shard map given (no collective: also the
-// device build's host fallback, which one rank may take alone)
+// ek_spmv_setup's body, the shard map given; also the device build's host
+// fallback, which one rank may take alone.  Sharded, it makes halo_build's
+// collectives: a rank that takes the fallback returns before the device
+// path's own halo_build, so every rank still makes exactly one call (checked
+// there).  A rank that fails before that call leaves its peers in the
+// setup's all-gather, as any collective setup does.
 void spmv_setup_rows(ek_ctx* c, int64_t n, const std::vector<int64_t>& off, const int32_t* rowptr, const int32_t* col,
                      const double* val) {
     set_shard(c, n, off);
@@ -1363,6 +1444,21 @@ int ek_spmv_format(ek_ctx* c, int32_t* packed, int64_t* stored_bytes) {
     EK_CATCH
 }
 
+int ek_comm_stats(ek_ctx* c, int64_t* exchanges, int64_t* sends, int64_t* recvs, double* exchange_ms,
+                  int64_t* exchanges_timed, double* allreduce_ms, int64_t* allreduces_timed) {
+    EK_TRY
+    check_ctx(c);
+    if (exchanges) *exchanges = c->hx_exchanges;
+    if (sends) *sends = c->hx_sends;
+    if (recvs) *recvs = c->hx_recvs;
+    if (exchange_ms) *exchange_ms = c->x_ms;
+    if (exchanges_timed) *exchanges_timed = c->x_timed;
+    if (allreduce_ms) *allreduce_ms = c->ar_ms;
+    if (allreduces_timed) *allreduces_timed = c->ar_timed;
+    return EK_OK;
+    EK_CATCH
+}
+
 int ek_spmv_exchange(ek_ctx* c, int32_t* halo, int64_t* recv_doubles, int64_t* send_doubles) {
     EK_TRY
     check_ctx(c);
@@ -1576,7 +1672,8 @@ struct Lanczos {
                 halo_exchange(c, f, s);
             }
             x = c->hx_X.as<double>();
-            fin.npart = c->hx_P.as<double>();
+            fin.npart = x;  // the ranks' partials at their block ends
+            fin.nidx = c->hx_pidx.as<int>();
             fin.nb = c->nranks;
             fin.nstride = 1;
             fin.fn2_out = c->fn2.as<double>() + i;
@@ -1988,6 +2085,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     const auto t0 = std::chrono::steady_clock::now();
     c->comm_ms = 0.0;
     c->n_ag = c->n_ar = 0;
+    c->comm_time = opts && opts->time_spmv && c->mr;
+    c->cm_rec.clear();
+    c->cm_used = 0;
+    if (c->comm_time) c->x_ms = c->ar_ms = 0.0, c->x_timed = c->ar_timed = 0;
     c->fied_n = 0;  // any earlier vector is void once a solve starts; set again only on success
     const int64_t n = c->n;
     const bool deflate = o.deflate != 0;
@@ -2637,6 +2738,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         double rs = 0.0;
         for (int b = 0; b < L.nub; ++b) rs += rpart[b];
         const double r2 = rs * inv * inv;
+        if (c->comm_time) comm_collect(c);
+        c->comm_time = false;
         if (lambda_out) *lambda_out = lambda;
         if (v_out)
             for (int64_t i = 0; i < n; ++i) v_out[i] = v[i] * sgn;
@@ -2694,6 +2797,11 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     ek::dev::fiedler_scale(s, xc, sgn, int(n), c->fied.as<double>());
     HIPCHK(hipGetLastError());
     c->fied_n = n;
+    if (c->comm_time) {
+        HIPCHK(hipStreamSynchronize(s));
+        comm_collect(c);
+    }
+    c->comm_time = false;
     if (lambda_out) *lambda_out = lambda;
     if (v_out)
         for (int64_t i = 0; i < n; ++i) v_out[i] = v[i] * sgn;

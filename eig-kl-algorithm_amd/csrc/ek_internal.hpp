@@ -182,6 +182,9 @@ struct StepFin {
     const double* fn2_i = nullptr;
     const double* bov_i = nullptr;
     int nstride = 1;  // npart[k * nstride], k < nb (the sharded step: each rank's ||f||^2 in its all-gather slot)
+    // the halo layout: rank k's partial at npart[nidx[k]] (its block end in
+    // the compact x, where the peer's one message put it); null: nstride
+    const int* nidx = nullptr;
     // ||f||^2 from the update (||f'||^2 - ||h||^2, k_update B32) when not
     // NaN; NaN: summed from npart
     const double* fast = nullptr;

@@ -48,12 +48,14 @@ constexpr int PER = EK_PANEL_PER;  // entries per thread per chunk
 constexpr int PCH = PER * PT;  // entries per chunk
 
 // thread-strided partial of npart (the adaptive kernel's strided_sum order)
-__device__ __forceinline__ double panel_strided_sum(const double* __restrict__ x, int n, int stride) {
+__device__ __forceinline__ double panel_strided_sum(const double* __restrict__ x, int n, int stride,
+                                                    const int* __restrict__ idx = nullptr) {
     double s = 0.0;
     for (int i0 = threadIdx.x; i0 < n; i0 += 4 * PT) {
         double v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = i0 + u * PT < n ? x[size_t(i0 + u * PT) * size_t(stride)] : 0.0;
+        for (int u = 0; u < 4; ++u)
+            v[u] = i0 + u * PT < n ? x[idx ? size_t(idx[i0 + u * PT]) : size_t(i0 + u * PT) * size_t(stride)] : 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (i0 + u * PT < n) s += v[u];
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
     // or, when that is NaN (a breakdown), the partials, whose loads go out first
     const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
     const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
-    const double npart_t = sum_parts ? panel_strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
+    const double npart_t = sum_parts ? panel_strided_sum(fin.npart, fin.nb, fin.nstride, fin.nidx) : 0.0;
     __syncthreads();
     // The workgroup's chunks, panel by panel (every workgroup walks the panels
     // in the same order).  The next chunk's words and row indices are loaded

@@ -44,13 +44,16 @@ __device__ __forceinline__ void finalize_publish(const StepFin& f, double n2) {
 
 // thread-strided partial of sum(x[0:n)): x[t] + x[t+256] + ... in order (the
 // order of k_finalize_step), loads batched so they are in flight together
-__device__ __forceinline__ double strided_sum(const double* __restrict__ x, int n, int stride) {
+__device__ __forceinline__ double strided_sum(const double* __restrict__ x, int n, int stride,
+                                              const int* __restrict__ idx = nullptr) {
     double s = 0.0;
     for (int i0 = threadIdx.x; i0 < n; i0 += 4 * SPMV_THREADS) {
         double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            v[u] = i0 + u * SPMV_THREADS < n ? x[size_t(i0 + u * SPMV_THREADS) * size_t(stride)] : 0.0;
+            v[u] = i0 + u * SPMV_THREADS < n
+                       ? x[idx ? size_t(idx[i0 + u * SPMV_THREADS]) : size_t(i0 + u * SPMV_THREADS) * size_t(stride)]
+                       : 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             if (i0 + u * SPMV_THREADS < n) s += v[u];
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(SPMV_THREADS, EK_SPMV_WAVES) void k_spmv_adaptive(c
     // only when it is NaN, a breakdown)
     const double fastv = fin.fast ? *fin.fast : __builtin_nan("");
     const bool sum_parts = fin.npart && isnan(fastv);  // (uniform over the workgroup)
-    const double npart_t = sum_parts ? strided_sum(fin.npart, fin.nb, fin.nstride) : 0.0;
+    const double npart_t = sum_parts ? strided_sum(fin.npart, fin.nb, fin.nstride, fin.nidx) : 0.0;
     auto norm2 = [&]() -> double {
         if (fin.npart) {
             const double n2 = sum_parts ? block_sum_all(npart_t, wsum) : fastv;

@@ -195,6 +195,20 @@ int ek_spmv_format(ek_ctx* ctx, int32_t* packed, int64_t* stored_bytes);
  * ||f||^2 partial).  A single context: 0, 0, 0.  No reference counterpart
  * (the reference has no sharded path). */
 int ek_spmv_exchange(ek_ctx* ctx, int32_t* halo, int64_t* recv_doubles, int64_t* send_doubles);
+/* The sharded Lanczos solves' exchange accounting since the last
+ * ek_spmv_setup: exchanges of f (one per Lanczos step) and the point-to-point
+ * messages this rank posted (halo form: ONE send and ONE receive per peer per
+ * exchange, each message the rows the receiver reads closed by the sender's
+ * ||f||^2 partial; host-staged: its pieces of the one all-gather).  With
+ * ek_lanczos_opts::time_spmv set on a solve, that solve's collectives are
+ * also timed: *exchange_ms over *exchanges_timed exchanges of f (RCCL: HIP
+ * events around the send/recv group or all-gather on its stream, waits for
+ * the peers included; host-staged: the host's view of the callback round
+ * trip) and *allreduce_ms over *allreduces_timed all-reduces.  The timings
+ * are reset by ek_spmv_setup and by a timed solve.  Any pointer may be NULL.
+ * No reference counterpart (the reference has no sharded path). */
+int ek_comm_stats(ek_ctx* ctx, int64_t* exchanges, int64_t* sends, int64_t* recvs, double* exchange_ms,
+                  int64_t* exchanges_timed, double* allreduce_ms, int64_t* allreduces_timed);
 /* Back-to-back SpMV launches on context-owned buffers, timed with HIP events
  * around the batch: *avg_us = average per launch (a sharded context: this
  * rank's rows over the all-gather layout, no collective).  fused = 2: also the

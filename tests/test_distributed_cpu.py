@@ -188,9 +188,9 @@ def _halo_worker(rank, world, port, out):
     slot-layout columns, one all-gather of the counts and one of the lists
     (setup), then per step ONE exchange of packed messages (here the
     host-staged form: an all-gather of every rank's padded messages, of which
-    each rank keeps its pieces) into the compact x whose block q holds q's
-    rows this rank reads, and the ranks' ||f||^2 partials into P (each
-    message is closed by its sender's partial)."""
+    each rank copies its one piece per peer) into the compact x whose block q
+    is q's message as sent: the rows of q this rank reads, then q's ||f||^2
+    partial at the block end (RCCL: one ncclSend / ncclRecv per peer)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -227,7 +227,8 @@ def _halo_worker(rank, world, port, out):
             sidx += list(lall[r, o:o + C[r, rank]]) + [ldv]
         sidx = np.array(sidx, np.int64)
         rcnt = [nrows if q == rank else C[rank, q] for q in range(world)]
-        base = np.concatenate([[0], np.cumsum(rcnt)])
+        base = np.concatenate([[0], np.cumsum(np.array(rcnt) + 1)])  # each block: rows, then the partial
+        pidx = base[:-1] + np.array(rcnt)
         src = []
         smax = 1
         for q in range(world):
@@ -257,14 +258,15 @@ def _halo_worker(rank, world, port, out):
         sbuf = np.zeros(smax)
         sbuf[:len(sidx)] = f[sidx]                        # k_halo_pack (messages)
         X = np.zeros(base[-1])
-        P = np.zeros(world)
         X[base[rank]: base[rank] + nrows] = f[:nrows]      # ... the own block and partial
-        P[rank] = f[ldv]
+        X[pidx[rank]] = f[ldv]
         g = ag(sbuf)                                       # the step's one exchange
+        pieces = 0
         for q in range(world):
-            if q != rank:
-                X[base[q]: base[q + 1]] = g[q, src[q]: src[q] + rcnt[q]]
-                P[q] = g[q, src[q] + rcnt[q]]
+            if q != rank:                                  # one piece per peer: rows + partial
+                X[base[q]: base[q + 1]] = g[q, src[q]: src[q] + rcnt[q] + 1]
+                pieces += 1
+        P = X[pidx]                                        # the SpMV prologue reads them at the block ends
         # the same products in the same order: y bit-equal to the slot layout's
         xs = np.zeros(world * S)
         for q in range(world):
@@ -273,7 +275,8 @@ def _halo_worker(rank, world, port, out):
         y_halo = _local_spmv(rp, colh, Sr.val, X)
         parts = list(P)
         out[rank] = {"same_bits": y_slot.tobytes() == y_halo.tobytes(),
-                     "partials": [float(p) for p in parts],
+                     "partials": [float(p) for p in parts], "pieces": pieces,
+                     "own_partial": float(f[ldv]),
                      "recv": int(sum(rcnt[q] + 1 for q in range(world) if q != rank)),
                      "recv_full": int((world - 1) * S)}
     finally:
@@ -292,4 +295,6 @@ def test_halo_exchange_layout(world):
     for r in range(world):
         assert out[r]["same_bits"], out[r]
         assert out[r]["partials"] == out[0]["partials"]
+        assert out[r]["partials"][r] == out[r]["own_partial"]
+        assert out[r]["pieces"] == world - 1  # one message from every peer
         assert out[r]["recv"] <= out[r]["recv_full"]

@@ -127,13 +127,21 @@ def _worker(rank, port, tmp, out):
                     ctx.spmv_setup(n, row0, S.rowptr, S.col, S.val)
                     c0 = dict(counts)
                     lam_h, v_h, st_h = ctx.lanczos_fiedler()
+                    ag = counts["allgather"] - c0["allgather"]
+                    cs = ctx.comm_stats()  # (before spmv_host: its exchange is not a step's)
+                    # the same solve with its collectives timed (exchange and all-reduce separately)
+                    _, _, st_t = ctx.lanczos_fiedler(time_spmv=True)
+                    ct = ctx.comm_stats()
                     hb[mode] = dict(lam=lam_h, v=v_h.tobytes(), ex=ctx.spmv_exchange(), matvecs=st_h["matvecs"],
-                                    ag=counts["allgather"] - c0["allgather"], y=ctx.spmv_host(x).tobytes())
+                                    ag=ag, y=ctx.spmv_host(x).tobytes(),
+                                    comm=cs, comm_t=ct, st_t={k: st_t[k] for k in ("matvecs", "allgathers",
+                                                                                   "allreduces")})
                 finally:
                     del os.environ["EK_MR_HALO"]
             r["halo"] = {"same_bits": hb["1"]["lam"] == hb["0"]["lam"] and hb["1"]["v"] == hb["0"]["v"],
                          "spmv_same": hb["1"]["y"] == hb["0"]["y"], "ex1": hb["1"]["ex"], "ex0": hb["0"]["ex"],
-                         "ag": hb["1"]["ag"], "matvecs": hb["1"]["matvecs"]}
+                         "ag": hb["1"]["ag"], "matvecs": hb["1"]["matvecs"], "comm": hb["1"]["comm"],
+                         "comm_t": hb["1"]["comm_t"], "st_t": hb["1"]["st_t"], "comm_gather": hb["0"]["comm"]}
             res[name] = r
         # the whole file path, sharded: rank 0 writes the results file
         rr, _ = ctx.solve_file(circuit_path("ibm01"), eig=1, out_dir=os.path.join(tmp, f"r{rank}"))
@@ -197,6 +205,18 @@ def test_two_rank_sharded_lanczos_through_comm_seam(tmp_path):
             assert hl["same_bits"] and hl["spmv_same"], hl
             assert hl["ex1"][0] and not hl["ex0"][0] and hl["ex1"][1] <= hl["ex0"][1], hl
             assert hl["ag"] == hl["matvecs"] + 1, hl  # (one exchange a step + the final vector's all-gather)
+            # ONE message to and ONE from every peer per exchange, one exchange a step
+            # (the partial rides at the end of the rows: the block-end layout)
+            cm = hl["comm"]
+            assert cm["exchanges"] == hl["matvecs"], hl
+            assert cm["sends"] == cm["recvs"] == (WORLD - 1) * cm["exchanges"], hl
+            assert hl["comm_gather"]["exchanges"] == 0 and hl["comm_gather"]["sends"] == 0, hl
+            assert hl["comm"]["exchanges_timed"] == 0, hl  # (untimed solve: nothing timed since the setup)
+            # the timed solve: every all-gather (the steps' exchanges + the final
+            # vector's) and every all-reduce timed, each kind on its own
+            ct, stt = hl["comm_t"], hl["st_t"]
+            assert ct["exchanges_timed"] == stt["allgathers"] and ct["allreduces_timed"] == stt["allreduces"], hl
+            assert ct["exchange_ms"] > 0 and ct["allreduce_ms"] > 0, hl
     assert r1["ibm01"]["row0"] > 0 and r0["ibm01"]["nrows"] + r1["ibm01"]["nrows"] == 12752
     assert r0["industry2"]["nrows"] != r1["industry2"]["nrows"]  # nnz-balanced: unequal slices
     # every rank holds the same full vector: identical Ritz pairs
@@ -310,6 +330,7 @@ def test_rccl_one_rank_production_path(ek, monkeypatch, name, reorth):
     h = ek.Hypergraph.read(circuit_path(name))
     L = h.laplacian()
     out = {}
+    timed = {}
     for mode in ("rccl", "host"):
         c = ek.Context(0)
         try:
@@ -319,8 +340,16 @@ def test_rccl_one_rank_production_path(ek, monkeypatch, name, reorth):
                 c.comm_init_host(1, 0, lambda x: x.copy(), lambda x: None)
             c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
             out[mode] = c.lanczos_fiedler(reorth=reorth)
+            # the same solve with its collectives timed: RCCL by HIP events on
+            # the stream, host-staged by the host's clock; the same bits
+            lam_t, v_t, st_t = c.lanczos_fiedler(reorth=reorth, time_spmv=True)
+            timed[mode] = (c.comm_stats(), st_t, lam_t == out[mode][0] and v_t.tobytes() == out[mode][1].tobytes())
         finally:
             c.close()
+    for mode, (cs, st_t, same) in timed.items():
+        assert same, mode
+        assert cs["exchanges_timed"] == st_t["allgathers"] and cs["allreduces_timed"] == st_t["allreduces"], (mode, cs)
+        assert cs["exchange_ms"] > 0 and cs["allreduce_ms"] > 0, (mode, cs)
     # the same path without the owned-slot / halo split of the SpMV (one SpMV
     # after the all-gather): other rounding, the same pair within tolerance
     monkeypatch.setenv("EK_MR_OVERLAP", "0")
@@ -339,8 +368,14 @@ def test_rccl_one_rank_production_path(ek, monkeypatch, name, reorth):
     try:
         c.comm_init(1, 0, ek.comm_unique_id())
         c.spmv_setup(h.nodes, 0, L.rowptr, L.col, L.val)
+        # the zero-row halo of one rank (the r05c failure):
+        # no peer, so no message and an empty send list; the pack launch packs
+        # zero message rows (the own block and partial only), and every step's
+        # exchange posts nothing
         assert c.spmv_exchange() == (True, 0, 0)
         lam_x, v_x, st_x = c.lanczos_fiedler(reorth=reorth)
+        cs_x = c.comm_stats()
+        assert cs_x["exchanges"] == st_x["matvecs"] and cs_x["sends"] == cs_x["recvs"] == 0, cs_x
     finally:
         c.close()
     (lam, v, st), (lam_h, v_h, st_h) = out["rccl"], out["host"]
