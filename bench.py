@@ -378,6 +378,11 @@ def main():
     if rank == 0:
         parity = headline_parity(ctx, path, out_dir, n, last, lcc and args.mult == 1.15 and args.seed == 1)
         log(f"parity: {parity}")
+    # the gather-only ceiling of the step's own SpMV (same grid, matrix stream
+    # and x gathers, nothing else; ek_spmv_gather_bench), and the product
+    # kernel back to back on the same matrix, for the roofline's reading
+    ceil_us = ctx.spmv_gather_bench(200)
+    prod_bb_us = ctx.spmv_bench(200, fused=False)
     lz = [r[0]["lanczos"] for r in results]
     spmv_timed = ev_step[0]["lanczos"]["spmv_timed"]
     spmv_us = 1e3 * ev_step[0]["lanczos"]["spmv_ms"] / max(1, spmv_timed)
@@ -451,6 +456,7 @@ def main():
             barrier()
             tt.append(max_over_ranks(time.time() - t))
         cs10 = c10.comm_stats()  # the timed solve's collectives (time_spmv on the last one)
+        ceil10_us = c10.spmv_gather_bench(100)
         b10 = c10.spmv_bytes(fused=False)
         us10 = 1e3 * st10["spmv_ms"] / max(1, st10["spmv_timed"])
         us10_max = max_over_ranks(us10)
@@ -467,7 +473,11 @@ def main():
                                        "all-gather of whole slots") if world > 1 else None,
                               "recv_MB_per_step_rank0": round(8 * rv10 / 1e6, 3),
                               "send_MB_per_step_rank0": round(8 * sd10 / 1e6, 3)},
-                 "projected_steps": st10["projected_steps"]}
+                 "projected_steps": st10["projected_steps"],
+                 "ceiling": {"gather_only_us_max_rank": round(max_over_ranks(ceil10_us), 3),
+                             "ceiling_frac_per_gpu": round(b10 / max_over_ranks(ceil10_us) / 1e3 / HBM_PEAK_GBS, 4),
+                             "what": "ek_spmv_gather_bench: the SpMV's grid, matrix stream and x / value gathers "
+                                     "with nothing else, back to back"}}
         if world > 1:
             # per rank, the timed solve's exchange of f and its all-reduces
             # separately (RCCL: HIP events around each on its stream, waits for
@@ -490,6 +500,7 @@ def main():
             syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,
                                 "achieved_GBps": round(b10 / us10_rp / 1e3, 1),
                                 "frac": round(b10 / us10_rp / 1e3 / HBM_PEAK_GBS, 4),
+                                "frac_of_ceiling": round(max_over_ranks(ceil10_us) / us10_rp, 4),
                                 "what": ("the resident 1-rank solve" if world == 1 else
                                          f"rank 0's shard of the {world}-rank map, 200 back-to-back fused launches "
                                          "(tools/spmv_probe.py shard)")}
@@ -643,6 +654,14 @@ def main():
                        "what": "HIP kernel start/end timestamps of every 4th SpMV of each Lanczos cycle of one "
                                "untimed step after the timed ones (eager launches: events are not graph nodes); the "
                                "start marker precedes the dispatch, so this also holds the ~1.5 us kernel boundary"},
+            "ceiling_frac": round(alg_bytes / ceil_us / 1e3 / HBM_PEAK_GBS, 4),
+            "frac_of_ceiling": round(ceil_us / us_line, 4),
+            "ceiling": {"gather_only_us": round(ceil_us, 3), "product_back_to_back_us": round(prod_bb_us, 3),
+                        "back_to_back_frac": round(alg_bytes / prod_bb_us / 1e3 / HBM_PEAK_GBS, 4),
+                        "what": ("ceiling_frac = bytes_per_launch / the gather-only kernel's time / peak: "
+                                 "ek_spmv_gather_bench runs this SpMV's grid over the same matrix words and makes the "
+                                 "same x and value-table gathers, summing in registers (no row reduction, no y, no "
+                                 "epilogue), 200 launches back to back; frac_of_ceiling = frac / ceiling_frac")},
             "fused_bytes_per_launch": int(fused_bytes),
             "fused_frac": round(fused_bytes / us_line / 1e3 / HBM_PEAK_GBS, 4),
             "stored_bytes_per_launch": int(stored),
@@ -670,6 +689,14 @@ def main():
         "metric": "wall-clock to final cut (s) + cut size, ibm18.hgr; SpMV GB/s vs HBM peak",
         "value": round(sec_per_step, 6),
         "unit": "s",
+        "value_is": ("the warm-context step: one in-process .hgr file -> results file solve (ek_solve_file) with the "
+                     "GPU context up, as a service runs it; e2e_s is the metric as SURVEY §8d states it"),
+        "e2e_s": fresh,
+        "e2e_is": ("process start -> results written: `gKL2 <headline .hgr> -EIG` spawned fresh (HIP start-up, library "
+                   "load, parse, solve, write), median of 5 (e2e_fresh_breakdown)"),
+        "cut": last["kl"]["net_cut_best"],
+        "cut_is": ("integer net cut of the best KL prefix (nets with pins on both sides), cKL.cpp:392-403's split; "
+                   "the fp32 running cut is result.best_cut"),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

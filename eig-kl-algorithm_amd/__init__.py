@@ -155,6 +155,7 @@ _sig("ek_spmv_format", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.
 _sig("ek_spmv_exchange", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("ek_comm_stats", ctypes.c_int, _P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64))
+_sig("ek_spmv_gather_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_spmv_bench", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
 _sig("ek_lanczos_default_opts", None, ctypes.POINTER(LanczosOpts))
 _sig("ek_lanczos_fiedler", ctypes.c_int, _P, ctypes.POINTER(LanczosOpts), ctypes.POINTER(ctypes.c_double), _P,
@@ -490,6 +491,12 @@ class Context:
         return {"exchanges": int(e.value), "sends": int(sd.value), "recvs": int(rv.value),
                 "exchange_ms": xm.value, "exchanges_timed": int(xt.value), "allreduce_ms": am.value,
                 "allreduces_timed": int(at.value)}
+
+    def spmv_gather_bench(self, iters=200):
+        """Average microseconds per launch of the SpMV's gather-only ceiling kernel (ek_spmv_gather_bench)."""
+        us = ctypes.c_double()
+        _chk(_lib.ek_spmv_gather_bench(self._c, int(iters), ctypes.byref(us)), "spmv_gather_bench")
+        return us.value
 
     def spmv_bench(self, iters=200, fused=True):
         """Average microseconds per back-to-back SpMV launch on resident buffers."""

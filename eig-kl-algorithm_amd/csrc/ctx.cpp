@@ -1350,6 +1350,38 @@ int ek_spmv_host(ek_ctx* c, const double* x, double* y) {
     EK_CATCH
 }
 
+int ek_spmv_gather_bench(ek_ctx* c, int iters, double* avg_us) {
+    EK_TRY
+    check_ctx(c);
+    if (!c->n) ek::fail(EK_ESTATE, "ek_spmv_gather_bench before ek_spmv_setup");
+    if (iters <= 0 || !avg_us) ek::fail(EK_EINVAL, "ek_spmv_gather_bench: bad argument");
+    hipStream_t s = c->stream;
+    const size_t X = size_t(x_extent(c));
+    DBuf x, sink;
+    x.ensure(X * 8);
+    sink.ensure(size_t(std::max(std::max(c->nrb_spmv, c->pn_G), 1)) * 8);
+    std::vector<double> h(X);
+    for (size_t i = 0; i < X; ++i) h[i] = double((i * 2654435761u) % 1000u) / 1000.0 - 0.5;
+    HIPCHK(hipMemcpyAsync(x.p, h.data(), X * 8, hipMemcpyHostToDevice, s));
+    const auto m = spmv_mat(c);
+    for (int i = 0; i < 10; ++i) ek::dev::spmv_gather_only(s, m, x.as<double>(), sink.as<double>());
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) ek::dev::spmv_gather_only(s, m, x.as<double>(), sink.as<double>());
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIPCHK(hipGetLastError());
+    *avg_us = 1e3 * double(ms) / iters;
+    return EK_OK;
+    EK_CATCH
+}
+
 int ek_spmv_bench(ek_ctx* c, int iters, int fused, double* avg_us) {
     EK_TRY
     check_ctx(c);
@@ -3173,6 +3205,8 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
     if (nets)
         HIPCHK(hipMemcpyAsync(cparts.data(), c->kl_count.p, cparts.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (ho.status == 3u)
+        ek::fail(EK_EHIP, "KL swap loop: an in-launch wait gave up (EK_KL_PIPE=0 runs the loop without them)");
     unsigned long long hc[3] = {0, 0, 0};
     for (int k = 0; k < 3; ++k)
         for (int b = 0; b < ncb; ++b) hc[k] += cparts[size_t(k) * size_t(ncb) + size_t(b)];
@@ -3193,7 +3227,18 @@ extern "C" int ek_kl_run(ek_ctx* c, int32_t limit, ek_swap* log_out, int64_t cap
         res->net_cut_best = nets ? int64_t(hc[1]) : -1;
         res->net_cut_final = nets ? int64_t(hc[2]) : -1;
         res->loop_ms = loop_ms;
-        if (std::getenv("EK_KL_PROF")) {
+        if (std::getenv("EK_KL_PROF") && ho.prof[13] == 0x9199ull) {  // the overlapped loop (k_kl_swap_pipe)
+            const double sw = double(std::max<long long>(1, ho.iterations)), gs = double(std::max<unsigned long long>(1, ho.prof[2]));
+            std::fprintf(stderr, "[kl-pipe] %lld swaps: speculated %.1f %%, hits %.1f %%; loop %.0f cycles/swap\n",
+                         (long long)ho.iterations, 100.0 * double(ho.prof[0]) / sw, 100.0 * double(ho.prof[1]) / gs,
+                         double(ho.prof[12]) / sw);
+            std::fprintf(stderr, "[kl-pipe] gain wave 0, cycles/swap: pair wait %.0f, P %.0f, speculative rows %.0f (per "
+                         "speculation), pair->barrier1 %.0f\n", double(ho.prof[3]) / gs, double(ho.prof[4]) / gs,
+                         double(ho.prof[5]) / double(std::max<unsigned long long>(1, ho.prof[0])), double(ho.prof[6]) / gs);
+            std::fprintf(stderr, "[kl-pipe] W wave, cycles/swap: barrier-2 wait %.0f, selection %.0f, pair->barrier1 %.0f, "
+                         "G2 span %.0f; G2a wave's G2 span %.0f\n", double(ho.prof[7]) / sw, double(ho.prof[8]) / sw,
+                         double(ho.prof[9]) / sw, double(ho.prof[10]) / sw, double(ho.prof[11]) / sw);
+        } else if (std::getenv("EK_KL_PROF")) {
             static const char* names[12] = {"select", "G1-key", "bar1", "G2a", "G2bc", "bar2", "G1-aux", "G1-sum",
                                             "n_stale", "n_late+tail", "G1-load", "G1-look"};
             std::fprintf(stderr, "[kl] %lld swaps, us/swap:", (long long)ho.iterations);

@@ -238,6 +238,8 @@ void panel_fill(hipStream_t s, int G, const int32_t* rowptr, const uint32_t* pk,
 void spmv_panel(hipStream_t s, const SpmvPanel& m, const double* dict, const double* x, double* y, const double* fn2,
                 const double* f, double* vcol, double* apart, const StepFin* fin, hipEvent_t ev_start,
                 hipEvent_t ev_stop, double* alpha_out, unsigned* actr);
+// the panel form's gather-only ceiling (kernels_panel.hip; ek_spmv_gather_bench)
+void panel_gather_only(hipStream_t s, const SpmvPanel& m, const double* dict, const double* x, double* sink);
 // host: the workgroup row ranges (equal nnz, <= PANEL_MAX_ROWS rows each)
 std::vector<int32_t> panel_row_ranges(const int32_t* rowptr, int64_t nrows, int target_groups);
 // pk[e] = (code << colbits) | col[e] from the device build's value table
@@ -278,6 +280,10 @@ constexpr int ALPHA_SUB = 32;  // first-level counters of the SpMV's last-block 
 // alpha_out (with apart): the last block to finish also reduces every block's
 // alpha partial (k_three_term's order and bits) into *alpha_out; actr: a
 // device counter, zero before the first such launch (re-armed by each)
+// the gather-only ceiling of either form: its grid, matrix stream and x /
+// value gathers with nothing else (ek_spmv_gather_bench); sink: never written
+// in practice (>= one double per workgroup)
+void spmv_gather_only(hipStream_t s, const SpmvMat& m, const double* x, double* sink);
 void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
           double* vcol, double* apart, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
           hipEvent_t ev_stop = nullptr, double* alpha_out = nullptr, unsigned* actr = nullptr);

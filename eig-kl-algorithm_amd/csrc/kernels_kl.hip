@@ -52,6 +52,12 @@
 #ifndef EK_E_TWO_TRIPS
 #define EK_E_TWO_TRIPS 1  // early rescans: gains, then the winner's descriptor (0: both in one trip, A/B; 2.03 vs 2.00 us/swap)
 #endif
+#ifndef EK_G1_DRAIN
+#define EK_G1_DRAIN 0  // lab: gain waves drain their stores at the loop top (vmcnt(0))
+#endif
+#ifndef EK_PIPE_SLEEP
+#define EK_PIPE_SLEEP 1  // k_kl_swap_pipe: s_sleep units between the polls of a wait
+#endif
 #ifndef EK_E_SLEEP
 #define EK_E_SLEEP 0  // early-rescan waves: s_sleep units before their loads (two-trip rescans: 0 best, 4: +0.01 us/swap)
 #endif
@@ -336,7 +342,8 @@ size_t kl_loop_lds_bytes(const KLDev& d) {
     constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
     const size_t b = (nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2 + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
                      (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2) * 8 +
-                     (2 * nck + KL_ITEM_CAP + 4 + 4 + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4;
+                     (2 * nck + KL_ITEM_CAP + 4 + 4 + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4 +
+                     128;  // (+ k_kl_swap_pipe's speculative pair, 16-B aligned)
     return b <= 152 * 1024 ? b : 0;
 }
 
@@ -581,6 +588,11 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 }
             }
         }
+#if EK_G1_DRAIN
+        // (lab) the gain waves wait for their previous gain stores here, beside
+        // the selection, so the row loads after it wait for nothing older
+        if (wv < NG) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
         // S. selection (cKL.cpp:341-355): the pair P published before barrier
         // 2 (one LDS round trip), or else lanes 0-31 reduce remain[0]'s keys,
         // 32-63 remain[1]'s; identical in every wave
@@ -1218,6 +1230,777 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
 }
 
 
+// ---------------------------------------------------------------------------
+// The swap loop with consecutive swaps overlapped (k_kl_swap_pipe; VERDICT r5
+// next-1).  The per-swap work, the LDS state and the parity rules are those of
+// k_kl_swap_loop; the schedule differs:
+//  * barrier 2 is a counter in LDS, not s_barrier.  The gain waves only arrive
+//    at it (once their reads of this swap's state are done) and never wait at
+//    it; the other waves wait for all eight arrivals before the selection;
+//  * right after barrier 1 each gain wave takes the next pair exactly from
+//    the state G2 is publishing (the EK_KL_NEXT rule above: the shadow keys of
+//    the other chunks, node1's / node2's chunks resolved as G2a resolves them,
+//    the winners' descriptors from the updated rows, the early rescan or the
+//    chunk table), loads that pair's neighbour rows and sums their gains into
+//    registers — while G2 and the next selection run in the other waves;
+//  * the W wave publishes the selection's pair (keys and descriptors, one LDS
+//    flag); a gain wave whose pair has the same keys commits its sums (gain
+//    stores, key merges, item lists) at once, otherwise it runs G1 on the
+//    published pair (a tagged chunk, a stale early rescan, an overflowing short
+//    list or more rows than one pass: no speculation).
+// A node's gain is recomputed from its row and the current sides alone
+// (cKL.cpp:253-272), so the sums are the same fp32 bits whenever they run:
+// the sides are the bitmaps after this swap (its flip applied by hand, as it
+// may still be in flight in the W_FLIP wave) with the next pair's two nodes
+// swapped.  The keys carry the positions, so equal keys are the same pair.
+// Every wait is a bounded poll: a wave that gives up raises an abort word the
+// others poll as well, and the launch ends with status 3 (EK_EHIP on the host)
+// instead of hanging.
+// PROF: per-swap counters and shader-clock spans of gain wave 0, the W wave
+// and the G2a wave (KLOut::prof, marker 0x9199 in [13]; printed by the host).
+template <bool PROF, bool SEGC>
+__global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_pipe(KLDev d, int limit, ek_swap* __restrict__ log,
+                                                                  long long cap, KLOut* __restrict__ out) {
+    constexpr int NW = KL_LOOP_THREADS / 64;
+    constexpr int E_PARTS = 2, NQ_E = KL_CHUNK / 64 / E_PARTS;
+    constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
+    constexpr int W_FLIP = W_EA - 1;
+    constexpr int LPR = SEGC ? 4 : 8, RPW = 64 / LPR;
+    constexpr int PPL = (SEGC ? KL_SEGC_PIECES : KL_SEG_LANES) / LPR;  // 16-B pieces per lane
+    constexpr unsigned POLL_CAP = 1u << 22;                              // polls before a wait gives up
+    static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * 2, "kl_loop_lds_bytes reserves staging for NG gain waves");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int half = lane >> 5, hl = lane & 31;
+    const int nsel = kl_sel_pad(d.nck0, d.nck1);
+    const int words = (d.n + 31) / 32;
+    // LDS carve: k_kl_swap_loop's (kl_loop_lds_bytes); nx_info / nx_key hold
+    // the published pair, nx_ok the waits' words
+    KLInfo* ci0 = reinterpret_cast<KLInfo*>(smem);
+    KLInfo* ci1 = ci0 + d.nck0;
+    KLInfo* it_info = ci1 + d.nck1;
+    KLInfo* er_info = it_info + KL_ITEM_CAP;
+    KLInfo* ab_info = er_info + 2 * E_PARTS;
+    KLInfo* nx_info = ab_info + 2 * KL_AB_CAP;
+    int4* sg_stage = reinterpret_cast<int4*>(nx_info + 2);
+    u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * KL_STAGE_ROWS * KL_STAGE_ROW);
+    u64* ck1 = ck0 + nsel;
+    u64* ckn0 = ck1 + nsel;
+    u64* ckn1 = ckn0 + d.nck0;
+    u64* it_key = ckn1 + d.nck1;
+    u64* er_key = it_key + KL_ITEM_CAP;
+    u64* ab_key = er_key + 2 * E_PARTS;
+    u64* nx_key = ab_key + 2 * KL_AB_CAP;
+    int* dtag0 = reinterpret_cast<int*>(nx_key + 2);
+    int* dtag1 = dtag0 + d.nck0;
+    int* ctag0 = dtag1 + d.nck1;
+    int* ctag1 = ctag0 + d.nck0;
+    int* it_cs = ctag1 + d.nck1;
+    int* s_stop = it_cs + KL_ITEM_CAP;  // [0..1] stop by parity, [3] the last tag
+    int* ab_cnt = s_stop + 4;           // [2][2]: short-list counts by swap parity
+    int* sync = ab_cnt + 4;  // [0] barrier-2 arrivals, [1] W's pair, [2] abort, [3] wave 0's speculative pair (iteration + 1)
+    uint32_t* s_side = reinterpret_cast<uint32_t*>(sync + 4);
+    uint32_t* s_lock = s_side + words;
+    float* s_wd = reinterpret_cast<float*>(s_lock + words);
+    // gain wave 0's speculative pair for waves 1 .. NG-1: [0..1] keys (0: none), [2..5] the two descriptors
+    u64* sp = reinterpret_cast<u64*>((reinterpret_cast<uintptr_t>(s_wd + (SEGC ? d.nwd : 0)) + 15) & ~uintptr_t(15));
+    if constexpr (SEGC)
+        for (int i = tid; i < d.nwd; i += KL_LOOP_THREADS) s_wd[i] = d.wdict[i];
+    for (int i = tid; i < nsel; i += KL_LOOP_THREADS) {
+        ck0[i] = i < d.nck0 ? d.ckey0[i] : 0ull;
+        ck1[i] = i < d.nck1 ? d.ckey1[i] : 0ull;
+    }
+    for (int i = tid; i < d.nck0; i += KL_LOOP_THREADS) {
+        ckn0[i] = d.ckey0[i];
+        ci0[i] = d.cinfo0[i];
+        dtag0[i] = ctag0[i] = -1;
+    }
+    for (int i = tid; i < d.nck1; i += KL_LOOP_THREADS) {
+        ckn1[i] = d.ckey1[i];
+        ci1[i] = d.cinfo1[i];
+        dtag1[i] = ctag1[i] = -1;
+    }
+    for (int i = tid; i < words; i += KL_LOOP_THREADS) {
+        s_side[i] = side_word(d.side_init, d.n, i);
+        s_lock[i] = 0u;
+    }
+    if (tid < 4) s_stop[tid] = tid == 3 ? -1 : 0;
+    if (tid < 4) ab_cnt[tid] = 0;
+    if (tid < 4) sync[tid] = 0;
+    __syncthreads();
+    float cut = *d.cut0, best = cut;  // loop-carried scalars: the W wave's lane 0 only
+    long long best_it = 0, it = 0;
+    unsigned term = 0;
+    unsigned long long pc[12] = {};  // PROF counters / spans (this wave's)
+    unsigned long long t_a = 0, t_b = 0;
+    auto now = [&]() -> unsigned long long { return PROF ? __builtin_amdgcn_s_memtime() : 0ull; };
+    const unsigned long long t_start = now();
+
+    // ---- waits (bounded; the abort word ends every other wait too)
+    auto aborted = [&]() -> bool { return __hip_atomic_load(&sync[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; };
+    auto give_up = [&]() { __hip_atomic_store(&sync[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    // barrier 2: this wave's LDS reads and writes of the swap are done
+    auto arrive = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_word = [&](int w, int target) -> bool {
+        for (unsigned p = 0;; ++p) {
+            const int v = __hip_atomic_load(&sync[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+            if constexpr (EK_PIPE_SLEEP > 0) __builtin_amdgcn_s_sleep(EK_PIPE_SLEEP);  // (spare the CU's scalar issue)
+            if ((p & 255u) == 255u) {  // (the abort word every 256 polls: one LDS round trip a poll)
+                if (__builtin_amdgcn_readfirstlane(int(aborted()))) return false;
+                if (p >= POLL_CAP) {
+                    give_up();
+                    return false;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        return true;
+    };
+
+    // ---- G1, split: the rows' loads and sums (no shared writes), then their commit.
+    // One pass over rows i0 + lane / LPR of the pair's neighbour lists; side_fn /
+    // lock_fn give the sides and locks the gains are computed under.  The row's
+    // first lane (gi >= 0 on return) holds its descriptor and sums.
+    auto g1_rows = [&](int i0, int pa, int la, int pb, int lb, auto&& side_fn, auto&& lock_fn, int& gi_o, int4& a_o,
+                       float& in_o, float& ex_o, bool& act_o) {
+        const int tot = la + lb;
+        const int gi = i0 + lane / LPR, j8 = lane % LPR, srow = lane / LPR;
+        int pg = gi < tot ? (gi < la ? pa + gi : pb + gi - la) : pa;
+        pg = min(max(pg, 0), int(d.nnz) - 1);  // (a speculative descriptor never addresses outside the CSR)
+        int4 piece[PPL];
+        if constexpr (SEGC) {
+#pragma unroll
+            for (int r = 0; r < PPL; ++r)
+                piece[r] = *reinterpret_cast<const int4*>(d.segc + size_t(pg) * KL_SEGC_PIECES + j8 + LPR * r);
+        } else {
+#pragma unroll
+            for (int r = 0; r < PPL; ++r)
+                piece[r] = d.seg ? *reinterpret_cast<const int4*>(d.seg + size_t(pg) * KL_SEG_LANES + j8 + LPR * r)
+                                 : make_int4(0, 0, 0, 0);
+        }
+        const int4 a = j8 == 0 ? *reinterpret_cast<const int4*>(d.aux + pg) : make_int4(0, 0, 0, 0);
+        v2f ie_seg = {0.0f, 0.0f};
+        int4* stage = sg_stage + wv * KL_STAGE_ROWS * KL_STAGE_ROW;
+        if constexpr (SEGC) {
+            const uint32_t cmask = (1u << d.wcolbits) - 1u;
+            v2f cc[PPL][4];
+#pragma unroll
+            for (int r = 0; r < PPL; ++r) {
+                const uint32_t wv4[4] = {uint32_t(piece[r].x), uint32_t(piece[r].y), uint32_t(piece[r].z),
+                                         uint32_t(piece[r].w)};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float wk = s_wd[wv4[k] >> d.wcolbits];
+                    const bool ek = side_fn(int(wv4[k] & cmask));
+                    cc[r][k] = v2f{ek ? 0.0f : wk, ek ? wk : 0.0f};
+                }
+            }
+            const int lenq = a.z;
+#pragma unroll
+            for (int st = 0; st < 4 * PPL; ++st) {
+                if (!__ballot(lenq > 4 * st)) break;
+                v2f x = ie_seg;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) x += cc[st / 4][k];  // in row order
+                ie_seg.x = quad_bcast(x.x, st % 4);
+                ie_seg.y = quad_bcast(x.y, st % 4);
+            }
+        } else if (d.seg) {
+#pragma unroll
+            for (int r = 0; r < PPL; ++r) {
+                const int4 pc = piece[r];
+                const bool e0 = side_fn(pc.x);
+                const bool e1 = side_fn(pc.z);
+                const float w0 = __int_as_float(pc.y), w1 = __int_as_float(pc.w);
+                stage[srow * KL_STAGE_ROW + j8 + LPR * r] =
+                    make_int4(__float_as_int(e0 ? 0.0f : w0), __float_as_int(e0 ? w0 : 0.0f),
+                              __float_as_int(e1 ? 0.0f : w1), __float_as_int(e1 ? w1 : 0.0f));
+            }
+        }
+        gi_o = -1;
+        if (j8 != 0 || gi >= tot) return;  // the row's first lane sums it
+        const int len = a.z, rp = a.y;
+        float internal = 0.0f, external = 0.0f;
+        int q = 0;
+        if constexpr (SEGC) {
+            internal = ie_seg.x;
+            external = ie_seg.y;
+            q = 2 * KL_SEG_LANES;
+        } else if (d.seg) {
+            int4 sg[KL_SEG_LANES];
+#pragma unroll
+            for (int j = 0; j < KL_SEG_LANES; ++j) sg[j] = stage[srow * KL_STAGE_ROW + j];
+            v2f ie = {0.0f, 0.0f};
+#pragma unroll
+            for (int b = 0; b < KL_SEG_LANES / 4; ++b) {
+                if (!__ballot(len > 8 * b)) break;
+#pragma unroll
+                for (int j = 4 * b; j < 4 * b + 4; ++j) {
+                    ie += v2f{__int_as_float(sg[j].x), __int_as_float(sg[j].y)};
+                    ie += v2f{__int_as_float(sg[j].z), __int_as_float(sg[j].w)};
+                }
+            }
+            internal = ie.x;
+            external = ie.y;
+            q = 2 * KL_SEG_LANES;
+        }
+        for (; q < len; q += 16) {  // beyond the inline segment: 16 loads in flight per pass
+            int cc[16];
+            float ww[16];
+            const int lim = int(d.nnz) - 1;  // (a speculative row stays inside the CSR)
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) {
+                cc[k2] = d.col[min(rp + q + k2, lim + 16)];  // col/w carry 16 zero entries of tail padding
+                ww[k2] = q + k2 < len ? d.w[min(rp + q + k2, lim)] : 0.0f;
+            }
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) {
+                cc[k2] = q + k2 < len ? cc[k2] : 0;
+                const bool e = side_fn(cc[k2]);
+                internal += e ? 0.0f : ww[k2];
+                external += e ? ww[k2] : 0.0f;
+            }
+        }
+        gi_o = gi;
+        a_o = a;
+        in_o = internal;
+        ex_o = external;
+        act_o = !lock_fn(a.x);
+    };
+    // the commit of one row (G1's writes): its gain, and its new key merged
+    // into its chunk's shadow key, node1's / node2's short list or a tag
+    auto g1_commit = [&](int gi, int4 a, float internal, float external, bool act, int cA, int cB, int tag,
+                         int abp) {
+        if (gi < 0) return;
+        const int u = a.x, rp = a.y, len = a.z;
+        const uint32_t pl = uint32_t(a.w);
+        const int ls = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / KL_CHUNK;
+        const bool ab = ls ? c == cB : c == cA;
+        const u64 K = (ls ? ck1 : ck0)[c];
+        int cs = -1;
+        u64 kn = 0ull;
+        KLInfo inf{0, 0, 0, 0};
+        if (act) {
+            const float g = external - internal;
+            const int s = ls;
+            (s ? d.gp1 : d.gp0)[pp] = g;
+            kn = key_max(s ? -g : g, pp);
+            if (ab) {
+                const int slot = atomicAdd(&ab_cnt[abp + s], 1);
+                if (slot < KL_AB_CAP) {
+                    ab_key[s * KL_AB_CAP + slot] = kn;
+                    ab_info[s * KL_AB_CAP + slot] = KLInfo{u, rp, len, pp};
+                }
+            } else {
+                if (uint32_t(~uint32_t(K & 0xffffffffull)) == uint32_t(pp) && kn < K) {
+                    (s ? dtag1 : dtag0)[c] = tag;
+                    s_stop[3] = tag;
+                } else if (kn > K) {
+                    atomicMax(&(s ? ckn1 : ckn0)[c], kn);
+                    if (gi >= KL_ITEM_CAP) {
+                        (s ? dtag1 : dtag0)[c] = tag;
+                        s_stop[3] = tag;
+                    }
+                }
+            }
+            cs = int((pl & 0x80000000u) | uint32_t(c));
+            inf = KLInfo{u, rp, len, pp};
+        }
+        if (gi < KL_ITEM_CAP) {
+            it_key[gi] = kn;
+            it_cs[gi] = cs;
+            it_info[gi] = inf;
+        }
+    };
+
+    bool fail = false;
+    if (wv < NG) {
+        // ================= gain waves
+        bool spec = false;
+        u64 sk0 = 0ull, sk1 = 0ull;
+        int s_gi = -1;
+        int4 s_a = make_int4(0, 0, 0, 0);
+        float s_in = 0.0f, s_ex = 0.0f;
+        bool s_act = false;
+        int pA = -1, pB = -1;  // the previous swap's pair (its flip may still be in flight)
+        for (;; ++it) {
+            if constexpr (PROF) t_a = now();
+            if (!wait_word(1, int(it) + 1)) {  // the selection's pair, published by W
+                fail = true;
+                break;
+            }
+            if constexpr (PROF) {
+                t_b = now();
+                pc[3] += t_b - t_a;  // waiting for the pair
+            }
+            const u64 k0 = nx_key[0], k1 = nx_key[1];
+            const v4i dA = *reinterpret_cast<const v4i*>(nx_info), dB = *reinterpret_cast<const v4i*>(nx_info + 1);
+            const u64 K0 = readlane_u64(k0, 0), K1 = readlane_u64(k1, 0);
+            if (K0 == 0ull || K1 == 0ull) break;
+            const int posA = int(~uint32_t(K0 & 0xffffffffull)), posB = int(~uint32_t(K1 & 0xffffffffull));
+            const int cA = posA / KL_CHUNK, cB = posB / KL_CHUNK;
+            const int A = __builtin_amdgcn_readfirstlane(dA.x), pa = __builtin_amdgcn_readfirstlane(dA.y),
+                      la = __builtin_amdgcn_readfirstlane(dA.z);
+            const int B = __builtin_amdgcn_readfirstlane(dB.x), pb = __builtin_amdgcn_readfirstlane(dB.y),
+                      lb = __builtin_amdgcn_readfirstlane(dB.z);
+            const int tot = la + lb, tag = int(it), abp = (tag & 1) * 2;
+            const int qA = pA, qB = pB;
+            // sides / locks after the previous swap (flip applied by hand), then this pair swapped
+            auto side_cur = [&](int x) -> bool {
+                const bool b = x == qA ? true : x == qB ? false : ((s_side[x >> 5] >> (x & 31)) & 1u) != 0;
+                return b ^ (x == A) ^ (x == B);
+            };
+            auto lock_cur = [&](int x) -> bool {
+                return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == qA || x == qB || x == A || x == B;
+            };
+            if constexpr (PROF) {
+                pc[2] += 1;
+                pc[1] += spec && sk0 == K0 && sk1 == K1;
+            }
+            if (spec && sk0 == K0 && sk1 == K1) {
+                g1_commit(s_gi, s_a, s_in, s_ex, s_act, cA, cB, tag, abp);
+            } else {
+                for (int i0 = wv * RPW; i0 < tot; i0 += NG * RPW) {
+                    int gi;
+                    int4 a;
+                    float in_, ex_;
+                    bool act;
+                    g1_rows(i0, pa, la, pb, lb, side_cur, lock_cur, gi, a, in_, ex_, act);
+                    g1_commit(gi, a, in_, ex_, act, cA, cB, tag, abp);
+                }
+            }
+            if constexpr (PROF) {
+                if (tid == 0 && s_in == -12345.0f) s_stop[2] = 0;  // keeps the commit's LDS writes ahead of the stamp
+                t_a = now();
+                pc[6] += t_a - t_b;  // pair -> barrier 1 (commit or G1)
+            }
+            __syncthreads();  // (1) gains, early rescans, merged keys and tags visible
+            if constexpr (PROF) t_a = now();
+            if (s_stop[it & 1]) {
+                ++it;
+                break;
+            }
+            // P. the next pair, exactly, from the state G2 is publishing
+            // (gain wave 0; it hands the pair to the other gain waves)
+            spec = false;
+            u64 kA = 0ull, kB = 0ull;
+            int nA = 0, npa = 0, nla = 0, nB = 0, npb = 0, nlb = 0;
+            bool okp = false;
+            if (wv == 0) {
+                const bool any_tag = s_stop[3] == tag;
+                const int s = half, cS = s ? cB : cA, nck = s ? d.nck1 : d.nck0;
+                const u64* ckn = s ? ckn1 : ckn0;
+                u64 k = 0ull;
+                for (int c0 = hl; c0 < nck; c0 += 4 * 32) {
+                    u64 kv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) kv[u] = ckn[min(c0 + 32 * u, nck - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const u64 v = kv[u] & (min(c0 + 32 * u, nck - 1) == cS ? 0ull : ~0ull);
+                        k = v > k ? v : k;
+                    }
+                }
+                u64 rk[E_PARTS];
+                v4i rf[E_PARTS];
+#pragma unroll
+                for (int q = 0; q < E_PARTS; ++q) {
+                    rk[q] = er_key[s * E_PARTS + q];
+                    rf[q] = *reinterpret_cast<const v4i*>(er_info + s * E_PARTS + q);
+                }
+                const int cnt = ab_cnt[abp + s];
+                const int hs = hl < KL_AB_CAP ? hl : KL_AB_CAP - 1;
+                const u64 bk_raw = ab_key[s * KL_AB_CAP + hs];
+                const v4i bf = *reinterpret_cast<const v4i*>(ab_info + s * KL_AB_CAP + hs);
+                const int il = lane < tot ? lane : 0;
+                const u64 ik = it_key[il];
+                const int ics = it_cs[il];
+                const v4i iinf = *reinterpret_cast<const v4i*>(it_info + il);
+                const bool have = hl < cnt && hl < KL_AB_CAP;
+                const u64 bk = have ? bk_raw : 0ull;
+                u64 R = rk[0];
+                v4i Rf = rf[0];
+#pragma unroll
+                for (int q = 1; q < E_PARTS; ++q) {
+                    const bool b = rk[q] > R;
+                    R = b ? rk[q] : R;
+                    Rf.x = b ? rf[q].x : Rf.x;
+                    Rf.y = b ? rf[q].y : Rf.y;
+                    Rf.z = b ? rf[q].z : Rf.z;
+                    Rf.w = b ? rf[q].w : Rf.w;
+                }
+                const int Rpos = int(~uint32_t(R & 0xffffffffull));
+                const bool stale = have && R != 0ull && bf.w == Rpos && bk < R;
+                const bool bad = any_tag || tot > 64 || __ballot(stale || cnt > KL_AB_CAP) != 0ull;
+                const u64 m = __ballot(cnt > 0) ? half_max_u64(bk) : 0ull;
+                const u64 kS = m > R ? m : R;
+                k = kS > k ? kS : k;
+                k = half_max_u64(k);
+                kA = readlane_u64(k, 0);
+                kB = readlane_u64(k, 32);
+                const bool own = lane < tot && ics != -1;
+                const u64 mA = __ballot(own && ics >= 0 && ik == kA), mB = __ballot(own && ics < 0 && ik == kB);
+                const u64 mS = s ? mB : mA;
+                v4i desc = Rf;
+                if (mA) {
+                    const int l = __ffsll((long long)mA) - 1;
+                    const v4i t = v4i{__builtin_amdgcn_readlane(iinf.x, l), __builtin_amdgcn_readlane(iinf.y, l),
+                                      __builtin_amdgcn_readlane(iinf.z, l), 0};
+                    if (!s) desc = t;
+                }
+                if (mB) {
+                    const int l = __ffsll((long long)mB) - 1;
+                    const v4i t = v4i{__builtin_amdgcn_readlane(iinf.x, l), __builtin_amdgcn_readlane(iinf.y, l),
+                                      __builtin_amdgcn_readlane(iinf.z, l), 0};
+                    if (s) desc = t;
+                }
+                if (!mS && k != R && k != 0ull)  // an unchanged chunk's winner (no G2 wave writes its entry)
+                    desc = *reinterpret_cast<const v4i*>((s ? ci1 : ci0) + int(~uint32_t(k & 0xffffffffull)) / KL_CHUNK);
+                // every read of this swap's state is done: barrier 2's arrival
+                arrive();
+                nA = __builtin_amdgcn_readlane(desc.x, 0);
+                npa = __builtin_amdgcn_readlane(desc.y, 0);
+                nla = __builtin_amdgcn_readlane(desc.z, 0);
+                nB = __builtin_amdgcn_readlane(desc.x, 32);
+                npb = __builtin_amdgcn_readlane(desc.y, 32);
+                nlb = __builtin_amdgcn_readlane(desc.z, 32);
+                okp = !bad && kA != 0ull && kB != 0ull && nla >= 0 && nlb >= 0 && nla + nlb <= NG * RPW && nA != nB;
+                if (lane == 0) {  // (to the other gain waves)
+                    sp[0] = okp ? kA : 0ull;
+                    sp[1] = kB;
+                    reinterpret_cast<v4i*>(sp + 2)[0] = v4i{nA, npa, nla, 0};
+                    reinterpret_cast<v4i*>(sp + 2)[1] = v4i{nB, npb, nlb, 0};
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __hip_atomic_store(&sync[3], int(it) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else {
+                arrive();  // (this wave reads none of the swap's shared state)
+                if (!wait_word(3, int(it) + 1)) {
+                    fail = true;
+                    break;
+                }
+                kA = sp[0];
+                kB = sp[1];
+                const v4i a0 = reinterpret_cast<const v4i*>(sp + 2)[0], b0 = reinterpret_cast<const v4i*>(sp + 2)[1];
+                kA = readlane_u64(kA, 0);
+                kB = readlane_u64(kB, 0);
+                okp = kA != 0ull;
+                nA = __builtin_amdgcn_readfirstlane(a0.x);
+                npa = __builtin_amdgcn_readfirstlane(a0.y);
+                nla = __builtin_amdgcn_readfirstlane(a0.z);
+                nB = __builtin_amdgcn_readfirstlane(b0.x);
+                npb = __builtin_amdgcn_readfirstlane(b0.y);
+                nlb = __builtin_amdgcn_readfirstlane(b0.z);
+            }
+            if constexpr (PROF) {
+                t_b = now();
+                pc[4] += t_b - t_a;  // barrier 1 -> the speculative pair
+            }
+            {
+                if (okp) {
+                    // the rows of the next pair under the sides after this swap and that pair's
+                    auto side_nx = [&](int x) -> bool {
+                        const bool b = x == A ? true : x == B ? false : ((s_side[x >> 5] >> (x & 31)) & 1u) != 0;
+                        return b ^ (x == nA) ^ (x == nB);
+                    };
+                    auto lock_nx = [&](int x) -> bool {
+                        return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B || x == nA || x == nB;
+                    };
+                    s_gi = -1;
+                    if (wv * RPW < nla + nlb)  // (rows for this wave)
+                        g1_rows(wv * RPW, npa, nla, npb, nlb, side_nx, lock_nx, s_gi, s_a, s_in, s_ex, s_act);
+                    spec = true;
+                    if constexpr (PROF) {
+                        pc[0] += 1;
+                        if (s_gi >= 0 && s_in == -12345.0f) s_stop[2] = 0;  // keeps the sums ahead of the stamp
+                        pc[5] += now() - t_b;  // the speculative rows
+                    }
+                    sk0 = kA;
+                    sk1 = kB;
+                }
+            }
+            pA = A;
+            pB = B;
+        }
+    } else {
+        // ================= W, early rescans, G2
+        for (;; ++it) {
+            if constexpr (PROF) t_a = now();
+            if (it > 0 && !wait_word(0, 8 * int(it))) {  // barrier 2 of the previous swap
+                fail = true;
+                break;
+            }
+            if constexpr (PROF) {
+                t_b = now();
+                pc[7] += t_b - t_a;  // waiting at barrier 2
+            }
+            // S. selection (cKL.cpp:341-355) by the W wave alone (lanes 0-31 remain[0]'s
+            // keys, 32-63 remain[1]'s), published to every other wave
+            u64 k0, k1;
+            v4i dA = v4i{0, 0, 0, 0}, dB = v4i{0, 0, 0, 0};
+            if (wv == W_W) {
+                u64 k = 0ull;
+                const u64* ck = half ? ck1 : ck0;
+                if (nsel <= 4 * 32) {
+                    u64 kv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) kv[u] = ck[min(hl + 32 * u, nsel - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) k = kv[u] > k ? kv[u] : k;
+                } else {
+                    for (int c0 = hl; c0 < nsel; c0 += 8 * 32) {
+                        u64 kv[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) kv[u] = ck[min(c0 + 32 * u, nsel - 1)];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) k = kv[u] > k ? kv[u] : k;
+                    }
+                }
+                k = half_max_u64(k);
+                k0 = readlane_u64(k, 0);
+                k1 = readlane_u64(k, 32);
+                if (k0 != 0ull && k1 != 0ull) {
+                    dA = *reinterpret_cast<const v4i*>(ci0 + int(~uint32_t(k0 & 0xffffffffull)) / KL_CHUNK);
+                    dB = *reinterpret_cast<const v4i*>(ci1 + int(~uint32_t(k1 & 0xffffffffull)) / KL_CHUNK);
+                }
+                if (lane == 0) {
+                    nx_key[0] = k0;
+                    nx_key[1] = k1;
+                    *reinterpret_cast<v4i*>(nx_info) = dA;
+                    *reinterpret_cast<v4i*>(nx_info + 1) = dB;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __hip_atomic_store(&sync[1], int(it) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else {
+                if (!wait_word(1, int(it) + 1)) {
+                    fail = true;
+                    break;
+                }
+                k0 = readlane_u64(nx_key[0], 0);
+                k1 = readlane_u64(nx_key[1], 0);
+                const v4i a0 = *reinterpret_cast<const v4i*>(nx_info), b0 = *reinterpret_cast<const v4i*>(nx_info + 1);
+                dA = v4i{__builtin_amdgcn_readfirstlane(a0.x), __builtin_amdgcn_readfirstlane(a0.y),
+                         __builtin_amdgcn_readfirstlane(a0.z), 0};
+                dB = v4i{__builtin_amdgcn_readfirstlane(b0.x), __builtin_amdgcn_readfirstlane(b0.y),
+                         __builtin_amdgcn_readfirstlane(b0.z), 0};
+            }
+            const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
+            const int cA = posA / KL_CHUNK, cB = posB / KL_CHUNK;
+            if constexpr (PROF) {
+                t_a = now();
+                pc[8] += t_a - t_b;  // barrier 2 -> the pair (selection)
+            }
+            if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
+            const int A = dA.x, pa = dA.y, la = dA.z, B = dB.x, pb = dB.y, lb = dB.z;
+            auto locked_now = [&](int x) -> bool { return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B; };
+            const int tot = la + lb;
+            const int tag = int(it);
+            const int abp = (tag & 1) * 2;
+            if (wv == W_W) {
+                // W. w(A,B) (getEdgeWeight, cKL.cpp:75-82) and the pair gain (cKL.cpp:360-386)
+                float gA = 0.f, gB = 0.f;
+                if (lane == 0) {
+                    gA = d.gp0[posA];
+                    gB = d.gp1[posB];
+                }
+                float wab = 0.0f;
+                bool found = false;
+                for (int i = lane; i < la; i += 64)
+                    if (d.col[pa + i] == B) {
+                        wab = d.w[pa + i];
+                        found = true;
+                    }
+                const u64 bal = __ballot(found);
+                if (bal) wab = __shfl(wab, __ffsll((long long)bal) - 1, 64);
+                if (lane == 0) {
+                    d.gp0[posA] = __builtin_nanf("");
+                    d.gp1[posB] = __builtin_nanf("");
+                    const float gain = gA - gB - 2.0f * wab;
+                    cut -= gain;
+                    if (cut < best) {
+                        best = cut;
+                        best_it = it + 1;
+                    }
+                    if (it < cap) log[it] = ek_swap{uint32_t(it + 1), uint32_t(A), uint32_t(B), gA, gB, gain, cut, 0u};
+                    int stop = 0;
+                    if (gain <= 0.0f) {
+                        if (++term > unsigned(limit)) stop = 1;
+                    } else {
+                        term = 0;
+                    }
+                    if (it + 1 >= d.n0 || it + 1 >= d.n1) stop = 1;
+                    s_stop[it & 1] = stop;
+                }
+            } else {
+                // E. early rescan of the chunk node1 (node2) leaves
+                const int s = wv <= W_EB ? 1 : 0, part = (s ? W_EB : W_EA) - wv;
+                const int p0 = (s ? cB : cA) * KL_CHUNK + part * NQ_E * 64;
+                KLInfo info;
+                bool mine;
+                const u64 kk = s ? chunk_rescan2<NQ_E>(d.gp1, d.pinfo1, 1, p0, posB, lane, &info, &mine)
+                                 : chunk_rescan2<NQ_E>(d.gp0, d.pinfo0, 0, p0, posA, lane, &info, &mine);
+                if (mine) {
+                    er_key[s * E_PARTS + part] = kk;
+                    er_info[s * E_PARTS + part] = info;
+                }
+            }
+            if constexpr (PROF) {
+                t_b = now();
+                pc[9] += t_b - t_a;  // the pair -> barrier 1 (W / early rescans)
+            }
+            __syncthreads();  // (1)
+            if constexpr (PROF) t_a = now();
+            if (s_stop[it & 1]) {
+                if (wv == W_FLIP && lane == 0) {  // the last swap's flip, for the sides written below
+                    atomicOr(&s_side[A >> 5], 1u << (A & 31));
+                    atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
+                }
+                ++it;
+                break;
+            }
+            const bool any_tag = s_stop[3] == tag;
+            if (wv == W_EA) {  // G2a, as in k_kl_swap_loop
+                const int s = half, cS = s ? cB : cA;
+                u64 rk[E_PARTS];
+                v4i rf[E_PARTS];
+#pragma unroll
+                for (int q = 0; q < E_PARTS; ++q) {
+                    rk[q] = er_key[s * E_PARTS + q];
+                    rf[q] = *reinterpret_cast<const v4i*>(er_info + s * E_PARTS + q);
+                }
+                const int cnt = ab_cnt[abp + s];
+                const int hs = hl < KL_AB_CAP ? hl : KL_AB_CAP - 1;
+                const u64 bk_raw = ab_key[s * KL_AB_CAP + hs];
+                const v4i bf = *reinterpret_cast<const v4i*>(ab_info + s * KL_AB_CAP + hs);
+                const bool have = hl < cnt && hl < KL_AB_CAP;
+                const u64 bk = have ? bk_raw : 0ull;
+                if (hl == 0) ab_cnt[2 - abp + s] = 0;  // the next swap's list (its G1 appends after barrier 2)
+                u64 R = rk[0];
+                v4i Rf = rf[0];
+#pragma unroll
+                for (int q = 1; q < E_PARTS; ++q) {
+                    const bool b = rk[q] > R;
+                    R = b ? rk[q] : R;
+                    Rf.x = b ? rf[q].x : Rf.x;
+                    Rf.y = b ? rf[q].y : Rf.y;
+                    Rf.z = b ? rf[q].z : Rf.z;
+                    Rf.w = b ? rf[q].w : Rf.w;
+                }
+                const int Rpos = int(~uint32_t(R & 0xffffffffull));
+                const bool stale = have && R != 0ull && bf.w == Rpos && bk < R;
+                const u64 hmask = s ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+                const bool st = (__ballot(stale) & hmask) != 0ull || cnt > KL_AB_CAP;
+                u64 m = 0ull;
+                if (__ballot(cnt > 0)) m = half_max_u64(bk);
+                if (!st) {
+                    if (m > R) {
+                        if (have && bk == m) {
+                            (s ? ck1 : ck0)[cS] = m;
+                            (s ? ckn1 : ckn0)[cS] = m;
+                            *reinterpret_cast<v4i*>((s ? ci1 : ci0) + cS) = bf;
+                        }
+                    } else if (hl == 0) {
+                        (s ? ck1 : ck0)[cS] = R;
+                        (s ? ckn1 : ckn0)[cS] = R;
+                        *reinterpret_cast<v4i*>((s ? ci1 : ci0) + cS) = Rf;
+                    }
+                }
+                const bool stA = __builtin_amdgcn_readlane(int(st), 0) != 0, stB = __builtin_amdgcn_readlane(int(st), 32) != 0;
+                for (int q = 0; q < 2; ++q) {
+                    if (!(q ? stB : stA)) continue;
+                    KLInfo info;
+                    bool mine;
+                    const u64 kk = q ? chunk_rescan(d.gp1, d.pinfo1, 1, cB, -1, lane, &info, &mine)
+                                     : chunk_rescan(d.gp0, d.pinfo0, 0, cA, -1, lane, &info, &mine);
+                    if (mine) {
+                        (q ? ck1 : ck0)[q ? cB : cA] = kk;
+                        (q ? ckn1 : ckn0)[q ? cB : cA] = kk;
+                        (q ? ci1 : ci0)[q ? cB : cA] = info;
+                    }
+                }
+            }
+            if (wv == W_FLIP && lane == 0) {  // the swap itself, for the next swap's lookups
+                atomicOr(&s_side[A >> 5], 1u << (A & 31));
+                atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
+                atomicOr(&s_lock[A >> 5], 1u << (A & 31));
+                atomicOr(&s_lock[B >> 5], 1u << (B & 31));
+            }
+            if (wv == W_EB || wv == W_EB - 1) {  // G2b
+                for (int i = (W_EB - wv) * 64 + lane; i < tot && i < KL_ITEM_CAP; i += 128) {
+                    const int cs = it_cs[i];
+                    const u64 kn = it_key[i];
+                    const int4 inf = *reinterpret_cast<const int4*>(it_info + i);
+                    if (cs == -1) continue;
+                    const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
+                    const u64 kmerged = (s ? ckn1 : ckn0)[c];
+                    const int dt = (s ? dtag1 : dtag0)[c];
+                    if ((s ? c == cB : c == cA) || dt == tag) continue;
+                    (s ? ck1 : ck0)[c] = kmerged;
+                    if (kmerged == kn) *reinterpret_cast<int4*>((s ? ci1 : ci0) + c) = inf;
+                }
+            }
+            // G2c. full rescans of the tagged chunks (the waves of this group, each claimed once)
+            for (int i = wv - NG; any_tag && i < tot; i += NW - NG) {
+                int cs;
+                if (i < KL_ITEM_CAP) cs = it_cs[i];
+                else {
+                    const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
+                    cs = locked_now(u) ? -1 : int((uint32_t(d.nd[u].c) & 0x80000000u) |
+                                                  ((uint32_t(d.nd[u].c) & 0x7fffffffu) / KL_CHUNK));
+                }
+                if (cs == -1) continue;
+                const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
+                if ((s ? dtag1 : dtag0)[c] != tag) continue;
+                int claimed = 0;
+                if (lane == 0) claimed = atomicMax(&(s ? ctag1 : ctag0)[c], tag) < tag;
+                if (!__shfl(claimed, 0, 64)) continue;
+                KLInfo info;
+                bool mine;
+                const u64 kk = s ? chunk_rescan(d.gp1, d.pinfo1, 1, c, -1, lane, &info, &mine)
+                                 : chunk_rescan(d.gp0, d.pinfo0, 0, c, -1, lane, &info, &mine);
+                if (mine) {
+                    (s ? ck1 : ck0)[c] = kk;
+                    (s ? ckn1 : ckn0)[c] = kk;
+                    (s ? ci1 : ci0)[c] = info;
+                }
+            }
+            arrive();  // (2), as a counter
+            if constexpr (PROF) pc[10] += now() - t_a;  // barrier 1 -> G2 done
+        }
+    }
+    if (fail) give_up();
+    __syncthreads();
+    for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
+    if (wv == W_W && lane == 0) {
+        out->iterations = it;
+        out->best_iter = best_it;
+        out->initial_cut = *d.cut0;
+        out->best_cut = best;
+        out->final_cut = cut;
+        out->status = sync[2] ? 3u : 2u;
+    }
+    if constexpr (PROF) {
+        // [0] speculations, [1] hits, [2] swaps, [3] gain wave 0 waiting for the pair, [4] its P, [5] its
+        // speculative rows, [6] pair -> barrier 1; W: [7] barrier-2 wait, [8] selection, [9] pair -> barrier 1;
+        // [10] W's G2 span, [11] G2a's; [12] loop cycles, [13] marker
+        if (wv == 0 && lane == 0)
+            for (int i = 0; i < 7; ++i) out->prof[i] = pc[i];
+        if (wv == W_W && lane == 0) {
+            for (int i = 7; i < 11; ++i) out->prof[i] = pc[i];
+            out->prof[12] = now() - t_start;
+            out->prof[13] = 0x9199ull;
+        }
+        if (wv == W_EA && lane == 0) out->prof[11] = pc[10];
+    } else if (tid == 0) {
+        for (int i = 0; i < 16; ++i) out->prof[i] = 0ull;
+    }
+}
+
+
 // The swap loop with its state in global memory: the fallback for graphs
 // whose bitmaps and chunk tables do not fit in LDS (and the A/B reference,
 // EK_KL_GLOBAL_STATE=1).  Four barriers per swap.  Only SMEM=false is launched.
@@ -1649,6 +2432,20 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
                            sink);
     }
     const bool prof = std::getenv("EK_KL_PROF") != nullptr;  // phase stamps: diagnostic instantiation
+    // the overlapped schedule (k_kl_swap_pipe); EK_KL_PIPE=0/1 forces it off/on
+    const char* pe = std::getenv("EK_KL_PIPE");
+    const bool pipe = pe && pe[0] ? pe[0] != '0' : false;
+    if (lds && pipe && !std::getenv("EK_KL_GLOBAL_STATE")) {
+        if (prof && d.segc)
+            hipLaunchKernelGGL((k_kl_swap_pipe<true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        else if (prof)
+            hipLaunchKernelGGL((k_kl_swap_pipe<true, false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        else if (d.segc)
+            hipLaunchKernelGGL((k_kl_swap_pipe<false, true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        else
+            hipLaunchKernelGGL((k_kl_swap_pipe<false, false>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
+        return;
+    }
     const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
     if (lds && !global_state && prof && d.segc)
         hipLaunchKernelGGL((k_kl_swap_loop<true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);

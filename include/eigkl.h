@@ -218,6 +218,13 @@ int ek_comm_stats(ek_ctx* ctx, int64_t* exchanges, int64_t* sends, int64_t* recv
  * + 16*nrows bytes over ek_spmv_bytes).  Measurement helper for bench.py's
  * size sweep; no reference counterpart. */
 int ek_spmv_bench(ek_ctx* ctx, int iters, int fused, double* avg_us);
+/* The gather-only ceiling of the context's SpMV (a roofline
+ * fraction read against its access pattern's own limit): back-to-back
+ * launches of a kernel with the SpMV's grid that streams the same matrix words
+ * (segments or column panels) and makes the same x and value-table gathers in
+ * the same order, summing the products in registers: no row reduction, no y,
+ * no epilogue.  *avg_us as in ek_spmv_bench.  No reference counterpart. */
+int ek_spmv_gather_bench(ek_ctx* ctx, int iters, double* avg_us);
 
 /* ------------------------------------------------------------------ */
 /* Lanczos / Fiedler: Spectra SymEigsSolver(op, 2, min(100,n/2)),        */

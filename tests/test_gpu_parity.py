@@ -187,14 +187,18 @@ def test_kl_random_init_synthetic(ek, oracle, ctx, mult, seed):
         assert res[k] == ores[k], k
 
 
-@pytest.mark.parametrize("mode", ["EK_KL_GLOBAL_STATE", "EK_KL_NOSEG", "EK_KL_NOSEGC"])
+@pytest.mark.parametrize("mode", ["EK_KL_GLOBAL_STATE", "EK_KL_NOSEG", "EK_KL_NOSEGC", "EK_KL_PIPE",
+                                  "EK_KL_PIPE+EK_KL_NOSEGC"])
 @pytest.mark.parametrize("name", ["ibm01", "industry2"])
 def test_kl_fallback_paths_bitexact(ek, oracle, ctx, monkeypatch, name, mode):
     # the global-state loop (graphs whose on-chip state does not fit LDS), the
     # LDS loop without inline neighbour rows (not enough memory for them) and
     # the plain (not weight-coded) inline rows (too many distinct weights) are
-    # forced here on shipped circuits; industry2 has rows of 910 entries
-    monkeypatch.setenv(mode, "1")
+    # forced here on shipped circuits; industry2 has rows of 910 entries.
+    # EK_KL_PIPE: the overlapped schedule (k_kl_swap_pipe, not the default:
+    # profiles/r06/kl), coded and plain inline rows
+    for m in mode.split("+"):
+        monkeypatch.setenv(m, "1")
     h = ek.Hypergraph.read(circuit_path(name))
     _, _, _, _, o0, o1 = ek.eig_read(eig_path(name), h.nodes)
     ctx.kl_graph_setup(h.kl_graph())
