@@ -1614,6 +1614,7 @@ struct Lanczos {
     bool pro = false;
     double pro_thresh = 0.0, pro_eps1 = 0.0;
     int pro_cgw = 0;  // ProLaunch::cgw (EK_PRO_CGW)
+    bool pro_cgw_env = false;  // EK_PRO_CGW set: no fitting to the resident grid
     // the decision inside the projection launch (no k_pro launch; needs the
     // projection's hand-off, upd_red 2).  EK_PRO_INLAUNCH=0: the k_pro launch
     bool proi = false;
@@ -1889,6 +1890,29 @@ struct Lanczos {
             pl.thresh = pro_thresh;
             pl.eps1 = pro_eps1;
             pl.cgw = pro_cgw;
+            // tickets (dispatch-order independence): a launch whose grid is
+            // not all resident at once takes them (pl.cap); EK_PRO_TICKETS=1
+            // on every launch, =0 on none (logical index = blockIdx: A/B)
+            static const int tickets = [] {
+                const char* e = std::getenv("EK_PRO_TICKETS");
+                return e && e[0] ? (e[0] == '0' ? 0 : 2) : 1;
+            }();
+            if (tickets) pl.tix = pro_pub() + size_t(ek::dev::PRO_PUB_WORDS) * ek::dev::PRO_PUB_STRIDE;
+            if (tickets == 1) {
+                pl.cap = ek::dev::gemvt_pro_capacity(nt, c->nrb_spmv > 12 * 256, pro_merge, pro_merge && b32,
+                                                     c->num_cu);
+                // the most workgroups per row block (<= pro_cgw) with which the
+                // cycle's widest launch is still resident at once: its launches
+                // then need no tickets (the headline: 8 -> 2, +0.2 ms a solve,
+                // against +1.0 ms for tickets on every launch;
+                // profiles/r06/dispatch_order_ab.txt)
+                const int ncg_max = (m + has_u0 + ek::dev::GT_COLS - 1) / ek::dev::GT_COLS;
+                auto grid = [&](int cg) { return ek::dev::gemvt_pro_grid(nrb, std::min(ncg_max, cg), ldv, pro_merge); };
+                int cg = pl.cgw;  // (0: one workgroup per tile, left as it is; EK_PRO_CGW: as set)
+                while (!pro_cgw_env && cg > 1 && grid(cg) > pl.cap) --cg;
+                if (!pro_cgw_env && cg > 0 && grid(cg) <= pl.cap) pl.cgw = cg;
+            }
+            pl.rev = std::getenv("EK_DISPATCH_REVERSE") ? 1 : 0;
             if (pro_merge) {
                 pl.merged = 1;
                 pl.npart = c->npart.as<double>();
@@ -2199,7 +2223,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
     // profiles/r05/pro/cgw_ab*.txt).  EK_PRO_CGW overrides (0: one workgroup
     // per tile)
     L.pro_cgw = std::max(8, 850 / std::max(1, L.nrb));
-    if (const char* e = std::getenv("EK_PRO_CGW"); e && e[0]) L.pro_cgw = std::atoi(e);
+    if (const char* e = std::getenv("EK_PRO_CGW"); e && e[0]) {
+        L.pro_cgw = std::atoi(e);
+        L.pro_cgw_env = true;
+    }
 
     const size_t ldv = size_t(L.ldv);
     c->V.ensure(ldv * size_t(m + 1) * 8);
@@ -2253,9 +2280,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         c->omega.ensure(3 * size_t(ek::dev::OMEGA_LD) * 8);
         c->prost.ensure(sizeof(ek::dev::ProState));
         // + the in-launch decision's words (PRO_PUB lines of 256 B), zero between launches
-        c->pflags.ensure(L.pro_pub_off() + size_t(ek::dev::PRO_PUB_WORDS) * 256);
+        // + the tickets of the in-launch jobs (8 lines of 256 B after them)
+        c->pflags.ensure(L.pro_pub_off() + size_t(ek::dev::PRO_PUB_WORDS + 8) * 256);
         HIPCHK(hipMemsetAsync(c->prost.p, 0, sizeof(ek::dev::ProState), s));
-        HIPCHK(hipMemsetAsync(L.pro_pub(), 0, size_t(ek::dev::PRO_PUB_WORDS) * 256, s));
+        HIPCHK(hipMemsetAsync(L.pro_pub(), 0, size_t(ek::dev::PRO_PUB_WORDS + 8) * 256, s));
     }
     // the step chunks' graphs (EK_LANCZOS_GRAPH=0: eager launches, A/B), kept
     // while every buffer and parameter their launches carry is unchanged

@@ -485,7 +485,23 @@ struct ProLaunch {
     int cgw = 0;
     int seg0 = 0, m = 0;
     double thresh = 0.0, eps1 = 0.0;
+    // dispatch-order independence: every workgroup takes its logical index
+    // from a ticket (8 counters by blockIdx % 8, PRO_PUB_STRIDE uints apart,
+    // zero before the launch; the last ticket of each re-arms it), so the
+    // jobs are handed out in dependency order whatever order the hardware
+    // dispatches the workgroups in.  null: logical index = blockIdx
+    unsigned* tix = nullptr;
+    int rev = 0;  // (test) the physical index reversed before anything else (EK_DISPATCH_REVERSE)
+    // > 0: workgroups of this kernel resident at once on the device; a launch
+    // whose grid fits is order-free by itself (every waiter's job is resident
+    // or runs as others finish), so it takes no tickets (gemvt_tt)
+    int cap = 0;
 };
+// resident capacity (workgroups) of the k_gemvt_pro instantiation gemvt_tt
+// launches for these flags on a device of num_cu compute units
+int gemvt_pro_capacity(bool nt, bool wide, bool merged, bool b32u, int num_cu);
+// the grid gemvt_tt launches with the in-launch decision (ncgl workgroups per row block)
+int gemvt_pro_grid(int nrb, int ncgl, int ldv, bool merged);
 // fn2_out[0] = sum(npart[0:nb]); if step >= 0: CGS2 (a3 == null):
 // alpha[step] = h1[step]+h2[step], offd[step] = h1[step-1]+h2[step-1]; three-term:
 // alpha[step] = *a3 + h2[step], offd[step] = sqrt(*fn2_i) + h2[step-1]

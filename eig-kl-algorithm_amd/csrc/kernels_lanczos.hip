@@ -390,10 +390,14 @@ __device__ __forceinline__ void gemvt_skip_tail(int ncols, int has_u0, int nrb, 
 
 // PROI: the step's decision is taken in this launch (ek_internal.hpp
 // ProLaunch); a poller's word, 1 + decision (thread 0)
-// Dispatch order: every wait here is on a workgroup with a LOWER index than
-// the waiter (the decider is block 0; the update's blocks follow the whole
-// projection), which relies on workgroups being dispatched in index order.
-// HIP does not promise that; the waits are therefore bounded, and *err (the
+// Dispatch order: every wait here is on a job with a LOWER logical index than
+// the waiter (the decider is job 0; the update's jobs follow the whole
+// projection).  With tickets (ProLaunch::tix, the default) a logical index is
+// handed out only after every lower one of its class, so no wait depends on
+// the order the hardware dispatches workgroups in; without them (EK_PRO_TICKETS
+// =0) the logical index is blockIdx and the waits rely on index-order
+// dispatch whenever the grid outgrows what is resident at once.  Either way
+// the waits are bounded, and *err (the
 // launch's ProState::timeouts, zero at the start of every solve) doubles as
 // an abort word: the first waiter that gives up counts itself there, and
 // every other waiter of the launch sees it within 256 polls and gives up too,
@@ -473,6 +477,28 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
     // PROI with pl.cgw: ncgl workgroups per row block walk the ncg groups
     const int ncgl = PROI && pl.cgw > 0 ? min(ncg, pl.cgw) : ncg;
     int nwg = int(gridDim.x), orig = int(blockIdx.x);
+    if constexpr (PROI) {
+        // The waits below are on jobs of LOWER logical index (the decider is
+        // job 0; the update's jobs follow every projection job).  With tickets
+        // (pl.tix) the logical index is the workgroup's place among the
+        // arrivals of its residue class, so a job is only handed out once every
+        // lower job of its class has been handed to a running workgroup: no
+        // wait can be on a workgroup that is not yet resident, in any dispatch
+        // order.  pl.rev (tests) reverses the physical index first.
+        if (pl.rev) orig = nwg - 1 - orig;
+        if (pl.tix) {
+            __shared__ int s_orig;
+            if (t == 0) {
+                const unsigned x = unsigned(orig) & 7u, cnt = (unsigned(nwg) - x + 7u) >> 3;
+                unsigned* q = pl.tix + PRO_PUB_STRIDE * x;
+                const unsigned j = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (j == cnt - 1u) __hip_atomic_store(q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+                s_orig = int(x + 8u * j);
+            }
+            __syncthreads();
+            orig = s_orig;
+        }
+    }
     if constexpr (PROI) PRO_STAMP(1);
     if constexpr (PROI) {
         // the decider: the first of 8 extra workgroups ahead of the map (the
@@ -835,8 +861,10 @@ __global__ __launch_bounds__(256) void k_gemvt(EK_GEMVT_PARAMS) {
 }
 // the projection with the in-launch decision (PROI); MRG: + the update's
 // workgroups (B32U: its fp32-shadow form)
+// (4 waves per SIMD: 128 VGPRs at most, four 256-thread workgroups per CU;
+// the tickets took the compiler's own choice to 129)
 template <bool NT, int APE, bool MRG, bool B32U>
-__global__ __launch_bounds__(256) void k_gemvt_pro(EK_GEMVT_PARAMS) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gemvt_pro(EK_GEMVT_PARAMS) {
     gemvt_body<true, NT, APE, true, MRG, B32U>(EK_GEMVT_ARGS);
 }
 #undef EK_GEMVT_PARAMS
@@ -1629,6 +1657,34 @@ void gemvt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_
                            h_out, nullptr, nullptr, ProLaunch{});
 }
 
+int gemvt_pro_grid(int nrb, int ncgl, int ldv, bool merged) {
+    return (EK_PRO_CG0_FIRST ? pro_slots(nrb) : nrb) * ncgl + 8 + (merged ? ldv / UPD_ROWS : 0);
+}
+
+int gemvt_pro_capacity(bool nt, bool wide, bool merged, bool b32u, int num_cu) {
+    int per = 0;
+#define EK_PRO_OCC(NT_, APE_, M_, B_)                                                                         \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_gemvt_pro<NT_, APE_, M_, B_>), \
+                                                       256, 0)
+#define EK_PRO_OCC_NT(APE_)                                     \
+    do {                                                        \
+        if (nt) {                                               \
+            if (!merged) EK_PRO_OCC(true, APE_, false, false);  \
+            else if (b32u) EK_PRO_OCC(true, APE_, true, true);  \
+            else EK_PRO_OCC(true, APE_, true, false);           \
+        } else {                                                \
+            if (!merged) EK_PRO_OCC(false, APE_, false, false); \
+            else if (b32u) EK_PRO_OCC(false, APE_, true, true); \
+            else EK_PRO_OCC(false, APE_, true, false);          \
+        }                                                       \
+    } while (0)
+    if (wide) EK_PRO_OCC_NT(24);
+    else EK_PRO_OCC_NT(12);
+#undef EK_PRO_OCC_NT
+#undef EK_PRO_OCC
+    return per * num_cu;
+}
+
 void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int has_u0, double u0val, int nreal,
               const double* w, const double* alpha, const double* vi, const double* vim1, const double* fn2_i,
               const double* bov_i, double* fp, double* part, float* v32col, const double* apart, int nparts,
@@ -1639,7 +1695,8 @@ void gemvt_tt(hipStream_t s, int ldv, int nrb, const double* V, int ncols, int h
     const dim3 g((pl && EK_PRO_CG0_FIRST ? pro_slots(nrb) : nrb) * ncgl + (pl ? 8 : 0) + (mrg ? ldv / UPD_ROWS : 0));
     // pl (PROI): the decision in this launch (8 more workgroups); alpha reduced by every
     // workgroup from apart (required) and published to pl->a3
-    const ProLaunch pv = pl ? *pl : ProLaunch{};
+    ProLaunch pv = pl ? *pl : ProLaunch{};
+    if (pv.tix && pv.cap > 0 && int(g.x) <= pv.cap) pv.tix = nullptr;  // the whole grid is resident: order-free
 #define EK_GEMVT_TT(KERNEL_)                                                                                           \
     hipLaunchKernelGGL(KERNEL_, g, dim3(256), 0, s, ldv, nrb, V, ncols, has_u0, u0val, nreal,                         \
                        w, part, apart ? nullptr : alpha, vi, vim1, fn2_i, bov_i, fp, (v32col || flag || pl) ? 1 : 0,   \

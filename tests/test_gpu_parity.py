@@ -465,6 +465,46 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     assert x[2] < 1e-8
 
 
+@pytest.mark.parametrize("which", ["ibm01", "headline"])
+def test_lanczos_inlaunch_waits_dispatch_order_free(ek, tmp_path, which):
+    """VERDICT r5 next-6.  The in-launch waits of the partially
+    reorthogonalised step (kernels_lanczos.hip gemvt_body, PROI): the
+    projection's column groups and the merged update's workgroups poll the
+    decider's words, the update's workgroups wait for the projection's done
+    counter.  Each waits on a job of lower logical index.  Such a launch is
+    free of any dispatch-order assumption when its whole grid is resident at
+    once (the default sizes the workgroups per row block so that it is: the
+    headline's 8 -> 2), and otherwise takes tickets: logical indices handed
+    out in arrival order per residue class.  Here the physical index is
+    reversed (EK_DISPATCH_REVERSE=1: job 0 would be the LAST workgroup
+    dispatched), in the default form, with 8 workgroups per row block (a
+    ~2,100-workgroup grid, twice what is resident, so its launches take
+    tickets) and with tickets on every launch; the solve must give the bits of
+    the plain launch every time, and so must the launch without tickets
+    (EK_PRO_TICKETS=0: logical index = blockIdx)."""
+    import subprocess
+    import sys
+    gen = {"ibm01": "ek.Hypergraph.read(circuit_path('ibm01'))",
+           "headline": "ek.Hypergraph.generate(1.15, 1).largest_component()[0]"}[which]
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); from conftest import load_package, circuit_path; "
+        "ek = load_package(); h = %s; c = ek.Context(0); c.spmv_setup_pins(h); lam, v, st = c.lanczos_fiedler(); "
+        "np.save(sys.argv[1], np.concatenate([[lam, st['matvecs'], st['residual'], st['projected_steps']], v]))"
+    ) % (os.path.dirname(os.path.abspath(__file__)), gen)
+    out = {}
+    rev = {"EK_DISPATCH_REVERSE": "1"}
+    for name, extra in (("plain", {}), ("reversed", rev), ("reversed_cgw8", dict(rev, EK_PRO_CGW="8")),
+                        ("reversed_tickets", dict(rev, EK_PRO_TICKETS="1")), ("no_tickets", {"EK_PRO_TICKETS": "0"})):
+        env = dict(os.environ, **extra)
+        f = str(tmp_path / f"{name}.npy")
+        subprocess.run([sys.executable, "-c", code, f], check=True, timeout=180, env=env)
+        out[name] = np.load(f)
+    x = out["plain"]
+    assert x[2] < 1e-8 and 0 < x[3] < x[1]
+    for name in out:
+        assert np.array_equal(out[name].view(np.uint64), x.view(np.uint64)), name
+
+
 @pytest.mark.parametrize("which", ["ibm01", "syn0.25"])
 def test_lanczos_pro_inlaunch_graph_replays(ek, tmp_path, which):
     """The in-launch decision (the projection's decider workgroup publishes
