@@ -212,6 +212,10 @@ struct ek_ctx {
     hipEvent_t chk_done[2] = {nullptr, nullptr}, chk_copied[2] = {nullptr, nullptr};
     hipEvent_t fin_ev = nullptr;  // the final Ritz vector's host copy landed
     double* chk_pin = nullptr;
+    // the checks' completion words (EK_CHK_POLL): one per slot, 256 B apart, in
+    // pinned host memory the check's gather writes last; the host polls them
+    unsigned* chk_word = nullptr;
+    unsigned chk_seq = 0;
     double* q_pin = nullptr;  // pinned staging of the restart's Q (MAX_NCV x (MAX_NCV + 1)), then the kept
                               // projected matrix for k_pro (2 x (MAX_NCV + 2))
     // the last Fiedler vector as returned (normalised, sign fixed), kept on
@@ -493,6 +497,7 @@ void ek_destroy(ek_ctx* c) {
     (void)hipStreamDestroy(c->kstream);
     (void)hipStreamDestroy(c->stream);
     if (c->chk_pin) (void)hipHostFree(c->chk_pin);
+    if (c->chk_word) (void)hipHostFree(c->chk_word);
     if (c->q_pin) (void)hipHostFree(c->q_pin);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
@@ -2345,6 +2350,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         }
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 4 * size_t(ek::dev::MAX_NCV + 2) * 8,
                              hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_word), 2 * 256, hipHostMallocCoherent));
+        std::memset(c->chk_word, 0, 2 * 256);
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
                              (size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) + 2 * size_t(ek::dev::MAX_NCV + 2)) * 8,
                              hipHostMallocDefault));
@@ -2411,6 +2418,33 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         const char* e = std::getenv("EK_CHK_KERNEL");
         return !(e && e[0] == '0');
     }();
+    // The mid-cycle check's gather on the compute stream itself, followed by
+    // a completion word the host polls (EK_CHK_POLL=0: the event on the
+    // compute stream, the gather on the copy stream, an event the host waits
+    // on).  The event was a barrier packet that drained the compute queue at
+    // every chunk boundary (~12 us each, ~57 a solve); a kernel in the stream
+    // is not.  The word is the gather's last store, made after every store of
+    // the slot is released to the system (k_chk_gather).
+    const bool chk_poll = chk_kernel && [] {
+        const char* e = std::getenv("EK_CHK_POLL");
+        return !(e && e[0] == '0');
+    }();
+    // the host's wait for a slot's completion word (bounded: a kernel that
+    // never ran must fail the solve, not hang the host)
+    auto chk_wait = [&](int sl, unsigned seq) {
+        volatile unsigned* w = c->chk_word + size_t(sl) * 64;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spin = 0; *w != seq; ++spin) {
+            if ((spin & 1023u) == 1023u) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
+                    ek::fail(EK_EHIP, "Lanczos: a mid-cycle check's completion word never arrived");
+                const hipError_t qe = hipStreamQuery(s);  // (a faulted stream ends the wait)
+                if (qe != hipSuccess && qe != hipErrorNotReady) HIPCHK(qe);
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    };
+    unsigned chk_seq_of[2] = {0u, 0u};
     bool cycle_reset = false;  // the restart already queued the resets below
     for (;;) {
         if (!cycle_reset) {
@@ -2455,7 +2489,14 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                 L.factorize(a, b);
                 launched = b;
                 int cur = -1;
-                if (b < m) {
+                if (b < m && chk_poll) {  // the gather in the stream, then its completion word
+                    double* pinned = L.chk_slot(slot);
+                    chk_seq_of[slot] = ++c->chk_seq;
+                    ek::dev::chk_gather(s, c->alpha.as<double>(), c->offd.as<double>(), c->fn2.as<double>(),
+                                        mr_step ? c->cflag.as<double>() : nullptr, b, m, L.CHK_FLAGS, pinned, -1,
+                                        c->chk_word + size_t(slot) * 64, chk_seq_of[slot]);
+                    cur = b - 1;
+                } else if (b < m) {
                     double* pinned = L.chk_slot(slot);
                     HIPCHK(hipEventRecord(c->chk_done[slot], s));
                     HIPCHK(hipStreamWaitEvent(c->cstream, c->chk_done[slot], 0));
@@ -2474,7 +2515,8 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                     cur = b - 1;  // complete: alpha, offd of steps < b - 1 (the fused finalize lags one step), fn2 <= b - 1
                 }
                 if (pend >= 0) {  // the previous chunk's check, while this chunk runs
-                    HIPCHK(hipEventSynchronize(c->chk_copied[pend_slot]));
+                    if (chk_poll) chk_wait(pend_slot, chk_seq_of[pend_slot]);
+                    else HIPCHK(hipEventSynchronize(c->chk_copied[pend_slot]));
                     const double* pa = L.chk_slot(pend_slot);
                     const int j = pend;
                     for (int i = from; i < j; ++i) {

@@ -439,9 +439,10 @@ struct ProState {
 };
 // dst[i], dst[m + i] (, dst[flags_off + i]) = alpha, offd (, flags) [i] for
 // i < b and dst[2m + i] = fn2[i] for i < bf (< 0: b): the mid-cycle check's
-// copy, one launch into pinned host memory
+// copy, one launch into pinned host memory.  done != null: then *done = seq
+// (system scope), after every store of the slot is released to the system
 void chk_gather(hipStream_t s, const double* alpha, const double* offd, const double* fn2, const double* flags, int b,
-                int m, size_t flags_off, double* dst, int bf = -1);
+                int m, size_t flags_off, double* dst, int bf = -1, unsigned* done = nullptr, unsigned seq = 0);
 // the implicit restart's uploads from pinned host staging in one launch:
 // qd[0:nq) = q_src, alpha[0:na) = kp[0:na) and offd[1:na) = kp[na+1:2na) when
 // kp != null, bov[0:nbov) = NaN (all-ones bits)

@@ -1812,7 +1812,8 @@ void pro_step(hipStream_t s, const double* apart, const double* wpart, int npart
 __global__ __launch_bounds__(256) void k_chk_gather(const double* __restrict__ alpha, const double* __restrict__ offd,
                                                     const double* __restrict__ fn2, const double* __restrict__ flags,
                                                     int b, int bf, int m, size_t flags_off,
-                                                    double* __restrict__ dst) {
+                                                    double* __restrict__ dst, unsigned* __restrict__ done,
+                                                    unsigned seq) {
     for (int i = int(threadIdx.x); i < bf; i += 256) {
         if (i < b) {
             dst[i] = alpha[i];
@@ -1821,12 +1822,21 @@ __global__ __launch_bounds__(256) void k_chk_gather(const double* __restrict__ a
         }
         dst[2 * m + i] = fn2[i];
     }
+    if (done) {
+        // the completion word the host polls instead of an event: every
+        // thread's stores to the pinned slot complete and are released to
+        // the system (vmcnt(0) + the system-scope fence) before the barrier,
+        // then one system-scope store of the sequence number
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 void chk_gather(hipStream_t s, const double* alpha, const double* offd, const double* fn2, const double* flags, int b,
-                int m, size_t flags_off, double* dst, int bf) {
+                int m, size_t flags_off, double* dst, int bf, unsigned* done, unsigned seq) {
     hipLaunchKernelGGL(k_chk_gather, dim3(1), dim3(256), 0, s, alpha, offd, fn2, flags, b, bf < 0 ? b : bf, m,
-                       flags_off, dst);
+                       flags_off, dst, done, seq);
 }
 
 // The implicit restart's uploads in ONE launch straight from the host's

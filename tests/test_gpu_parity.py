@@ -406,7 +406,7 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
                                     "EK_UPD_RED=2", "EK_V_NT=1", "pro:EK_UPD_RED=0", "pro:EK_UPD_RED=2",
                                     "pro:EK_V_NT=1", "pro:EK_PRO_INLAUNCH=0", "pro:EK_PRO_MERGE=0",
                                     "pro:EK_PRO_CGW=0", "pro:EK_PRO_CGW=1", "pro:EK_VQ_IB=8",
-                                    "pro:EK_CHK_FENCE=0"])
+                                    "pro:EK_CHK_FENCE=0", "pro:EK_CHK_POLL=0"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
@@ -427,8 +427,10 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
       block; EK_PRO_CGW=1: one per row block walking them all) against one
       workgroup per (row block, column group) tile (EK_PRO_CGW=0);
     * the restart's V Q with 8 basis rows in flight per trip (EK_VQ_IB=8)
-      against 16, and the mid-cycle check's chunk event with a system-scope
-      fence (EK_CHK_FENCE=0) against the device-scope default.
+      against 16, the mid-cycle check's chunk event with a system-scope
+      fence (EK_CHK_FENCE=0) against the device-scope one, and that event
+      path (EK_CHK_POLL=0) against the default gather in the compute stream
+      with a polled completion word.
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses.  These run the full
     reorthogonalisation (EK_REORTH=1); "plain:" runs both sides on the plain
