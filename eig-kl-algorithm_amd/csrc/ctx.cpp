@@ -1631,6 +1631,15 @@ struct Lanczos {
     float* V32() { return b32 ? c->V32.as<float>() : nullptr; }
     float* col32(int j) { return b32 ? c->V32.as<float>() + size_t(j) * ldv : nullptr; }
     int seg0 = 0;  // first step of the current run of steps (cycle start or injected vector)
+    // a mid-cycle check wanted at the end of the next factorize() chunk
+    // (chk_dst != null): factorize_fused folds its copy into the chunk's last
+    // SpMV (StepFin::chk_*) and sets chk_folded; other forms leave it to the
+    // k_chk_gather launch
+    double* chk_dst = nullptr;
+    unsigned* chk_word = nullptr;
+    const unsigned* chk_seq_src = nullptr;
+    int chk_b = 0;
+    bool chk_folded = false;
     // steps [k, kend) of a run that started at seg0 (the driver enqueues a
     // cycle in chunks to check convergence between them)
     void factorize(int k, int kend) {
@@ -1943,6 +1952,15 @@ struct Lanczos {
             }
             if (pro) fin.wpart = c->wpart.as<double>();  // ||w||^2 partials for k_pro (also at i == seg0)
             if (mrg) fin.pub_rearm = pro_pub();  // (the merged update's words and done counter)
+            if (chk_dst && i == kend - 1 && i > seg0) {  // the check's copy, in this SpMV's block 0
+                fin.chk_dst = chk_dst;
+                fin.chk_word = chk_word;
+                fin.chk_seq_src = chk_seq_src;
+                fin.chk_b = chk_b;
+                fin.chk_m = m;
+                fin.chk_fn2 = fn2;
+                chk_folded = true;
+            }
             const bool timed = spmv_timed_step(i);
             // the SpMV's last block also reduces alpha into a3 (k_three_term's bits)
             ek::dev::spmv(s, spmv_mat(c), c->f.as<double>(), c->w.as<double>(), fn2 + i, c->f.as<double>(), col(i),
@@ -2076,6 +2094,9 @@ struct Lanczos {
         } else {
             matvecs += kend - k;
             if (b32) u32_steps += kend - k;
+            // (the replayed launches carry the check's fold exactly when the
+            // captured ones did: factorize_fused's condition, constant per chunk)
+            if (chk_dst && kend - 1 > seg0) chk_folded = true;
         }
         HIPCHK(hipGraphLaunch(it->second, s));
     }
@@ -2350,8 +2371,10 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
         }
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_pin), 2 * 4 * size_t(ek::dev::MAX_NCV + 2) * 8,
                              hipHostMallocDefault));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_word), 2 * 256, hipHostMallocCoherent));
-        std::memset(c->chk_word, 0, 2 * 256);
+        // [slot * 64]: the completion words; [128 + slot * 64]: the sequence
+        // numbers the folded copy stores (written by the host before the chunk)
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->chk_word), 4 * 256, hipHostMallocCoherent));
+        std::memset(c->chk_word, 0, 4 * 256);
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->q_pin),
                              (size_t(ek::dev::MAX_NCV) * size_t(ek::dev::MAX_NCV + 1) + 2 * size_t(ek::dev::MAX_NCV + 2)) * 8,
                              hipHostMallocDefault));
@@ -2486,15 +2509,34 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
             int pend = -1, pend_slot = 0, slot = 0;
             while (a < m) {
                 const int b = std::min(m, a + chunk);
+                if (b < m && chk_poll) {  // this chunk ends with a check: its copy rides on the chunk's last SpMV
+                    chk_seq_of[slot] = ++c->chk_seq;
+                    c->chk_word[128 + size_t(slot) * 64] = chk_seq_of[slot];  // (read by the kernel at run time)
+                    L.chk_dst = L.chk_slot(slot);
+                    L.chk_word = c->chk_word + size_t(slot) * 64;
+                    L.chk_seq_src = c->chk_word + 128 + size_t(slot) * 64;
+                    L.chk_b = b;
+                    L.chk_folded = false;
+                    // EK_CHK_FOLD=1: the copy rides in block 0 of the chunk's last
+                    // SpMV instead of its own k_chk_gather launch (opt-in: same
+                    // bits, no measurable gain on the headline, r06w A/B)
+                    static const bool fold = [] {
+                        const char* e = std::getenv("EK_CHK_FOLD");
+                        return e && e[0] == '1';
+                    }();
+                    if (!fold || mr_step) L.chk_dst = nullptr, L.chk_folded = false;
+                }
                 L.factorize(a, b);
                 launched = b;
                 int cur = -1;
-                if (b < m && chk_poll) {  // the gather in the stream, then its completion word
-                    double* pinned = L.chk_slot(slot);
-                    chk_seq_of[slot] = ++c->chk_seq;
-                    ek::dev::chk_gather(s, c->alpha.as<double>(), c->offd.as<double>(), c->fn2.as<double>(),
-                                        mr_step ? c->cflag.as<double>() : nullptr, b, m, L.CHK_FLAGS, pinned, -1,
-                                        c->chk_word + size_t(slot) * 64, chk_seq_of[slot]);
+                if (b < m && chk_poll) {  // the chunk's last SpMV (or a gather after it), then the completion word
+                    if (!L.chk_folded) {
+                        ek::dev::chk_gather(s, c->alpha.as<double>(), c->offd.as<double>(), c->fn2.as<double>(),
+                                            mr_step ? c->cflag.as<double>() : nullptr, b, m, L.CHK_FLAGS,
+                                            L.chk_slot(slot), -1, c->chk_word + size_t(slot) * 64, chk_seq_of[slot]);
+                    }
+                    L.chk_dst = nullptr;
+                    L.chk_folded = false;
                     cur = b - 1;
                 } else if (b < m) {
                     double* pinned = L.chk_slot(slot);

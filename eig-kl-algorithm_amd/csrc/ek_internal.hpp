@@ -203,6 +203,18 @@ struct StepFin {
     // projection's decision words + done counter, zeroed by block 0
     float* v32col = nullptr;
     unsigned* pub_rearm = nullptr;
+    // the Lanczos mid-cycle check's copy, folded into the chunk's last SpMV
+    // (ctx.cpp chk_poll): block 0, once its finalize has published, copies
+    // alpha / offd [0, chk_b) and fn2 [0, chk_b) into the pinned slot chk_dst
+    // (alpha at 0, offd at chk_m, fn2 at 2 chk_m), releases them to the
+    // system and stores chk_seq to *chk_word, which the host polls
+    double* chk_dst = nullptr;
+    unsigned* chk_word = nullptr;
+    const double* chk_fn2 = nullptr;  // the fn2 array (fn2_out points at its entry `step + 1`)
+    // the sequence number to store, read at run time from pinned host memory
+    // the host sets before the launch (a captured graph replays the pointer)
+    const unsigned* chk_seq_src = nullptr;
+    int chk_b = 0, chk_m = 0;
 };
 
 // kernels_spmv.hip — CSR-adaptive fp64 SpMV (row blocks precomputed on host)

@@ -30,6 +30,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include "ek_device.hpp"
 #include "ek_internal.hpp"
 
 namespace ek {
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(PT) void k_spmv_panel(SpmvPanel m, const double* __
             }
         }
     }
+    if (fin.chk_dst && w == 0) chk_mirror(fin, t, PT);  // (the check's copy: workgroup 0 only)
     const double scale = (fn2 || fin.npart) ? (n2 > 0.0 ? 1.0 / sqrt(n2) : 0.0) : 1.0;
     double av = 0.0, wv = 0.0;
     for (int r = t; r < nr; r += PT) {

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstring>
 
+#include "ek_device.hpp"
 #include "ek_internal.hpp"
 
 namespace ek {
@@ -195,6 +196,7 @@ __global__ __launch_bounds__(SPMV_THREADS, EK_SPMV_WAVES) void k_spmv_adaptive(c
 
     if (LONG && cnt > BLOCK_NNZ) {  // vector mode: single long row
         const double scale = scale_of(norm2());
+        if (fin.chk_dst && blockIdx.x == 0) chk_mirror(fin, t, SPMV_THREADS);
         double s = 0.0;
         const uint32_t cmask = (1u << colbits) - 1u;
         const int olo = fin.own_lo, ohi = fin.own_hi;  // (the halo SpMV: the own slot's entries are 0)
@@ -270,6 +272,7 @@ __global__ __launch_bounds__(SPMV_THREADS, EK_SPMV_WAVES) void k_spmv_adaptive(c
         for (int u = 0; u < PER; ++u) xv[u] = ci[u] >= 0 ? x[ci[u]] : 0.0;
     }
     const double scale = scale_of(norm2());  // overlaps the gathers in flight
+    if (fin.chk_dst && blockIdx.x == 0) chk_mirror(fin, t, SPMV_THREADS);  // (the check's copy: block 0 only)
     if (t <= nr) rbeg[t] = rb0;
     if (t == 0 && nr == SPMV_THREADS) rbeg[SPMV_THREADS] = rb1;
 #pragma unroll

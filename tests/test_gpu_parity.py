@@ -406,7 +406,8 @@ def test_lanczos_basis32_synthetic_breakdowns(ek, ctx, which):
                                     "EK_UPD_RED=2", "EK_V_NT=1", "pro:EK_UPD_RED=0", "pro:EK_UPD_RED=2",
                                     "pro:EK_V_NT=1", "pro:EK_PRO_INLAUNCH=0", "pro:EK_PRO_MERGE=0",
                                     "pro:EK_PRO_CGW=0", "pro:EK_PRO_CGW=1", "pro:EK_VQ_IB=8",
-                                    "pro:EK_CHK_FENCE=0", "pro:EK_CHK_POLL=0"])
+                                    "pro:EK_CHK_FENCE=0", "pro:EK_CHK_POLL=0",
+                                    "pro:EK_CHK_FOLD=1"])
 def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     """Device-side restructurings give the bits of the forms they replace:
     * the single-GPU step without the three-term launch (alpha reduced by the
@@ -429,8 +430,9 @@ def test_lanczos_device_paths_bit_identical(ek, tmp_path, which, switch):
     * the restart's V Q with 8 basis rows in flight per trip (EK_VQ_IB=8)
       against 16, the mid-cycle check's chunk event with a system-scope
       fence (EK_CHK_FENCE=0) against the device-scope one, and that event
-      path (EK_CHK_POLL=0) against the default gather in the compute stream
-      with a polled completion word.
+      path (EK_CHK_POLL=0) against the default polled completion word, and
+      that word's copy folded into block 0 of the chunk's last SpMV
+      (EK_CHK_FOLD=1, graph replays included) against its own launch.
     syn0.25 goes through breakdowns (injected vectors, beta = 0) and restarts,
     syn2 through restarts whose residual collapses.  These run the full
     reorthogonalisation (EK_REORTH=1); "plain:" runs both sides on the plain
