@@ -1369,12 +1369,43 @@ int ek_spmv_gather_bench(ek_ctx* c, int iters, double* avg_us) {
     for (size_t i = 0; i < X; ++i) h[i] = double((i * 2654435761u) % 1000u) / 1000.0 - 0.5;
     HIPCHK(hipMemcpyAsync(x.p, h.data(), X * 8, hipMemcpyHostToDevice, s));
     const auto m = spmv_mat(c);
-    for (int i = 0; i < 10; ++i) ek::dev::spmv_gather_only(s, m, x.as<double>(), sink.as<double>());
+    // EK_GATHER_MODE (lab, kernels_spmv.hip k_lab_gather_step): 1 the gather +
+    // a skipped step's update as two launches, 2 as one grid with an in-launch
+    // wait, 3 the update alone; 0 (default) the gather-only ceiling
+    const char* gm = std::getenv("EK_GATHER_MODE");
+    const int mode = gm ? std::atoi(gm) : 0;
+    DBuf part, ctr, wv, fv, fpart;
+    const int R = int(std::max<int64_t>(c->nrows, 1));
+    if (mode) {
+        if (mode < 0 || mode > 3 || !m.pk || m.panel.G > 0 || c->mr)
+            ek::fail(EK_EINVAL, "EK_GATHER_MODE %d: the single-context coded CSR form only", mode);
+        if (mode == 2 && m.nblocks > ek::dev::lab_step_capacity())
+            ek::fail(EK_EINVAL, "EK_GATHER_MODE 2: %d blocks exceed the %d resident at once", m.nblocks,
+                     ek::dev::lab_step_capacity());
+        part.ensure(size_t(m.nblocks) * 8);
+        ctr.ensure(66 * 64 * 4);
+        wv.ensure(size_t(R) * 3 * 8);
+        fv.ensure(size_t(R) * 8);
+        fpart.ensure(size_t(m.nblocks) * 8);
+        HIPCHK(hipMemsetAsync(part.p, 0, part.bytes, s));
+        HIPCHK(hipMemsetAsync(ctr.p, 0, ctr.bytes, s));
+        HIPCHK(hipMemsetAsync(wv.p, 0, wv.bytes, s));
+    }
+    unsigned gen = 0;
+    auto launch = [&] {
+        if (!mode) return ek::dev::spmv_gather_only(s, m, x.as<double>(), sink.as<double>());
+        ++gen;
+        const double* w = wv.as<double>();
+        ek::dev::lab_gather_step(s, m, mode, x.as<double>(), part.as<double>(), ctr.as<unsigned>(),
+                                 gen, R, w, w + R, w + 2 * size_t(R), fv.as<double>(),
+                                 fpart.as<double>());
+    };
+    for (int i = 0; i < 10; ++i) launch();
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, s));
-    for (int i = 0; i < iters; ++i) ek::dev::spmv_gather_only(s, m, x.as<double>(), sink.as<double>());
+    for (int i = 0; i < iters; ++i) launch();
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;

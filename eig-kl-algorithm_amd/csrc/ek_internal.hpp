@@ -296,6 +296,13 @@ constexpr int ALPHA_SUB = 32;  // first-level counters of the SpMV's last-block 
 // value gathers with nothing else (ek_spmv_gather_bench); sink: never written
 // in practice (>= one double per workgroup)
 void spmv_gather_only(hipStream_t s, const SpmvMat& m, const double* x, double* sink);
+// (lab) the skipped step's SpMV + update as two launches (mode 1) or one grid
+// with an in-launch wait (mode 2; needs nblocks <= lab_step_capacity()), or the
+// update alone (mode 3): ek_spmv_gather_bench's EK_GATHER_MODE
+int lab_step_capacity();
+void lab_gather_step(hipStream_t s, const SpmvMat& m, int mode, const double* x, double* part, unsigned* ctr,
+                     unsigned target, int n, const double* w, const double* v, const double* u, double* f,
+                     double* fpart);
 void spmv(hipStream_t s, const SpmvMat& m, const double* x, double* y, const double* fn2, const double* f,
           double* vcol, double* apart, const StepFin* fin = nullptr, hipEvent_t ev_start = nullptr,
           hipEvent_t ev_stop = nullptr, double* alpha_out = nullptr, unsigned* actr = nullptr);

@@ -410,6 +410,133 @@ __global__ __launch_bounds__(SPMV_THREADS) void k_spmv_gather_only(const int4* _
     if (acc == -1.2345e300 && rb == 7) sink[blockIdx.x] = acc;  // (keeps every load; never true in practice)
 }
 
+// (lab: VERDICT r5 next-4's single-grid question, ek_spmv_gather_bench with
+// EK_GATHER_MODE 1-3) A skipped Lanczos step is the SpMV, then a launch that
+// reduces the SpMV's per-block partials (alpha) and updates every row
+// elementwise (f = w - alpha v - beta u, with ||f||^2 partials).  Fusing the two
+// into one grid replaces that kernel boundary by an in-launch grid-wide wait:
+// every block's partial must be in before any block may update.  These lab
+// kernels price the two forms on the product's grid and access pattern:
+// k_lab_gather_step<false> + k_lab_step (mode 1: the boundary) against
+// k_lab_gather_step<true> (mode 2: the wait; all blocks resident, counted by
+// the host), and k_lab_step alone (mode 3: the update's own time).  The
+// partials travel as agent-scope stores and loads and the arrival count is a
+// relaxed add after vmcnt(0), the product's hand-off idiom (EK_HANDOFF_ORDER).
+__device__ __forceinline__ double lab_block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int t = threadIdx.x;
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int i = 0; i < SPMV_THREADS / 64; ++i) r += red[i];
+    __syncthreads();
+    return r;
+}
+__device__ __forceinline__ void lab_step_body(const double* part, int G, int n, const double* w, const double* v,
+                                              const double* u, double* f, double* fpart, double beta, double* red) {
+    const int t = threadIdx.x;
+    double a = 0.0;
+    for (int i = t; i < G; i += SPMV_THREADS)
+        a += __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double alpha = lab_block_sum(a, red);
+    const int per = (n + int(gridDim.x) - 1) / int(gridDim.x);
+    const int r0 = int(blockIdx.x) * per, r1 = min(n, r0 + per);
+    double q = 0.0;
+    for (int i = r0 + t; i < r1; i += SPMV_THREADS) {
+        const double fi = w[i] - alpha * v[i] - beta * u[i];
+        f[i] = fi;
+        q += fi * fi;
+    }
+    q = lab_block_sum(q, red);
+    if (t == 0) fpart[blockIdx.x] = q;
+}
+template <bool WAIT>
+__global__ __launch_bounds__(SPMV_THREADS) void k_lab_gather_step(const int4* __restrict__ desc,
+                                                                  const int32_t* __restrict__ col,
+                                                                  const double* __restrict__ val, int colbits,
+                                                                  const uint16_t* __restrict__ rel,
+                                                                  const double* __restrict__ x, double* part,
+                                                                  unsigned* ctr, unsigned target, int n,
+                                                                  const double* w, const double* v, const double* u,
+                                                                  double* f, double* fpart) {
+    __shared__ double red[SPMV_THREADS / 64];
+    constexpr int PER = SPMV_SEG_NNZ / SPMV_THREADS;
+    const int t = threadIdx.x;
+    const uint32_t cmask = (1u << colbits) - 1u;
+    uint32_t wd[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) wd[k] = uint32_t(col[size_t(blockIdx.x) * SPMV_SEG_NNZ + t + k * SPMV_THREADS]);
+    const int rb = rel[size_t(blockIdx.x) * SPMV_REL_STRIDE + t];
+    const int4 dsc = desc[blockIdx.x];
+    double acc = 0.0;
+    if (dsc.w > SPMV_SEG_NNZ) {
+        for (int i = t; i < dsc.w; i += SPMV_THREADS) {
+            const uint32_t wv = uint32_t(col[dsc.z + i]);
+            acc += val[wv >> colbits] * x[wv & cmask];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) acc += val[wd[k] >> colbits] * x[wd[k] & cmask];
+    }
+    acc += double(rb) * 0.0;
+    const double bs = lab_block_sum(acc, red);
+    if (t == 0) __hip_atomic_store(part + blockIdx.x, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (WAIT) {
+        // two-level arrival (one counter for every block serialises ~2k adds
+        // on one line): block b adds to sub-counter b % 32 (64 uints apart);
+        // the last of a sub adds to the top counter; the last of those stores
+        // the generation into 32 flag lines, each polled by its sub's blocks
+        if (t == 0) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the partial is stored before the arrival
+            const unsigned G = gridDim.x, sub = blockIdx.x & 31u, nsub = G < 32u ? G : 32u;
+            const unsigned per = (G - sub + 31u) / 32u;  // blocks of this sub
+            const unsigned old = __hip_atomic_fetch_add(ctr + 64 * (1 + sub), 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1u == target * per) {
+                const unsigned top = __hip_atomic_fetch_add(ctr, 1u, EK_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT);
+                if (top + 1u == target * nsub)
+                    for (unsigned q = 0; q < nsub; ++q)
+                        __hip_atomic_store(ctr + 64 * (33 + q), target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            while (__hip_atomic_load(ctr + 64 * (33 + sub), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+                __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();
+        lab_step_body(part, int(gridDim.x), n, w, v, u, f, fpart, 0.5, red);
+    }
+}
+__global__ __launch_bounds__(SPMV_THREADS) void k_lab_step(const double* part, int G, int n, const double* w,
+                                                           const double* v, const double* u, double* f,
+                                                           double* fpart) {
+    __shared__ double red[SPMV_THREADS / 64];
+    lab_step_body(part, G, n, w, v, u, f, fpart, 0.5, red);
+}
+
+int lab_step_capacity() {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_lab_gather_step<true>),
+                                                     SPMV_THREADS, 0) != hipSuccess)
+        return 0;
+    return per * cus;
+}
+
+void lab_gather_step(hipStream_t s, const SpmvMat& m, int mode, const double* x, double* part, unsigned* ctr,
+                     unsigned target, int n, const double* w, const double* v, const double* u, double* f,
+                     double* fpart) {
+    const int4* d = reinterpret_cast<const int4*>(m.desc);
+    const int32_t* pk = reinterpret_cast<const int32_t*>(m.pk);
+    if (mode == 1 || mode == 2) {
+        if (mode == 2)
+            hipLaunchKernelGGL((k_lab_gather_step<true>), dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, d, pk, m.dict,
+                               m.colbits, m.rel, x, part, ctr, target, n, w, v, u, f, fpart);
+        else
+            hipLaunchKernelGGL((k_lab_gather_step<false>), dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, d, pk, m.dict,
+                               m.colbits, m.rel, x, part, ctr, target, n, w, v, u, f, fpart);
+    }
+    if (mode == 1 || mode == 3)
+        hipLaunchKernelGGL(k_lab_step, dim3(m.nblocks), dim3(SPMV_THREADS), 0, s, part, m.nblocks, n, w, v, u, f, fpart);
+}
+
 void spmv_gather_only(hipStream_t s, const SpmvMat& m, const double* x, double* sink) {
     if (m.panel.G > 0) {
         panel_gather_only(s, m.panel, m.dict, x, sink);
