@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <chrono>
 #include <memory>
+#include <mutex>
 #include <cmath>
 #include <cstring>
 #include <filesystem>
@@ -86,8 +87,11 @@ struct CtxInit {
             if (rc != EK_OK) err = ek_last_error();
         });
     }
+    std::once_flag joined;  // get() is called from the solve's thread and the KL adjacency's
     ek_ctx* get() {
-        if (th.joinable()) th.join();
+        std::call_once(joined, [this] {
+            if (th.joinable()) th.join();
+        });
         if (rc != EK_OK) throw Fail{"GPU init: " + err};
         return ctx;
     }

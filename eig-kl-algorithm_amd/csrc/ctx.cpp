@@ -220,7 +220,7 @@ struct ek_ctx {
                               // projected matrix for k_pro (2 x (MAX_NCV + 2))
     // the last Fiedler vector as returned (normalised, sign fixed), kept on
     // the device for ek_kl_set_partition_fiedler, and that split's scratch
-    DBuf fied, sp_sorted, sp_flag, sp_pos, sp_tmp;
+    DBuf fied, sp_out, sp_tmp;
     int64_t fied_n = 0;
 };
 
@@ -2494,6 +2494,9 @@ extern "C" int ek_lanczos_fiedler(ek_ctx* c, const ek_lanczos_opts* opts, double
                     ek::fail(EK_EHIP, "Lanczos: a mid-cycle check's completion word never arrived");
                 const hipError_t qe = hipStreamQuery(s);  // (a faulted stream ends the wait)
                 if (qe != hipSuccess && qe != hipErrorNotReady) HIPCHK(qe);
+                if (qe == hipSuccess && *w != seq)  // (the stream drained: the word can no longer arrive)
+                    ek::fail(EK_EHIP, "Lanczos: the stream finished without a mid-cycle check's completion word "
+                                      "(slot %d: %u, expected %u)", sl, *w, seq);
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
@@ -3209,33 +3212,31 @@ int ek_kl_set_partition_fiedler(ek_ctx* c, double* median_out, int64_t* n0_out, 
     hipStream_t s = c->stream;
     const int ni = int(n);
     const double* v = c->fied.as<double>();
-    c->sp_sorted.ensure(size_t(n) * 8);
-    c->sp_flag.ensure(size_t(n) * 4);
-    c->sp_pos.ensure(size_t(n) * 4);
     const size_t tb = ek::dev::split_tmp_bytes(ni);
     c->sp_tmp.ensure(tb);
+    c->sp_out.ensure(64);
     // the median: ranks n/2 (and n/2 - 1 for even n, their mean), the values
-    // nth_element gives ek_median_split
-    ek::dev::split_sort(s, c->sp_tmp.p, tb, v, c->sp_sorted.as<double>(), ni);
-    const size_t hi = size_t(n / 2);
-    double mid[2] = {0.0, 0.0};
-    HIPCHK(hipMemcpyAsync(mid, c->sp_sorted.as<double>() + (n % 2 == 0 ? hi - 1 : hi), 2 * 8,
-                          hipMemcpyDeviceToHost, s));
+    // nth_element gives ek_median_split (a radix select on the device)
+    const unsigned hi = unsigned(n / 2), lo = n % 2 == 0 ? hi - 1 : hi;
+    auto* keys = c->sp_out.as<unsigned long long>();
+    ek::dev::split_select(s, c->sp_tmp.p, v, ni, lo, hi, keys);
+    unsigned long long kk[2] = {0ull, 0ull};
+    HIPCHK(hipMemcpyAsync(kk, keys, 16, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    const double mid[2] = {ek::dev::key_value(kk[0]), ek::dev::key_value(kk[1])};
     const double med = n % 2 == 0 ? (mid[0] + mid[1]) / 2.0 : mid[0];
     c->kl_order0.ensure(size_t(n) * 4);
     c->kl_order1.ensure(size_t(n) * 4);
     c->kl_side_init.ensure(size_t(n));
     c->kl_plist.ensure(size_t(n) * 4);
-    ek::dev::split_flags_scan(s, c->sp_tmp.p, tb, v, ni, med, c->sp_flag.as<uint32_t>(), c->sp_pos.as<uint32_t>());
-    ek::dev::split_scatter(s, v, c->sp_pos.as<uint32_t>(), ni, med, c->kl_order0.as<int32_t>(),
-                           c->kl_order1.as<int32_t>(), c->kl_plist.as<uint32_t>(), c->kl_side_init.as<uint8_t>());
+    unsigned* n0_dev = reinterpret_cast<unsigned*>(c->sp_out.as<unsigned long long>() + 2);
+    ek::dev::split_partition(s, c->sp_tmp.p, v, ni, med, c->kl_order0.as<int32_t>(), c->kl_order1.as<int32_t>(),
+                             c->kl_plist.as<uint32_t>(), c->kl_side_init.as<uint8_t>(), n0_dev);
     HIPCHK(hipGetLastError());
-    uint32_t last[2] = {0, 0};  // pos0[n-1], flag0[n-1]
-    HIPCHK(hipMemcpyAsync(&last[0], c->sp_pos.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&last[1], c->sp_flag.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+    unsigned n0u = 0;
+    HIPCHK(hipMemcpyAsync(&n0u, n0_dev, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const int64_t n0 = int64_t(last[0]) + int64_t(last[1]);
+    const int64_t n0 = int64_t(n0u);
     partition_on_device(c, n0, n - n0);
     if (median_out) *median_out = med;
     if (n0_out) *n0_out = n0;

@@ -543,11 +543,15 @@ void zero_pad_rows(hipStream_t s, double* V, int ldv, int nreal, int ncols);
 // device median split of the Fiedler vector (kernels_kl.hip)
 size_t split_tmp_bytes(int n);
 void fiedler_scale(hipStream_t s, const double* x, double sgn, int n, double* out);
-void split_sort(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, double* sorted, int n);
-void split_flags_scan(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, int n, double med, uint32_t* flag0,
-                      uint32_t* pos0);
-void split_scatter(hipStream_t s, const double* v, const uint32_t* pos0, int n, double med, int32_t* order0,
-                   int32_t* order1, uint32_t* plist, uint8_t* side);
+// the sort keys of the values at ranks k0 and k1 of v (radix select) into
+// keys_out[0..1] (device); key_value turns a key back into its double
+void split_select(hipStream_t s, void* tmp, const double* v, int n, unsigned k0, unsigned k1,
+                  unsigned long long* keys_out);
+double key_value(unsigned long long key);
+// the remain[] lists, plist and initial sides of the split at med; n0_out
+// (device): the side-0 count
+void split_partition(hipStream_t s, void* tmp, const double* v, int n, double med, int32_t* order0, int32_t* order1,
+                     uint32_t* plist, uint8_t* side, unsigned* n0_out);
 // f = f*sigma + x*hk ; per-block sum of f^2 -> npart
 void axpby_norm(hipStream_t s, int ldv, double* f, double sigma, const double* x, double hk, double* npart);
 // x = x / sqrt(*n2) ... and deflate helpers

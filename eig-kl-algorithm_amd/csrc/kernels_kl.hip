@@ -29,7 +29,6 @@
 //                     N(node1) u N(node2) (one lane per row), re-key only the
 //                     chunks those nodes live in.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cfloat>
 #include <algorithm>
@@ -2493,68 +2492,223 @@ __global__ __launch_bounds__(256) void k_fiedler_scale(const double* __restrict_
     if (i < n) out[i] = x[i] * sgn;
 }
 
-// flag0[i] = 1 for a node on side 0: !(med > v[i]) is bit 0 of ek_median_split
-__global__ __launch_bounds__(256) void k_split_flags(const double* __restrict__ v, int n, double med,
-                                                     uint32_t* __restrict__ flag0) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) flag0[i] = med > v[i] ? 0u : 1u;
+// The median's two ranks by a radix select (no sort): the fp64 values as the
+// ordered 64-bit keys of a radix sort (sign flipped, negatives inverted: -0
+// before +0, exactly a radix sort's order), eight passes of one byte from the
+// top.  A pass histograms the byte of the keys that match the prefix found so
+// far (LDS bins, then agent-scope adds into that pass's 256 global bins); its
+// last block to finish (two-level arrival counter) scans the bins, extends the
+// prefix by the byte holding the rank and subtracts the keys below it.  Both
+// ranks (n/2 - 1 and n/2 of an even n) are selected in the same passes.  The
+// keys come out identical to a full sort's entries at those ranks.
+constexpr int SEL_THREADS = 256, SEL_PER = 8, SEL_PASSES = 8;
+constexpr int SEL_SUB = 16;  // first-level arrival counters, 64 uints apart
+struct SelState {
+    unsigned long long prefix[2], mask[2];
+    unsigned k[2];
+    unsigned pad[2];
+    unsigned hist[SEL_PASSES][2][256];
+    unsigned ctr[(SEL_SUB + 1) * 64];
+};
+
+__device__ __forceinline__ unsigned long long ord_key(double v) {
+    const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(v));
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
-// remain[] lists in node order (cKL.cpp:155-174) from the exclusive scan of
-// the side-0 flags: position pos0[i] in list 0, or i - pos0[i] in list 1;
-// plist and the initial sides as ek_kl_set_partition builds them
-__global__ __launch_bounds__(256) void k_split_scatter(const double* __restrict__ v, const uint32_t* __restrict__ pos0,
-                                                       int n, double med, int32_t* __restrict__ order0,
-                                                       int32_t* __restrict__ order1, uint32_t* __restrict__ plist,
-                                                       uint8_t* __restrict__ side) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const bool one = med > v[i];
-    const uint32_t p0 = pos0[i];
-    if (one) {
-        const uint32_t p1 = uint32_t(i) - p0;
-        order1[p1] = i;
-        plist[i] = p1 | 0x80000000u;
-    } else {
-        order0[p0] = i;
-        plist[i] = p0;
+__global__ __launch_bounds__(SEL_THREADS) void k_select_init(SelState* st, unsigned k0, unsigned k1) {
+    // (the histograms and counters are zeroed by the host's memset)
+    if (threadIdx.x < 2) {
+        st->prefix[threadIdx.x] = 0ull;
+        st->mask[threadIdx.x] = 0ull;
+        st->k[threadIdx.x] = threadIdx.x ? k1 : k0;
     }
-    side[i] = one ? 1 : 0;
 }
 
-#define SPLIT_CHK(call)                                                                            \
-    do {                                                                                           \
-        const hipError_t e_ = (call);                                                              \
-        if (e_ != hipSuccess) ek::fail(EK_EHIP, "%s failed: %s", #call, hipGetErrorString(e_));    \
-    } while (0)
+__global__ __launch_bounds__(SEL_THREADS) void k_select_pass(const double* __restrict__ v, int n, SelState* st,
+                                                             int pass, unsigned long long* keys_out) {
+    __shared__ unsigned h[2][256];
+    __shared__ int s_last;
+    const int t = threadIdx.x;
+    h[0][t] = 0u;
+    h[1][t] = 0u;
+    const unsigned long long p0 = st->prefix[0], m0 = st->mask[0], p1 = st->prefix[1], m1 = st->mask[1];
+    const int shift = 56 - 8 * pass;
+    __syncthreads();
+    const int base = int(blockIdx.x) * SEL_THREADS * SEL_PER;
+#pragma unroll
+    for (int u = 0; u < SEL_PER; ++u) {
+        const int i = base + u * SEL_THREADS + t;
+        if (i < n) {
+            const unsigned long long key = ord_key(v[i]);
+            const unsigned d = unsigned(key >> shift) & 255u;
+            if ((key & m0) == p0) atomicAdd(&h[0][d], 1u);
+            if ((key & m1) == p1) atomicAdd(&h[1][d], 1u);
+        }
+    }
+    __syncthreads();
+    for (int r = 0; r < 2; ++r)
+        if (h[r][t]) __hip_atomic_fetch_add(&st->hist[pass][r][t], h[r][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every thread's adds performed before the block arrives
+    __syncthreads();
+    if (t == 0) {
+        const unsigned nb = gridDim.x, g = blockIdx.x % SEL_SUB;
+        const unsigned gsize = (nb - g + SEL_SUB - 1) / SEL_SUB, ngroups = nb < SEL_SUB ? nb : SEL_SUB;
+        s_last = 0;
+        if (__hip_atomic_fetch_add(st->ctr + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u)
+            s_last = __hip_atomic_fetch_add(st->ctr + SEL_SUB * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     ngroups - 1u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the last block: every bin's total, then the byte holding each rank (one
+    // wave per rank: an inclusive scan of its 256 bins, 4 per lane)
+    if (t < SEL_SUB + 1) st->ctr[t * 64] = 0u;  // re-armed for the next pass
+    const int w = t >> 6, l = t & 63;
+    if (w < 2) {
+        unsigned c[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            c[q] = __hip_atomic_load(&st->hist[pass][w][4 * l + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sum += c[q];
+        }
+        unsigned incl = sum;  // inclusive scan of the lanes' sums
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(incl, o, 64);
+            if (l >= o) incl += y;
+        }
+        const unsigned k = st->k[w];
+        unsigned below = incl - sum;  // keys in the bins of the lanes before this one
+        int dsel = -1;
+        unsigned bsel = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (dsel < 0 && k >= below && k < below + c[q]) {
+                dsel = 4 * l + q;
+                bsel = below;
+            }
+            below += c[q];
+        }
+        if (dsel >= 0) {  // exactly one lane holds the rank
+            const unsigned long long pf = st->prefix[w] | (static_cast<unsigned long long>(dsel) << shift);
+            st->prefix[w] = pf;
+            st->mask[w] |= 255ull << shift;
+            st->k[w] = k - bsel;
+            if (pass == SEL_PASSES - 1) keys_out[w] = pf;
+        }
+    }
+}
 
 size_t split_tmp_bytes(int n) {
-    size_t a = 0, b = 0;
-    SPLIT_CHK(hipcub::DeviceRadixSort::SortKeys(nullptr, a, static_cast<const double*>(nullptr),
-                                             static_cast<double*>(nullptr), n));
-    SPLIT_CHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<const uint32_t*>(nullptr),
-                                            static_cast<uint32_t*>(nullptr), n));
-    return std::max(a, b);
+    const size_t blocks = size_t((n + 1023) / 1024) + 1;
+    return sizeof(SelState) + 256 + blocks * 4 + 64;
 }
 
 void fiedler_scale(hipStream_t s, const double* x, double sgn, int n, double* out) {
     hipLaunchKernelGGL(k_fiedler_scale, dim3((n + 255) / 256), dim3(256), 0, s, x, sgn, n, out);
 }
 
-void split_sort(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, double* sorted, int n) {
-    SPLIT_CHK(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, v, sorted, n, 0, 64, s));
+void split_select(hipStream_t s, void* tmp, const double* v, int n, unsigned k0, unsigned k1,
+                  unsigned long long* keys_out) {
+    SelState* st = static_cast<SelState*>(tmp);
+    const hipError_t e = hipMemsetAsync(st, 0, sizeof(SelState), s);
+    if (e != hipSuccess) ek::fail(EK_EHIP, "split_select: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(k_select_init, dim3(1), dim3(SEL_THREADS), 0, s, st, k0, k1);
+    const int nb = (n + SEL_THREADS * SEL_PER - 1) / (SEL_THREADS * SEL_PER);
+    for (int p = 0; p < SEL_PASSES; ++p)
+        hipLaunchKernelGGL(k_select_pass, dim3(nb), dim3(SEL_THREADS), 0, s, v, n, st, p, keys_out);
 }
 
-void split_flags_scan(hipStream_t s, void* tmp, size_t tmp_bytes, const double* v, int n, double med, uint32_t* flag0,
-                      uint32_t* pos0) {
-    hipLaunchKernelGGL(k_split_flags, dim3((n + 255) / 256), dim3(256), 0, s, v, n, med, flag0);
-    SPLIT_CHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, flag0, pos0, n, s));
+double key_value(unsigned long long key) {
+    const unsigned long long u = (key >> 63) ? (key & 0x7fffffffffffffffull) : ~key;
+    double d;
+    std::memcpy(&d, &u, 8);
+    return d;
 }
 
-void split_scatter(hipStream_t s, const double* v, const uint32_t* pos0, int n, double med, int32_t* order0,
-                   int32_t* order1, uint32_t* plist, uint8_t* side) {
-    hipLaunchKernelGGL(k_split_scatter, dim3((n + 255) / 256), dim3(256), 0, s, v, pos0, n, med, order0, order1, plist,
-                       side);
+// remain[] lists in node order (cKL.cpp:155-174): side 0 holds the nodes with
+// !(med > v[i]) (bit 0 of ek_median_split).  k_split_count counts them per
+// 1024-node block; k_split_place gives each node its position (the blocks
+// before it, summed by every block, plus an in-block exclusive scan) in list
+// 0, or i - that in list 1, and writes plist and the initial sides as
+// ek_kl_set_partition builds them; the last block also writes n0.
+constexpr int PART_THREADS = 256, PART_PER = 4, PART_BLOCK = PART_THREADS * PART_PER;
+__global__ __launch_bounds__(PART_THREADS) void k_split_count(const double* __restrict__ v, int n, double med,
+                                                              unsigned* __restrict__ bcount) {
+    __shared__ unsigned ws[PART_THREADS / 64];
+    const int t = threadIdx.x, base = int(blockIdx.x) * PART_BLOCK;
+    unsigned c = 0;
+#pragma unroll
+    for (int u = 0; u < PART_PER; ++u) {
+        const int i = base + t * PART_PER + u;
+        if (i < n && !(med > v[i])) ++c;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((t & 63) == 0) ws[t >> 6] = c;
+    __syncthreads();
+    if (t == 0) bcount[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(PART_THREADS) void k_split_place(const double* __restrict__ v, int n, double med,
+                                                              const unsigned* __restrict__ bcount,
+                                                              int32_t* __restrict__ order0, int32_t* __restrict__ order1,
+                                                              uint32_t* __restrict__ plist, uint8_t* __restrict__ side,
+                                                              unsigned* __restrict__ n0_out) {
+    __shared__ unsigned ws[PART_THREADS / 64];
+    __shared__ unsigned wscan[PART_THREADS / 64];
+    const int t = threadIdx.x, base = int(blockIdx.x) * PART_BLOCK;
+    // side-0 nodes in the blocks before this one
+    unsigned before = 0;
+    for (int b = t; b < int(blockIdx.x); b += PART_THREADS) before += bcount[b];
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+    if ((t & 63) == 0) ws[t >> 6] = before;
+    bool f[PART_PER];
+    unsigned c = 0;
+#pragma unroll
+    for (int u = 0; u < PART_PER; ++u) {
+        const int i = base + t * PART_PER + u;
+        f[u] = i < n && !(med > v[i]);
+        c += f[u] ? 1u : 0u;
+    }
+    // exclusive scan of the threads' counts over the block (wave scan, then
+    // the waves' totals)
+    const int l = t & 63, w = t >> 6;
+    unsigned incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(incl, o, 64);
+        if (l >= o) incl += y;
+    }
+    if (l == 63) wscan[w] = incl;
+    __syncthreads();
+    unsigned off = ws[0] + ws[1] + ws[2] + ws[3];
+    for (int q = 0; q < w; ++q) off += wscan[q];
+    unsigned p0 = off + incl - c;
+#pragma unroll
+    for (int u = 0; u < PART_PER; ++u) {
+        const int i = base + t * PART_PER + u;
+        if (i >= n) break;
+        if (f[u]) {
+            order0[p0] = i;
+            plist[i] = p0;
+            side[i] = 0;
+            ++p0;
+        } else {
+            const uint32_t p1 = uint32_t(i) - p0;
+            order1[p1] = i;
+            plist[i] = p1 | 0x80000000u;
+            side[i] = 1;
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1 && t == PART_THREADS - 1) *n0_out = p0;
+}
+
+void split_partition(hipStream_t s, void* tmp, const double* v, int n, double med, int32_t* order0, int32_t* order1,
+                     uint32_t* plist, uint8_t* side, unsigned* n0_out) {
+    unsigned* bcount = reinterpret_cast<unsigned*>(static_cast<char*>(tmp) + sizeof(SelState) + 256);
+    const int nb = (n + PART_BLOCK - 1) / PART_BLOCK;
+    hipLaunchKernelGGL(k_split_count, dim3(nb), dim3(PART_THREADS), 0, s, v, n, med, bcount);
+    hipLaunchKernelGGL(k_split_place, dim3(nb), dim3(PART_THREADS), 0, s, v, n, med, bcount, order0, order1, plist,
+                       side, n0_out);
 }
 
 }  // namespace dev

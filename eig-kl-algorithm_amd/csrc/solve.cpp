@@ -44,7 +44,9 @@ struct ThreadStatus {
     int code = EK_OK;
     std::string msg;
 };
-ThreadStatus kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
+// The host build needs no context: in a fresh process it runs while the HIP
+// runtime starts (get_ctx waits for that only before the uploads).
+ThreadStatus kl_graph_host(const std::function<ek_ctx*()>* get_ctx, const ek_hgr* h, int threads) {
     ThreadStatus st;
     try {
         PhaseTimer pt("kl_thread");
@@ -52,6 +54,7 @@ ThreadStatus kl_graph_host(ek_ctx* ctx, const ek_hgr* h, int threads) {
         ek_csr G;
         build_kl_graph(*h, G);
         pt.mark("graph built");
+        ek_ctx* ctx = (*get_ctx)();
         chk(ek_kl_graph_setup(ctx, h->nodes, G.rowptr.data(), G.col.data(), G.val32.data()));
         pt.mark("graph set up");
         chk(ek_kl_nets_setup(ctx, h->nets, h->net_ptr.data(), h->pins.data()));
@@ -128,7 +131,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     // (and the HIP runtime's) a few cores
     auto start_kl_graph = [&] {
         if (rank == 0)
-            kg = std::async(std::launch::async, kl_graph_host, get_ctx(), &h,
+            kg = std::async(std::launch::async, kl_graph_host, &get_ctx, &h,
                             o.eig == 1 ? std::max(1, host_threads() - 4) : 0);
     };
     // -EIG without a sign reference: the median split runs on the device,
@@ -137,10 +140,12 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     const bool dev_split = o.eig == 1 && !(o.sign_ref && o.sign_ref[0]);
     std::vector<double> v;  // (host split only)
     if (o.eig == 1) {
-        // the KL adjacency starts on its host thread before the Laplacian
-        // rows are assembled on the GPU, and runs while the GPU solves
+        // the KL adjacency starts on its host thread before the context is
+        // asked for (a fresh process: while the HIP runtime starts) and runs
+        // while the GPU solves
+        start_kl_graph();
         fiedler_vector(get_ctx(), rank, nranks, h, o, r.lambda, v, r.lanczos, &r.t_laplacian, &r.t_lanczos,
-                       start_kl_graph, &r.t_spmv_setup, !dev_split);
+                       nullptr, &r.t_spmv_setup, !dev_split);
         if (rank != 0) {
             r.t_total = since(t0);
             return;

@@ -24,7 +24,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def probe(hgr, reps=5, env_extra=None, cwd=None):
-    tool = os.path.join(REPO, "eig-kl-algorithm_amd", "build", "bin", "gKL2")
+    # EK_COLD_BUILD: another build directory (an A/B library beside its own gKL2)
+    tool = os.path.join(REPO, "eig-kl-algorithm_amd", os.environ.get("EK_COLD_BUILD", "build"), "bin", "gKL2")
     env = dict(os.environ, EK_COLD_TRACE="1", **(env_extra or {}))
     cwd = cwd or tempfile.mkdtemp(prefix="ekcold_")
     runs = []
