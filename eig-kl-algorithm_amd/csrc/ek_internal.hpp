@@ -606,6 +606,9 @@ struct KLDev {
     const KLInfo* segc = nullptr;
     const float* wdict = nullptr;  // exact fp32 weight of each code (nwd entries)
     int nwd = 0, wcolbits = 0;
+    // side and locked bitmaps (2 x ceil(n/32) words) for the on-chip loop when
+    // they do not fit its LDS budget (k_kl_swap_loop<.., GB>)
+    uint32_t* gbits = nullptr;
 };
 constexpr int KL_SEGC_PIECES = 8;
 constexpr int KL_WDICT_CAP = 4096;  // codes kept in LDS; more distinct weights: plain segments
@@ -613,7 +616,7 @@ constexpr int KL_SEG_LANES = 16;  // 16-B pieces of 2 entries: 32 entries inline
 constexpr int KL_ITEM_CAP = 256;  // updated rows whose new key/descriptor are kept in LDS (more: rederived, tagged)
 // LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
 // chunk winners on chip (0 when they do not fit: global-state mode).
-size_t kl_loop_lds_bytes(const KLDev& d);
+size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps = true);
 struct KLOut {
     long long iterations;
     long long best_iter;

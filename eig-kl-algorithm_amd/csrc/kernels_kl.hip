@@ -334,8 +334,8 @@ constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded
 // swaps have none.
 constexpr int KL_AB_CAP = 16;
 
-size_t kl_loop_lds_bytes(const KLDev& d) {
-    const size_t words = (size_t(d.n) + 31) / 32;
+size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps) {
+    const size_t words = bitmaps ? (size_t(d.n) + 31) / 32 : 0;
     const size_t nck = size_t(d.nck0) + size_t(d.nck1);
     // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * 2 (early rescans), as carved by the kernel
     constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
@@ -462,7 +462,12 @@ __device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const
 // SEGC: the rows' inline segments are the weight-coded ones (KLDev::segc),
 // decoded through the weight table in LDS; the staged contributions and the
 // sums are the same as from the plain segments.
-template <bool PROF, bool SEGC>
+// GB: the side / locked bitmaps live in global memory (KLDev::gbits: a graph
+// whose n/4 bytes of bitmaps exceed the LDS budget while the rest still fits);
+// they are read with agent-scope loads (performed at the L2, past the CU's
+// vector L1) and flipped with agent-scope atomics, drained before barrier 2.
+// The logic and the swap log are the on-chip form's.
+template <bool PROF, bool SEGC, bool GB = false>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int limit, ek_swap* __restrict__ log,
                                                                   long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
@@ -507,9 +512,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     // swap's G1 fills (so P never reads a reset count)
     int* ab_cnt = s_stop + 4;
     int* nx_ok = ab_cnt + 4;  // [4]: [0] = 1 when P published the next pair
-    uint32_t* s_side = reinterpret_cast<uint32_t*>(nx_ok + 4);
+    uint32_t* s_side = GB ? d.gbits : reinterpret_cast<uint32_t*>(nx_ok + 4);
     uint32_t* s_lock = s_side + words;
-    float* s_wd = reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
+    float* s_wd = GB ? reinterpret_cast<float*>(nx_ok + 4) : reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
+    auto bits_at = [&](const uint32_t* p) -> uint32_t {  // a bitmap word (GB: at the L2)
+        if constexpr (GB) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else return *p;
+    };
     if constexpr (SEGC)
         for (int i = tid; i < d.nwd; i += KL_LOOP_THREADS) s_wd[i] = d.wdict[i];
     for (int i = tid; i < nsel; i += KL_LOOP_THREADS) {
@@ -527,9 +536,15 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         dtag1[i] = ctag1[i] = -1;
     }
     for (int i = tid; i < words; i += KL_LOOP_THREADS) {
-        s_side[i] = side_word(d.side_init, d.n, i);
-        s_lock[i] = 0u;
+        if constexpr (GB) {
+            __hip_atomic_store(s_side + i, side_word(d.side_init, d.n, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(s_lock + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            s_side[i] = side_word(d.side_init, d.n, i);
+            s_lock[i] = 0u;
+        }
     }
+    if constexpr (GB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bitmaps stored before the barrier
     if (tid < 4) s_stop[tid] = tid == 3 ? -1 : 0;
     if (tid < 4) ab_cnt[tid] = 0;
     if (tid < 4) nx_ok[tid] = 0;  // the first swap selects
@@ -660,9 +675,11 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         // pre-swap bitmaps and applies the swap itself: node1 and node2 (never
         // equal) change side and become locked.
         auto side_now = [&](int x) -> bool {
-            return (((s_side[x >> 5] >> (x & 31)) & 1u) != 0) ^ (x == A) ^ (x == B);
+            return (((bits_at(s_side + (x >> 5)) >> (x & 31)) & 1u) != 0) ^ (x == A) ^ (x == B);
         };
-        auto locked_now = [&](int x) -> bool { return ((s_lock[x >> 5] >> (x & 31)) & 1u) || x == A || x == B; };
+        auto locked_now = [&](int x) -> bool {
+            return ((bits_at(s_lock + (x >> 5)) >> (x & 31)) & 1u) || x == A || x == B;
+        };
         const int tot = la + lb;
         const int tag = int(it);
         const int abp = EK_KL_NEXT ? (tag & 1) * 2 : 0;  // this swap's short-list counts (ab_cnt)
@@ -1006,10 +1023,18 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         if (wv == W_FLIP && lane == 0) {  // the swap itself, for the next swap's lookups (barrier 2)
             // LDS atomics without return: four independent operations instead
             // of four dependent read-modify-write round trips
-            atomicOr(&s_side[A >> 5], 1u << (A & 31));
-            atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
-            atomicOr(&s_lock[A >> 5], 1u << (A & 31));
-            atomicOr(&s_lock[B >> 5], 1u << (B & 31));
+            if constexpr (GB) {  // at the L2, drained before barrier 2
+                __hip_atomic_fetch_or(s_side + (A >> 5), 1u << (A & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_and(s_side + (B >> 5), ~(1u << (B & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_or(s_lock + (A >> 5), 1u << (A & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_or(s_lock + (B >> 5), 1u << (B & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                atomicOr(&s_side[A >> 5], 1u << (A & 31));
+                atomicAnd(&s_side[B >> 5], ~(1u << (B & 31)));
+                atomicOr(&s_lock[A >> 5], 1u << (A & 31));
+                atomicOr(&s_lock[B >> 5], 1u << (B & 31));
+            }
         }
         if constexpr (EK_KL_NEXT) {
             if (wv == W_PF) {
@@ -1196,7 +1221,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         }
     }
     __syncthreads();
-    for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((s_side[u >> 5] >> (u & 31)) & 1u);
+    for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((bits_at(s_side + (u >> 5)) >> (u & 31)) & 1u);
     if (EK_KL_PREFETCH && wv == W_PF && lane == 0 && pf_sink == 0x5a5a5a5au) out->prof[12] = 1ull;  // keeps P's loads
     if (lane == 0) {
         out->warr[wv] = w_arr1;
@@ -2412,7 +2437,12 @@ __global__ __launch_bounds__(256) void k_touch(const int4* __restrict__ p, long 
 }
 
 void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out) {
-    const size_t lds = kl_loop_lds_bytes(d);
+    // the on-chip loop with its bitmaps in LDS; else (a larger graph) with
+    // them in global memory while the rest fits (EK_KL_GBITS=1 forces that
+    // form: tests); else the global-state loop
+    const bool force_gb = std::getenv("EK_KL_GBITS") && std::getenv("EK_KL_GBITS")[0] == '1';
+    const size_t lds = force_gb ? 0 : kl_loop_lds_bytes(d);
+    const size_t lds_gb = d.gbits && !std::getenv("EK_KL_GLOBAL_STATE") ? kl_loop_lds_bytes(d, false) : 0;
     // Warm the Infinity Cache with the per-entry arrays the swap loop reads at
     // random (inline segments, then descriptors, so the descriptors are the
     // most recent): most of its one dependent round trip per swap then hits
@@ -2446,6 +2476,15 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
         return;
     }
     const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
+    if (!lds && lds_gb) {
+        if (d.segc)
+            hipLaunchKernelGGL((k_kl_swap_loop<false, true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_gb, s, d, limit,
+                               log, cap, out);
+        else
+            hipLaunchKernelGGL((k_kl_swap_loop<false, false, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_gb, s, d, limit,
+                               log, cap, out);
+        return;
+    }
     if (lds && !global_state && prof && d.segc)
         hipLaunchKernelGGL((k_kl_swap_loop<true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds, s, d, limit, log, cap, out);
     else if (lds && !global_state && prof)

@@ -188,7 +188,7 @@ def test_kl_random_init_synthetic(ek, oracle, ctx, mult, seed):
 
 
 @pytest.mark.parametrize("mode", ["EK_KL_GLOBAL_STATE", "EK_KL_NOSEG", "EK_KL_NOSEGC", "EK_KL_PIPE",
-                                  "EK_KL_PIPE+EK_KL_NOSEGC"])
+                                  "EK_KL_PIPE+EK_KL_NOSEGC", "EK_KL_GBITS", "EK_KL_GBITS+EK_KL_NOSEGC"])
 @pytest.mark.parametrize("name", ["ibm01", "industry2"])
 def test_kl_fallback_paths_bitexact(ek, oracle, ctx, monkeypatch, name, mode):
     # the global-state loop (graphs whose on-chip state does not fit LDS), the
@@ -196,7 +196,9 @@ def test_kl_fallback_paths_bitexact(ek, oracle, ctx, monkeypatch, name, mode):
     # the plain (not weight-coded) inline rows (too many distinct weights) are
     # forced here on shipped circuits; industry2 has rows of 910 entries.
     # EK_KL_PIPE: the overlapped schedule (k_kl_swap_pipe, not the default:
-    # profiles/r06/kl), coded and plain inline rows
+    # profiles/r06/kl), coded and plain inline rows.  EK_KL_GBITS: the on-chip
+    # loop with its side / locked bitmaps in global memory (the form graphs
+    # above ~500k nodes take), coded and plain inline rows
     for m in mode.split("+"):
         monkeypatch.setenv(m, "1")
     h = ek.Hypergraph.read(circuit_path(name))

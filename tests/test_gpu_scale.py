@@ -316,3 +316,28 @@ def test_seed_sweep_pipeline_vs_oracle(ek, oracle, ctx, mult, seed):
     log, res = _kl_vs_oracle(ek, oracle, ctx, h, bits)
     swap_fields_equal(log_d, log)
     assert res_d["net_cut_best"] == res["net_cut_best"]
+
+
+def test_kl_large_graph_bitmaps_off_chip(ek, ctx, monkeypatch):
+    """A graph whose side / locked bitmaps (n/4 bytes) exceed the KL loop's LDS
+    budget: the 3.0x synthetic (605,760 nodes).  The on-chip loop then keeps
+    the bitmaps in global memory (k_kl_swap_loop<.., GB>, the default there)
+    and must give the global-state loop's swap log bit for bit (that loop is
+    held to the oracle on the shipped circuits: test_kl_fallback_paths_bitexact)
+    while running several times faster."""
+    h = ek.Hypergraph.generate(3.0, 3)
+    lam, v, st, bits = _fiedler_bits(ek, ctx, h)
+    ctx.kl_graph_setup(h.kl_graph())
+    ctx.kl_nets_setup(*h.pins())
+    ctx.kl_set_partition_bits(bits)
+    log, res = ctx.kl_run()
+    monkeypatch.setenv("EK_KL_GLOBAL_STATE", "1")
+    log_g, res_g = ctx.kl_run()
+    monkeypatch.delenv("EK_KL_GLOBAL_STATE")
+    assert res["iterations"] == res_g["iterations"] > 10000
+    swap_fields_equal(log, log_g)
+    for k in ("best_iter", "net_cut_best", "net_cut_final"):
+        assert res[k] == res_g[k], k
+    us, us_g = 1e3 * res["loop_ms"] / res["iterations"], 1e3 * res_g["loop_ms"] / res_g["iterations"]
+    print(f"3.0x KL: {us:.3f} us/swap (bitmaps off chip) vs {us_g:.3f} (global-state loop)")
+    assert us < 0.5 * us_g
