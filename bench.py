@@ -517,6 +517,8 @@ def main():
             else:
                 log(f"syn10 traffic: {t10['error']}")
             syn10["traffic"] = t10
+        if extras and rank == 0:  # the whole -EIG pipeline on it below (sub-config syn10_pipeline)
+            h10.write(os.path.join(work, "syn10.hgr"))
         del h10
 
     if rank != 0:
@@ -533,6 +535,10 @@ def main():
                   ("syn1", (1.0, 1), "the whole 1.0x seed-1 synthetic (SURVEY §8d's first stand-in; disconnected: "
                                      "lambda1 = 0, its Lanczos length set by rounding noise)"),
                   ("syn2", (2.0, 2), "configs[3] circuit_generator 2.0x shape, seed 2 (disconnected)")]
+        if os.path.exists(os.path.join(work, "syn10.hgr")):
+            inputs.append(("syn10_pipeline", os.path.join(work, "syn10.hgr"),
+                           "configs[4]'s graph (10x seed 10, 2.02M nodes) through the whole -EIG file path on ONE "
+                           "GPU: Lanczos, device split, KL (the on-chip loop with its bitmaps off chip)"))
         for name, p, what in inputs:
             if isinstance(p, tuple):
                 hp = ek.Hypergraph.generate(*p)
