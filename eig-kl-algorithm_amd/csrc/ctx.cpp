@@ -3095,7 +3095,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     c->kl_side.ensure(size_t(n));
     c->kl_side_init.ensure(size_t(n));
     // (also the side / locked bitmaps of the on-chip loop when they exceed
-    // its LDS budget: 2 ceil(n/32) words, KLDev::gbits)
+    // its LDS budget: 2 ceil(n/32) words, k_kl_swap_loop<.., GB>)
     c->kl_locked.ensure(std::max(size_t(n), size_t((n + 31) / 32) * 8 + 64));
     c->kl_plist.ensure(size_t(n) * 4);
     c->kl_sides_tmp.ensure(size_t(n));
@@ -3275,7 +3275,6 @@ ek::dev::KLDev kl_dev(ek_ctx* c) {
     d.side = c->kl_side.as<uint8_t>();
     d.side_init = c->kl_side_init.as<uint8_t>();
     d.locked = c->kl_locked.as<uint8_t>();
-    d.gbits = c->kl_locked.as<uint32_t>();
     d.gp0 = c->kl_gp0.as<float>();
     d.gp1 = c->kl_gp1.as<float>();
     d.order0 = c->kl_order0.as<int32_t>();

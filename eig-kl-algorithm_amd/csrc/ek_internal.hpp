@@ -576,7 +576,10 @@ struct KLDev {
     const float* w = nullptr;
     uint8_t* side = nullptr;        // current split (0/1); final sides after the loop
     const uint8_t* side_init = nullptr;
-    uint8_t* locked = nullptr;      // erased from remain[] (global-state mode only)
+    // erased from remain[] (global-state mode only); the on-chip loop whose
+    // side / locked bitmaps exceed its LDS budget keeps them here instead
+    // (k_kl_swap_loop<.., GB>: 2 ceil(n/32) words)
+    uint8_t* locked = nullptr;
     float* gp0 = nullptr;           // gains of remain[0] nodes, by POSITION (NaN = erased)
     float* gp1 = nullptr;           // gains of remain[1] nodes, by position
     const int32_t* order0 = nullptr;  // remain[0] positions -> node
@@ -606,9 +609,6 @@ struct KLDev {
     const KLInfo* segc = nullptr;
     const float* wdict = nullptr;  // exact fp32 weight of each code (nwd entries)
     int nwd = 0, wcolbits = 0;
-    // side and locked bitmaps (2 x ceil(n/32) words) for the on-chip loop when
-    // they do not fit its LDS budget (k_kl_swap_loop<.., GB>)
-    uint32_t* gbits = nullptr;
 };
 constexpr int KL_SEGC_PIECES = 8;
 constexpr int KL_WDICT_CAP = 4096;  // codes kept in LDS; more distinct weights: plain segments

@@ -462,7 +462,7 @@ __device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const
 // SEGC: the rows' inline segments are the weight-coded ones (KLDev::segc),
 // decoded through the weight table in LDS; the staged contributions and the
 // sums are the same as from the plain segments.
-// GB: the side / locked bitmaps live in global memory (KLDev::gbits: a graph
+// GB: the side / locked bitmaps live in global memory (in KLDev::locked: a graph
 // whose n/4 bytes of bitmaps exceed the LDS budget while the rest still fits);
 // they are read with agent-scope loads (performed at the L2, past the CU's
 // vector L1) and flipped with agent-scope atomics, drained before barrier 2.
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     // swap's G1 fills (so P never reads a reset count)
     int* ab_cnt = s_stop + 4;
     int* nx_ok = ab_cnt + 4;  // [4]: [0] = 1 when P published the next pair
-    uint32_t* s_side = GB ? d.gbits : reinterpret_cast<uint32_t*>(nx_ok + 4);
+    uint32_t* s_side = GB ? reinterpret_cast<uint32_t*>(d.locked) : reinterpret_cast<uint32_t*>(nx_ok + 4);
     uint32_t* s_lock = s_side + words;
     float* s_wd = GB ? reinterpret_cast<float*>(nx_ok + 4) : reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
     auto bits_at = [&](const uint32_t* p) -> uint32_t {  // a bitmap word (GB: at the L2)
@@ -2442,7 +2442,7 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
     // form: tests); else the global-state loop
     const bool force_gb = std::getenv("EK_KL_GBITS") && std::getenv("EK_KL_GBITS")[0] == '1';
     const size_t lds = force_gb ? 0 : kl_loop_lds_bytes(d);
-    const size_t lds_gb = d.gbits && !std::getenv("EK_KL_GLOBAL_STATE") ? kl_loop_lds_bytes(d, false) : 0;
+    const size_t lds_gb = d.locked && !std::getenv("EK_KL_GLOBAL_STATE") ? kl_loop_lds_bytes(d, false) : 0;
     // Warm the Infinity Cache with the per-entry arrays the swap loop reads at
     // random (inline segments, then descriptors, so the descriptors are the
     // most recent): most of its one dependent round trip per swap then hits
