@@ -66,6 +66,14 @@ ThreadStatus kl_graph_host(const std::function<ek_ctx*()>* get_ctx, const ek_hgr
     return st;
 }
 
+// the KL adjacency's host threads: beside a Lanczos solve, all but 4 of the
+// host's (the solve's thread, the HIP runtime's); EK_KL_GRAPH_THREADS
+// overrides (A/B)
+int kl_graph_threads(bool beside_solve) {
+    if (const char* e = std::getenv("EK_KL_GRAPH_THREADS"); e && std::atoi(e) > 0) return std::atoi(e);
+    return beside_solve ? std::max(1, host_threads() - 4) : 0;
+}
+
 // the results file's text buffer, kept across calls (one caller at a time)
 struct TextCache {
     std::mutex mu;
@@ -131,8 +139,7 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     // (and the HIP runtime's) a few cores
     auto start_kl_graph = [&] {
         if (rank == 0)
-            kg = std::async(std::launch::async, kl_graph_host, &get_ctx, &h,
-                            o.eig == 1 ? std::max(1, host_threads() - 4) : 0);
+            kg = std::async(std::launch::async, kl_graph_host, &get_ctx, &h, kl_graph_threads(o.eig == 1));
     };
     // -EIG without a sign reference: the median split runs on the device,
     // from the Fiedler vector the Lanczos solve left there, once the KL graph
