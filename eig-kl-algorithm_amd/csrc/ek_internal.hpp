@@ -616,7 +616,7 @@ constexpr int KL_SEG_LANES = 16;  // 16-B pieces of 2 entries: 32 entries inline
 constexpr int KL_ITEM_CAP = 256;  // updated rows whose new key/descriptor are kept in LDS (more: rederived, tagged)
 // LDS bytes the loop kernel needs to keep side/locked bitmaps, chunk keys and
 // chunk winners on chip (0 when they do not fit: global-state mode).
-size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps = true);
+size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps = true, bool fixed = false);
 struct KLOut {
     long long iterations;
     long long best_iter;

@@ -333,15 +333,19 @@ constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded
 // chunk is rescanned).  A chunk holds 1024 of the list's positions, so most
 // swaps have none.
 constexpr int KL_AB_CAP = 16;
+// chunks a list may have for k_kl_swap_loop's fixed LDS layout (FIX)
+constexpr int KL_FIX_NCK = 128;
 
-size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps) {
+size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps, bool fixed) {
+    if (fixed && (d.nck0 > KL_FIX_NCK || d.nck1 > KL_FIX_NCK || d.nwd > KL_WDICT_CAP)) return 0;
     const size_t words = bitmaps ? (size_t(d.n) + 31) / 32 : 0;
-    const size_t nck = size_t(d.nck0) + size_t(d.nck1);
+    const size_t nck = fixed ? size_t(2 * KL_FIX_NCK) : size_t(d.nck0) + size_t(d.nck1);
     // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * 2 (early rescans), as carved by the kernel
     constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
     const size_t b = (nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2 + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
-                     (2 * size_t(kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2) * 8 +
-                     (2 * nck + KL_ITEM_CAP + 4 + 4 + 4) * 4 + 2 * words * 4 + size_t(d.segc ? d.nwd : 0) * 4 +
+                     (2 * size_t(fixed ? KL_FIX_NCK : kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2) * 8 +
+                     (2 * nck + KL_ITEM_CAP + 4 + 4 + 4) * 4 + 2 * words * 4 +
+                     (fixed ? size_t(KL_WDICT_CAP) : size_t(d.segc ? d.nwd : 0)) * 4 +
                      128;  // (+ k_kl_swap_pipe's speculative pair, 16-B aligned)
     return b <= 152 * 1024 ? b : 0;
 }
@@ -467,7 +471,12 @@ __device__ __forceinline__ u64 chunk_rescan1(const float* __restrict__ gp, const
 // they are read with agent-scope loads (performed at the L2, past the CU's
 // vector L1) and flipped with agent-scope atomics, drained before barrier 2.
 // The logic and the swap log are the on-chip form's.
-template <bool PROF, bool SEGC, bool GB = false>
+// FIX: every LDS array at a compile-time offset, sized for KL_FIX_NCK chunks a
+// list and KL_WDICT_CAP weight codes (the bitmaps last): the addresses fold
+// into the LDS instructions' offsets instead of ~25 SGPRs of carve pointers,
+// which the register allocator otherwise spills into VGPR lanes and reloads
+// inside the loop.  Taken when both lists have at most KL_FIX_NCK chunks.
+template <bool PROF, bool SEGC, bool GB = false, bool FIX = false>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int limit, ek_swap* __restrict__ log,
                                                                   long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
@@ -482,12 +491,13 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = lane >> 5, hl = lane & 31;
-    const int nsel = kl_sel_pad(d.nck0, d.nck1);
+    const int nsel = FIX ? KL_FIX_NCK : kl_sel_pad(d.nck0, d.nck1);
     const int words = (d.n + 31) / 32;
+    const int lc0 = FIX ? KL_FIX_NCK : d.nck0, lc1 = FIX ? KL_FIX_NCK : d.nck1;  // the carve's chunk counts
     // LDS carve (kl_loop_lds_bytes): 16-B records first, then 8-B, then 4-B
     KLInfo* ci0 = reinterpret_cast<KLInfo*>(smem);  // chunk winners' descriptors
-    KLInfo* ci1 = ci0 + d.nck0;
-    KLInfo* it_info = ci1 + d.nck1;  // per updated row: {node, rowptr, len, position}
+    KLInfo* ci1 = ci0 + lc0;
+    KLInfo* it_info = ci1 + lc1;  // per updated row: {node, rowptr, len, position}
     KLInfo* er_info = it_info + KL_ITEM_CAP;  // [2][E_PARTS] early-rescan winners
     KLInfo* ab_info = er_info + 2 * E_PARTS;  // [2][KL_AB_CAP] updated rows in node1's / node2's chunk
     KLInfo* nx_info = ab_info + 2 * KL_AB_CAP;  // [2] the next pair's descriptors, published by P (EK_KL_NEXT)
@@ -495,16 +505,16 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     u64* ck0 = reinterpret_cast<u64*>(sg_stage + NG * KL_STAGE_ROWS * KL_STAGE_ROW);  // chunk keys (zero-padded to nsel)
     u64* ck1 = ck0 + nsel;
     u64* ckn0 = ck1 + nsel;  // shadow keys: G1 merges risen keys here, G2 publishes them
-    u64* ckn1 = ckn0 + d.nck0;
-    u64* it_key = ckn1 + d.nck1;           // per updated row: its new key
+    u64* ckn1 = ckn0 + lc0;
+    u64* it_key = ckn1 + lc1;           // per updated row: its new key
     u64* er_key = it_key + KL_ITEM_CAP;     // [2][E_PARTS] early-rescan keys
     u64* ab_key = er_key + 2 * E_PARTS;     // [2][KL_AB_CAP] their new keys
     u64* nx_key = ab_key + 2 * KL_AB_CAP;   // [2] the next pair's keys, published by P
     int* dtag0 = reinterpret_cast<int*>(nx_key + 2);  // iteration that tagged a late rescan
-    int* dtag1 = dtag0 + d.nck0;
-    int* ctag0 = dtag1 + d.nck1;  // iteration that claimed it
-    int* ctag1 = ctag0 + d.nck0;
-    int* it_cs = ctag1 + d.nck1;  // per updated row: list << 31 | chunk (-1: locked)
+    int* dtag1 = dtag0 + lc0;
+    int* ctag0 = dtag1 + lc1;  // iteration that claimed it
+    int* ctag1 = ctag0 + lc0;
+    int* it_cs = ctag1 + lc1;  // per updated row: list << 31 | chunk (-1: locked)
     int* s_stop = it_cs + KL_ITEM_CAP;  // [4], by iteration parity
     // rows appended to ab_* by this swap's G1, per list: [0..1], reset by
     // G2a after its read.  With EK_KL_NEXT, [2][2] by iteration parity: G2a
@@ -512,9 +522,12 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     // swap's G1 fills (so P never reads a reset count)
     int* ab_cnt = s_stop + 4;
     int* nx_ok = ab_cnt + 4;  // [4]: [0] = 1 when P published the next pair
-    uint32_t* s_side = GB ? reinterpret_cast<uint32_t*>(d.locked) : reinterpret_cast<uint32_t*>(nx_ok + 4);
+    // (FIX: the weight table at its fixed offset, then the bitmaps)
+    uint32_t* s_side = GB ? reinterpret_cast<uint32_t*>(d.locked)
+                     : FIX ? reinterpret_cast<uint32_t*>(nx_ok + 4 + KL_WDICT_CAP)
+                           : reinterpret_cast<uint32_t*>(nx_ok + 4);
     uint32_t* s_lock = s_side + words;
-    float* s_wd = GB ? reinterpret_cast<float*>(nx_ok + 4) : reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
+    float* s_wd = (GB || FIX) ? reinterpret_cast<float*>(nx_ok + 4) : reinterpret_cast<float*>(s_lock + words);  // weight table (SEGC)
     auto bits_at = [&](const uint32_t* p) -> uint32_t {  // a bitmap word (GB: at the L2)
         if constexpr (GB) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else return *p;
@@ -2483,6 +2496,18 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
         else
             hipLaunchKernelGGL((k_kl_swap_loop<false, false, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_gb, s, d, limit,
                                log, cap, out);
+        return;
+    }
+    // the fixed LDS layout when the chunk lists allow it (EK_KL_FIXLDS=0: off, A/B)
+    const char* fx = std::getenv("EK_KL_FIXLDS");
+    const size_t lds_fix = lds && !global_state && !prof && !(fx && fx[0] == '0') ? kl_loop_lds_bytes(d, true, true) : 0;
+    if (lds_fix) {
+        if (d.segc)
+            hipLaunchKernelGGL((k_kl_swap_loop<false, true, false, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_fix, s, d,
+                               limit, log, cap, out);
+        else
+            hipLaunchKernelGGL((k_kl_swap_loop<false, false, false, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_fix, s, d,
+                               limit, log, cap, out);
         return;
     }
     if (lds && !global_state && prof && d.segc)
