@@ -367,8 +367,9 @@ def main():
     last, swap_log = results[-1]
     # the SpMV's kernel timestamps come from one more step, untimed: the timed
     # steps launch without timing events (a launch with events costs the host
-    # ~7 us more, tools/lanczos_wall.py).  Both launch eagerly: the default
-    # partial reorthogonalisation (reorth=3) captures no HIP graphs
+    # ~7 us more, tools/lanczos_wall.py).  (The timed steps replay the
+    # Lanczos chunks' HIP graphs on one context; a step with events launches
+    # eagerly.)
     ev_step = step(time_spmv=True)
     barrier()
     log(f"timed: {args.steps} steps, {sec_per_step * 1e3:.2f} ms/step; last step {last['t_total']:.4f} s "
@@ -457,6 +458,9 @@ def main():
             tt.append(max_over_ranks(time.time() - t))
         cs10 = c10.comm_stats()  # the timed solve's collectives (time_spmv on the last one)
         ceil10_us = c10.spmv_gather_bench(100)
+        # (every collective on every rank, in the same order: the max is taken
+        # here once, not inside rank-0-only blocks below)
+        ceil10_max = max_over_ranks(ceil10_us)
         b10 = c10.spmv_bytes(fused=False)
         us10 = 1e3 * st10["spmv_ms"] / max(1, st10["spmv_timed"])
         us10_max = max_over_ranks(us10)
@@ -474,8 +478,8 @@ def main():
                               "recv_MB_per_step_rank0": round(8 * rv10 / 1e6, 3),
                               "send_MB_per_step_rank0": round(8 * sd10 / 1e6, 3)},
                  "projected_steps": st10["projected_steps"],
-                 "ceiling": {"gather_only_us_max_rank": round(max_over_ranks(ceil10_us), 3),
-                             "ceiling_frac_per_gpu": round(b10 / max_over_ranks(ceil10_us) / 1e3 / HBM_PEAK_GBS, 4),
+                 "ceiling": {"gather_only_us_max_rank": round(ceil10_max, 3),
+                             "ceiling_frac_per_gpu": round(b10 / ceil10_max / 1e3 / HBM_PEAK_GBS, 4),
                              "what": "ek_spmv_gather_bench: the SpMV's grid, matrix stream and x / value gathers "
                                      "with nothing else, back to back"}}
         if world > 1:
@@ -500,7 +504,7 @@ def main():
             syn10["rocprof"] = {"spmv_avg_us": round(us10_rp, 3), "spmv_calls": calls10,
                                 "achieved_GBps": round(b10 / us10_rp / 1e3, 1),
                                 "frac": round(b10 / us10_rp / 1e3 / HBM_PEAK_GBS, 4),
-                                "frac_of_ceiling": round(max_over_ranks(ceil10_us) / us10_rp, 4),
+                                "frac_of_ceiling": round(ceil10_max / us10_rp, 4),
                                 "what": ("the resident 1-rank solve" if world == 1 else
                                          f"rank 0's shard of the {world}-rank map, 200 back-to-back fused launches "
                                          "(tools/spmv_probe.py shard)")}
