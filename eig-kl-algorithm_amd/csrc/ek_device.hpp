@@ -34,3 +34,44 @@ __device__ __forceinline__ void chk_mirror(const StepFin& f, int t, int nthreads
 
 }  // namespace dev
 }  // namespace ek
+
+// (lab: EK_OUT_STORE, an A/B build switch) the Lanczos step's vector outputs
+// (the SpMV's y and basis column, the three-term residual f) stored
+// 0: plainly; 1: non-temporal; 2: agent-scope (sc1, written through the L2)
+#ifndef EK_OUT_STORE
+#define EK_OUT_STORE 0
+#endif
+__device__ __forceinline__ void out_store(double* p, double v) {
+#if EK_OUT_STORE == 1
+    __builtin_nontemporal_store(v, p);
+#elif EK_OUT_STORE == 2
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void out_store(float* p, float v) {
+#if EK_OUT_STORE == 1
+    __builtin_nontemporal_store(v, p);
+#elif EK_OUT_STORE == 2
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void out_store2(double* p, double2 v) {
+#if EK_OUT_STORE == 1
+    typedef double nd2 __attribute__((ext_vector_type(2)));
+    nd2 x;
+    x.x = v.x;
+    x.y = v.y;
+    __builtin_nontemporal_store(x, reinterpret_cast<nd2*>(p));
+#elif EK_OUT_STORE == 2
+    out_store(p, v.x);
+    out_store(p + 1, v.y);
+#else
+    *reinterpret_cast<double2*>(p) = v;
+#endif
+}
+

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "ek_device.hpp"
 #include "ek_internal.hpp"
 
 #ifndef EK_UPD_UB
@@ -689,7 +690,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 const size_t r = size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t);
                 // (merged: stored only once the step is known to skip — a
                 // projecting step's f is written by the update in this launch)
-                if constexpr (!MRG) *reinterpret_cast<double2*>(fp + r) = y;
+                if constexpr (!MRG) out_store2(fp + r, y);
                 if (v32col) *reinterpret_cast<float2*>(v32col + r) = make_float2(float(tv[k].x), float(tv[k].y));
             }
         }
@@ -716,7 +717,7 @@ __device__ __forceinline__ void gemvt_body(int ldv, int nrb, const double* __res
                 if (skip) {  // f = f'
 #pragma unroll
                     for (int k = 0; k < KR; ++k)
-                        *reinterpret_cast<double2*>(fp + size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t)) = xs[k];
+                        out_store2(fp + size_t(rbk) * GT_ROWS + size_t(k) * 512 + 2 * size_t(t), xs[k]);
                 }
             }
             if (skip) {

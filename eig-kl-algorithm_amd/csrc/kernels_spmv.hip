@@ -217,11 +217,11 @@ __global__ __launch_bounds__(SPMV_THREADS, EK_SPMV_WAVES) void k_spmv_adaptive(c
         if (t == 0) {
             const double a0 = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
             const double a = fin.ybase ? fin.ybase[r0] + a0 : a0;
-            y[r0] = a * scale;
+            out_store(y + r0, a * scale);
             if (vcol) {
                 const double v = f[r0] * scale;
-                vcol[r0] = v;
-                if (fin.v32col) fin.v32col[r0] = float(v);
+                out_store(vcol + r0, v);
+                if (fin.v32col) out_store(fin.v32col + r0, float(v));
                 if (apart) store_sc1(apart + blockIdx.x, v * (a * scale));
                 if (fin.wpart) fin.wpart[blockIdx.x] = (a * scale) * (a * scale);
             }
@@ -289,11 +289,11 @@ __global__ __launch_bounds__(SPMV_THREADS, EK_SPMV_WAVES) void k_spmv_adaptive(c
     double av = 0.0, wv = 0.0;
     if (g < nr && lane == 0) {
         const double yr = (fin.ybase ? fin.ybase[r0 + g] + s : s) * scale;
-        y[r0 + g] = yr;
+        out_store(y + r0 + g, yr);
         if (vcol) {
             const double v = fr * scale;
-            vcol[r0 + g] = v;
-            if (fin.v32col) fin.v32col[r0 + g] = float(v);
+            out_store(vcol + r0 + g, v);
+            if (fin.v32col) out_store(fin.v32col + r0 + g, float(v));
             av = v * yr;
             wv = yr * yr;
         }
