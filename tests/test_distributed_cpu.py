@@ -298,3 +298,41 @@ def test_halo_exchange_layout(world):
         assert out[r]["partials"][r] == out[r]["own_partial"]
         assert out[r]["pieces"] == world - 1  # one message from every peer
         assert out[r]["recv"] <= out[r]["recv_full"]
+
+
+def test_bench_collectives_on_every_rank():
+    """bench.py at N > 1: every collective (max_over_ranks, barrier, dist.*)
+    must run on every rank in the same order, so none may sit under a
+    condition that differs between ranks.  A static check of the script: a
+    collective's enclosing ifs may test only rank-independent names (world,
+    args, extras, the loop index, comm), or `... or world > 1` (every rank
+    enters at N > 1).  Round 6 had one under `if us10_rp:` (rank 0's rocprof
+    result), and the N = 2 run died with its ranks' all-reduces paired wrongly."""
+    import ast
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+    tree = ast.parse(open(path).read())
+    parents = {ch: node for node in ast.walk(tree) for ch in ast.iter_child_nodes(node)}
+    allowed = {"world", "args", "extras", "i", "comm"}
+
+    def all_ranks_enter(test):  # `x or world > 1`
+        return isinstance(test, ast.BoolOp) and isinstance(test.op, ast.Or) and any(
+            isinstance(v, ast.Compare) and isinstance(v.left, ast.Name) and v.left.id == "world" for v in test.values)
+
+    bad = []
+    for node in ast.walk(tree):
+        if not isinstance(node, ast.Call):
+            continue
+        f = node.func
+        is_dist = isinstance(f, ast.Attribute) and isinstance(f.value, ast.Name) and f.value.id == "dist"
+        if not (isinstance(f, ast.Name) and f.id in ("max_over_ranks", "barrier")) and not is_dist:
+            continue
+        if is_dist and f.attr in ("destroy_process_group", "init_process_group"):
+            continue  # (setup and teardown: outside the measured sequence)
+        p = parents.get(node)
+        while p is not None and not isinstance(p, ast.FunctionDef):
+            if isinstance(p, ast.If) and not all_ranks_enter(p.test):
+                extra = {n.id for n in ast.walk(p.test) if isinstance(n, ast.Name)} - allowed
+                if extra:
+                    bad.append((node.lineno, sorted(extra)))
+            p = parents.get(p)
+    assert not bad, f"collectives under rank-dependent conditions (line, names): {bad}"
