@@ -564,7 +564,13 @@ void start_vector(hipStream_t s, int ldv, long long row0, int nreal, double* x);
 
 // kernels_kl.hip
 constexpr int KL_LOOP_THREADS = 512;  // 8 waves: 256 VGPRs per lane, no spills in the swap loop
-constexpr int KL_CHUNK = 1024;  // positions per chunk key (a few keys per lane: barrier-free selection)
+// 2048 since round 6: against 1024, 1.5 % a swap at the headline and 3-19 %
+// from the 2x to the 10x synthetic (fewer chunk keys to select from);
+// 512 and 4096 were slower (profiles/r06/kl/kl_chunk_*.txt)
+#ifndef EK_KL_CHUNK
+#define EK_KL_CHUNK 2048  // (A/B builds: EXTRA_DEFS=-DEK_KL_CHUNK=1024)
+#endif
+constexpr int KL_CHUNK = EK_KL_CHUNK;  // positions per chunk key (a few keys per lane: barrier-free selection)
 struct alignas(16) KLInfo {
     int32_t a, b, c, d;
 };

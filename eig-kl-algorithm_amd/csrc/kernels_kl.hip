@@ -333,8 +333,9 @@ constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded
 // chunk is rescanned).  A chunk holds 1024 of the list's positions, so most
 // swaps have none.
 constexpr int KL_AB_CAP = 16;
-// chunks a list may have for k_kl_swap_loop's fixed LDS layout (FIX)
-constexpr int KL_FIX_NCK = 128;
+// chunks a list may have for k_kl_swap_loop's fixed LDS layout (FIX): 131,072
+// positions a list
+constexpr int KL_FIX_NCK = 131072 / KL_CHUNK;
 
 size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps, bool fixed) {
     if (fixed && (d.nck0 > KL_FIX_NCK || d.nck1 > KL_FIX_NCK || d.nwd > KL_WDICT_CAP)) return 0;

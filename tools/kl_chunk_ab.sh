@@ -1,0 +1,11 @@
+# GPU box: KL chunk size 512 / 2048 builds (EK_KL_CHUNK): KL parity subset per
+# build, then the warm step against the default (1024) build.
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+for c in 512 2048; do
+  EK_LIB_PATH=eig-kl-algorithm_amd/build_c$c/libeigkl_hip.so timeout -k 10 600 python3 -u -m pytest -m gpu -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_scale.py -k "kl_bitexact or fallback_paths or headline_solve or bitmaps_off_chip" > gpurun_out/kl_chunk_$c.log 2>&1 || { tail -20 gpurun_out/kl_chunk_$c.log; exit 1; }
+  tail -1 gpurun_out/kl_chunk_$c.log
+done
+timeout -k 10 600 python3 tools/step_ab.py eig-kl-algorithm_amd/build/libeigkl_hip.so eig-kl-algorithm_amd/build_c512/libeigkl_hip.so 2 2>&1 | grep -v amdgpu.ids > gpurun_out/kl_chunk_ab.txt || exit 1
+timeout -k 10 600 python3 tools/step_ab.py eig-kl-algorithm_amd/build/libeigkl_hip.so eig-kl-algorithm_amd/build_c2048/libeigkl_hip.so 2 2>&1 | grep -v amdgpu.ids >> gpurun_out/kl_chunk_ab.txt || exit 1
+cat gpurun_out/kl_chunk_ab.txt
