@@ -333,6 +333,12 @@ constexpr int KL_STAGE_ROWS = 16;  // rows a gain wave stages per pass (16 coded
 // chunk is rescanned).  A chunk holds 1024 of the list's positions, so most
 // swaps have none.
 constexpr int KL_AB_CAP = 16;
+// waves rescanning each of the two chunks node1 / node2 leave (E); the other
+// waves but the pair-gain one run the gain updates (A/B: EK_KL_EPARTS=1)
+#ifndef EK_KL_EPARTS
+#define EK_KL_EPARTS 2
+#endif
+constexpr int KL_E_PARTS = EK_KL_EPARTS;
 // chunks a list may have for k_kl_swap_loop's fixed LDS layout (FIX): 131,072
 // positions a list
 constexpr int KL_FIX_NCK = 131072 / KL_CHUNK;
@@ -341,8 +347,8 @@ size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps, bool fixed) {
     if (fixed && (d.nck0 > KL_FIX_NCK || d.nck1 > KL_FIX_NCK || d.nwd > KL_WDICT_CAP)) return 0;
     const size_t words = bitmaps ? (size_t(d.n) + 31) / 32 : 0;
     const size_t nck = fixed ? size_t(2 * KL_FIX_NCK) : size_t(d.nck0) + size_t(d.nck1);
-    // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * 2 (early rescans), as carved by the kernel
-    constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * 2;
+    // staging for the gain waves: NG = waves - 1 (pair gain) - 2 * KL_E_PARTS (early rescans), as carved by the kernel
+    constexpr size_t NG = KL_LOOP_THREADS / 64 - 1 - 2 * KL_E_PARTS;
     const size_t b = (nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2 + NG * KL_STAGE_ROWS * KL_STAGE_ROW) * sizeof(KLInfo) +
                      (2 * size_t(fixed ? KL_FIX_NCK : kl_sel_pad(d.nck0, d.nck1)) + nck + KL_ITEM_CAP + 4 + 2 * KL_AB_CAP + 2) * 8 +
                      (2 * nck + KL_ITEM_CAP + 4 + 4 + 4) * 4 + 2 * words * 4 +
@@ -484,11 +490,11 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     // roles: W_W the pair gain; E_PARTS waves per chunk rescan node1's chunk
     // (waves W_EA, W_EA-1, ...) and E_PARTS node2's (W_EB, W_EB-1, ...);
     // waves 0 .. NG-1 run the gain updates
-    constexpr int E_PARTS = 2, NQ_E = KL_CHUNK / 64 / E_PARTS;
+    constexpr int E_PARTS = KL_E_PARTS, NQ_E = KL_CHUNK / 64 / E_PARTS;
     constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
     constexpr int W_PF = W_W;  // also runs P, the prefetch of the provisional next pair
     constexpr int W_FLIP = W_EA - 1;  // flips the side / lock bitmaps after barrier 1 (an early-rescan wave)
-    static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * 2, "kl_loop_lds_bytes reserves staging for NG gain waves");
+    static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * KL_E_PARTS, "kl_loop_lds_bytes reserves staging for NG gain waves");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // no static LDS: keeps it 16-B aligned
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = lane >> 5, hl = lane & 31;
@@ -1300,13 +1306,13 @@ template <bool PROF, bool SEGC>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_pipe(KLDev d, int limit, ek_swap* __restrict__ log,
                                                                   long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
-    constexpr int E_PARTS = 2, NQ_E = KL_CHUNK / 64 / E_PARTS;
+    constexpr int E_PARTS = KL_E_PARTS, NQ_E = KL_CHUNK / 64 / E_PARTS;
     constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
     constexpr int W_FLIP = W_EA - 1;
     constexpr int LPR = SEGC ? 4 : 8, RPW = 64 / LPR;
     constexpr int PPL = (SEGC ? KL_SEGC_PIECES : KL_SEG_LANES) / LPR;  // 16-B pieces per lane
     constexpr unsigned POLL_CAP = 1u << 22;                              // polls before a wait gives up
-    static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * 2, "kl_loop_lds_bytes reserves staging for NG gain waves");
+    static_assert(NG == KL_LOOP_THREADS / 64 - 1 - 2 * KL_E_PARTS, "kl_loop_lds_bytes reserves staging for NG gain waves");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int half = lane >> 5, hl = lane & 31;
