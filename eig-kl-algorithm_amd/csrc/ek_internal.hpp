@@ -563,7 +563,10 @@ void resid_partial(hipStream_t s, int ldv, const double* w, const double* x, dou
 void start_vector(hipStream_t s, int ldv, long long row0, int nreal, double* x);
 
 // kernels_kl.hip
-constexpr int KL_LOOP_THREADS = 512;  // 8 waves: 256 VGPRs per lane, no spills in the swap loop
+#ifndef EK_KL_THREADS
+#define EK_KL_THREADS 512  // (A/B builds: EXTRA_DEFS=-DEK_KL_THREADS=768)
+#endif
+constexpr int KL_LOOP_THREADS = EK_KL_THREADS;  // 8 waves: 256 VGPRs per lane, no spills in the swap loop
 // 2048 since round 6: against 1024, 1.5 % a swap at the headline and 3-19 %
 // from the 2x to the 10x synthetic (fewer chunk keys to select from);
 // 512 and 4096 were slower (profiles/r06/kl/kl_chunk_*.txt)

@@ -1243,7 +1243,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
     __syncthreads();
     for (int u = tid; u < d.n; u += KL_LOOP_THREADS) d.side[u] = uint8_t((bits_at(s_side + (u >> 5)) >> (u & 31)) & 1u);
     if (EK_KL_PREFETCH && wv == W_PF && lane == 0 && pf_sink == 0x5a5a5a5au) out->prof[12] = 1ull;  // keeps P's loads
-    if (lane == 0) {
+    if (lane == 0 && (NW <= 8 || wv < 8)) {  // (KLOut::warr holds 8 waves' stamps)
         out->warr[wv] = w_arr1;
         out->warr[8 + wv] = w_arr2;
         out->warr[16 + wv] = w_g2a;
