@@ -3023,6 +3023,7 @@ extern "C" {
 int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t* col, const float* w) {
     EK_TRY
     check_ctx(c);
+    ek::PhaseTimer pt("kl_graph_setup");
     if (n <= 0 || n > INT32_MAX || !rowptr || !col || !w) ek::fail(EK_EINVAL, "ek_kl_graph_setup: bad argument");
     const int64_t nnz = rowptr[n];
     for (int64_t r = 0; r < n; ++r)
@@ -3035,6 +3036,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
         });
         if (bad) ek::fail(EK_EINVAL, "ek_kl_graph_setup: column out of range");
     }
+    pt.mark("checks");
     hipStream_t s = c->kstream;
     // not ready until this setup has finished: a failure part-way must not
     // leave the previous graph's flags over this one's sizes
@@ -3061,6 +3063,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
         HIPCHK(hipMemcpyAsync(c->kl_w.p, dw, size_t(nnz) * 4, hipMemcpyHostToDevice, s));
         up.off += size_t(nnz) * 8;
     }
+    pt.mark("CSR staged");
     // inline neighbour-row segments for the swap loop: weight-coded (128 B per
     // entry) when the distinct weights fit the code bits and the LDS table,
     // else plain (256 B per entry); skipped past 32 GB.  EK_KL_NOSEGC=1 at
@@ -3071,6 +3074,7 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     c->kl_segc_ok = !std::getenv("EK_KL_NOSEGC") &&
                     size_t(nnz) * ek::dev::KL_SEGC_PIECES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30) &&
                     ek::dev::kl_weight_codes(n, nnz, col, w, kw, wdict, wcolbits);
+    pt.mark("weight codes");
     c->kl_seg_ok = !c->kl_segc_ok && size_t(nnz) * ek::dev::KL_SEG_LANES * sizeof(ek::dev::KLInfo) <= (size_t(32) << 30);
     if (c->kl_segc_ok) {
         DBuf dkw;
@@ -3103,7 +3107,9 @@ int ek_kl_graph_setup(ek_ctx* c, int64_t n, const int32_t* rowptr, const int32_t
     c->kl_cut0.ensure(16);
     c->kl_out.ensure(sizeof(ek::dev::KLOut));
     c->kl_count.ensure(64);
+    pt.mark("segments queued");
     HIPCHK(hipStreamSynchronize(s));
+    pt.mark("synchronised");
     c->kl_graph_ready = true;
     c->kl_part_ready = false;
     return EK_OK;

@@ -6,6 +6,7 @@ timeout -k 10 120 python3 -c "
 import importlib.util
 spec=importlib.util.spec_from_file_location('ek','eig-kl-algorithm_amd/__init__.py'); ek=importlib.util.module_from_spec(spec); spec.loader.exec_module(ek)
 ek.Hypergraph.generate(1.15,1).largest_component()[0].write('/tmp/h115.hgr')" || exit 1
+: > $GRAFT_REPO_ROOT/gpurun_out/cold_kl_trace.txt
 cd /tmp/ekck
 for g in 1 0; do
   echo "=== EK_LANCZOS_GRAPH=$g" >> $GRAFT_REPO_ROOT/gpurun_out/cold_kl_trace.txt
