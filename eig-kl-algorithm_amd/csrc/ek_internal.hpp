@@ -112,7 +112,9 @@ void build_kl_graph(const ek_hgr& h, ek_csr& out);
 // (first insertion) in the given order; writes the iteration order to out.
 void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch);
 void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch,
-                     std::vector<int32_t>& bk0, std::vector<int32_t>& bk1);  // (reused bucket arrays)
+                     std::vector<int32_t>& bk0, std::vector<int32_t>& bk1);
+void hashtable_order_index(const uint32_t* keys, int64_t cnt, int32_t* out_idx, std::vector<int32_t>& scratch,
+                           std::vector<int32_t>& bk0, std::vector<int32_t>& bk1);  // (reused bucket arrays)
 uint64_t hashtable_next_buckets(uint64_t cur);  // bucket count after the rehash that follows `cur`
 
 // host_linalg.cpp — small dense/tridiagonal kernels for the IRL driver

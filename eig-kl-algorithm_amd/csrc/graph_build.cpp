@@ -49,6 +49,14 @@ void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vect
 // (bk0 / bk1: the bucket arrays, reused across calls: no allocation per row)
 void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vector<int32_t>& scratch,
                      std::vector<int32_t>& bk0, std::vector<int32_t>& bk1) {
+    std::vector<int32_t> idx(static_cast<size_t>(cnt));
+    hashtable_order_index(keys, cnt, idx.data(), scratch, bk0, bk1);
+    for (int64_t q = 0; q < cnt; ++q) out[q] = keys[idx[size_t(q)]];
+}
+// the same iteration order as indices into keys (out_idx[q] = p: keys[p] is
+// the q-th key iterated)
+void hashtable_order_index(const uint32_t* keys, int64_t cnt, int32_t* out_idx, std::vector<int32_t>& scratch,
+                           std::vector<int32_t>& bk0, std::vector<int32_t>& bk1) {
     constexpr int32_t NIL = -1, BB = -2, EMPTY = -3;
     if (cnt == 0) return;
     scratch.resize(size_t(cnt));
@@ -122,7 +130,7 @@ void hashtable_order(const uint32_t* keys, int64_t cnt, uint32_t* out, std::vect
         ++count;
     }
     int64_t q = 0;
-    for (int32_t p = head; p != NIL; p = next[p]) out[q++] = keys[p];
+    for (int32_t p = head; p != NIL; p = next[p]) out_idx[q++] = p;
 }
 
 // ---------------------------------------------------------------------------
@@ -387,11 +395,47 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
         std::vector<std::pair<int64_t, std::pair<uint32_t, float>>> first;  // (first pair, (key, sum))
         std::vector<uint32_t> keys, order;
         std::vector<std::pair<uint32_t, float>> bykey;
+        std::vector<float> dsum;
+        std::vector<int32_t> oidx;
         for (int64_t a = lo; a < hi; ++a) {
             const int64_t b = cnt[size_t(a)], e = cnt[size_t(a) + 1];
             if (b == e) {
                 P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
                 fcnt[size_t(a)] = 0;
+                continue;
+            }
+            if (e - b <= 64) {
+                // a short row (all but hubs): its distinct keys in first-
+                // occurrence order and their sums in pair order, by a linear
+                // search — the sort path's keys and fp32 sums, without sorting
+                keys.clear();
+                dsum.clear();
+                for (int64_t x = b; x < e; ++x) {
+                    const uint32_t key = pk[size_t(x)];
+                    size_t u = 0;
+                    while (u < keys.size() && keys[u] != key) ++u;
+                    if (u == keys.size()) {
+                        keys.push_back(key);
+                        dsum.push_back(0.0f + pw[size_t(x)]);  // operator[]'s 0.0f, then += in pair order
+                    } else {
+                        dsum[u] += pw[size_t(x)];
+                    }
+                }
+                oidx.resize(keys.size());
+                try {
+                    hashtable_order_index(keys.data(), int64_t(keys.size()), oidx.data(), scratch, bk0, bk1);
+                } catch (const Error&) {
+                    too_big = true;
+                    return;
+                }
+                for (int32_t p : oidx) {
+                    const uint32_t key = keys[size_t(p)];
+                    P.key.push_back(key);
+                    P.w.push_back(dsum[size_t(p)]);
+                    if (int64_t(key) != a) ++bc[key];
+                }
+                fcnt[size_t(a)] = int32_t(oidx.size());
+                P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
                 continue;
             }
             idx.resize(size_t(e - b));
