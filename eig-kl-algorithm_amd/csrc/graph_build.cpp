@@ -59,6 +59,31 @@ void hashtable_order_index(const uint32_t* keys, int64_t cnt, int32_t* out_idx, 
                            std::vector<int32_t>& bk0, std::vector<int32_t>& bk1) {
     constexpr int32_t NIL = -1, BB = -2, EMPTY = -3;
     if (cnt == 0) return;
+    if (cnt <= 13) {
+        // the first insert rehashes to 13 buckets and the next rehash comes
+        // at the 14th key: a short row's whole life at B = 13 (the loop
+        // below with a constant modulus and stack arrays)
+        int32_t bkt[13], next[13], head = NIL;
+        for (int32_t& x : bkt) x = EMPTY;
+        for (int32_t node = 0; node < int32_t(cnt); ++node) {
+            const uint32_t b = keys[node] % 13u;
+            if (bkt[b] == EMPTY) {
+                next[node] = head;
+                head = node;
+                if (next[node] != NIL) bkt[keys[next[node]] % 13u] = node;
+                bkt[b] = BB;
+            } else if (bkt[b] == BB) {
+                next[node] = head;
+                head = node;
+            } else {
+                next[node] = next[bkt[b]];
+                next[bkt[b]] = node;
+            }
+        }
+        int64_t q = 0;
+        for (int32_t p = head; p != NIL; p = next[p]) out_idx[q++] = p;
+        return;
+    }
     scratch.resize(size_t(cnt));
     int32_t* next = scratch.data();
     std::vector<int32_t>* cur_b = &bk0;
@@ -298,64 +323,69 @@ void build_laplacian(const ek_hgr& h, ek_csr& L) { build_laplacian_rows(h, 0, h.
 
 // ---------------------------------------------------------------------------
 // cKL.cpp:107-131 + connections() order (cKL.cpp:229-248).
-// Every phase parallel, no atomics, no per-row allocations (round 4; the
-// round-3 form counted and filled one global pair list net by net on one
-// thread and kept a std::vector per row: ~20 ms on the box's host, against a
-// ~22 ms Lanczos solve it has to hide behind).  Thread t owns the nets
-// [nets t/T, nets (t+1)/T) in phase A and the rows [n t/T, n (t+1)/T) in
-// phases B and C; per-thread counts (T x n, one array reused) give every
-// thread its own slots, in thread order:
-//   A. pairs (j < q) of every net, filed under their smaller endpoint: a row's
-//      slots from thread t precede thread t+1's, and each thread walks its
-//      nets in order, so every row's pairs lie in the reference's loop order;
-//   B. per row: its pairs stable-sorted by key (each key's pairs in loop
-//      order, summed in fp32 in that order); the keys in first-pair order
-//      (the map's insertion order) through the emulated map iteration, into
-//      the thread's own buffer;
-//   C. forward parts copied into place; backward parts (for node k, the rows
-//      i < k holding k) scattered to per-thread slots, which puts them in
-//      ascending row order without a sort.
+// Every phase parallel, no atomics, no per-row allocations, and no per-thread
+// arrays of n counts (round 6: the T x n count matrix of round 4, 128 MB at
+// the 10x graph on 16 threads, was zeroed and walked four times).  Rows go to
+// T owners by a multiply-shift (owner(r) = r M >> 32, nondecreasing), so each
+// owner holds a contiguous row range.  Thread t walks the nets
+// [nets t/T, nets (t+1)/T) in phase A and owner t's rows in phases B and C:
+//   A. pairs (j < q) of every net, by smaller endpoint: counted per (thread,
+//      owner), then written to the owner's bucket in thread order — so each
+//      row's pairs lie in the reference's loop order — and sorted by row
+//      within the owner (a stable counting sort over its own rows);
+//   B. per row: distinct keys in first-pair order (the map's insertion
+//      order) with their pairs' fp32 sums in loop order, then through the
+//      emulated map iteration, into the thread's own buffer;
+//   C. backward parts (for node k, the rows i < k holding k): every forward
+//      entry is bucketed by k's owner in row order and counting-sorted by k,
+//      which puts each list in ascending row order without a comparison sort.
 // The result is the round-3 form's, bit for bit (test_kl_graph_matches_oracle,
 // test_kl_row_order_*, test_kl_graph_repeated_pins).
 void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     PhaseTimer pt("kl_graph");
     const int64_t n = h.nodes, nets = h.nets;
     const int T = int(std::max<int64_t>(1, std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 4096))));
-    dvec<int32_t> loc(static_cast<size_t>(T) * static_cast<size_t>(n));  // per-thread counts, then slots (within a row)
-    auto zero_loc = [&](int t) {
-        std::memset(loc.data() + size_t(t) * size_t(n), 0, size_t(n) * sizeof(int32_t));
+    const uint64_t M = n > 0 ? (uint64_t(T) << 32) / uint64_t(n) : 0;
+    auto owner = [M](uint64_t r) { return int(uint64_t(r * M) >> 32); };  // < T for r < n
+    std::vector<int64_t> lo(size_t(T) + 1);  // owner u's rows: [lo[u], lo[u + 1])
+    for (int u = 0; u <= T; ++u) {
+        int64_t r = (u == T || M == 0) ? n : std::min<int64_t>(n, int64_t((uint64_t(u) << 32) / M));
+        while (r > 0 && owner(uint64_t(r - 1)) >= u) --r;
+        while (r < n && owner(uint64_t(r)) < u) ++r;
+        lo[size_t(u)] = r;
+    }
+    // per (thread, owner) counts -> slot bases: bucket u holds threads 0..T-1 in order
+    std::vector<int64_t> hc(size_t(T) * size_t(T));
+    std::vector<int64_t> base(size_t(T) + 1);
+    auto bucket_bases = [&]() {
+        int64_t run = 0;
+        for (int u = 0; u < T; ++u) {
+            base[size_t(u)] = run;
+            for (int t = 0; t < T; ++t) {
+                int64_t& x = hc[size_t(t) * size_t(T) + size_t(u)];
+                const int64_t v = x;
+                x = run;
+                run += v;
+            }
+        }
+        base[size_t(T)] = run;
     };
     // A. pairs by smaller endpoint
     run_threads(T, [&](int t) {
-        zero_loc(t);
-        int32_t* c = loc.data() + size_t(t) * size_t(n);
+        int64_t* c = hc.data() + size_t(t) * size_t(T);
         for (int64_t e = nets * t / T; e < nets * (t + 1) / T; ++e) {
             const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
             const int32_t* pe = h.pins.data() + p0;
             for (int64_t j = 0; j + 1 < k; ++j)
-                for (int64_t q = j + 1; q < k; ++q) ++c[std::min(pe[j], pe[q])];
+                for (int64_t q = j + 1; q < k; ++q) ++c[owner(uint32_t(std::min(pe[j], pe[q])))];
         }
     });
-    dvec<int64_t> cnt(static_cast<size_t>(n) + 1);
-    run_threads(T, [&](int t) {  // per row: the total, and each thread's slot base relative to the row
-        for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
-            int64_t run = 0;
-            for (int u = 0; u < T; ++u) {
-                int32_t& x = loc[size_t(u) * size_t(n) + size_t(r)];
-                const int64_t v = x;
-                x = int32_t(run);
-                run += v;
-            }
-            cnt[size_t(r) + 1] = run;
-        }
-    });
-    cnt[0] = 0;
-    for (int64_t i = 0; i < n; ++i) cnt[size_t(i) + 1] += cnt[size_t(i)];
-    const int64_t npairs = cnt[size_t(n)];
-    dvec<uint32_t> pk(static_cast<size_t>(npairs));
-    dvec<float> pw(static_cast<size_t>(npairs));
+    bucket_bases();
+    const int64_t npairs = base[size_t(T)];
+    dvec<uint32_t> tr(static_cast<size_t>(npairs)), tk(static_cast<size_t>(npairs));  // bucketed (row, key)
+    dvec<float> tw(static_cast<size_t>(npairs));
     run_threads(T, [&](int t) {
-        int32_t* c = loc.data() + size_t(t) * size_t(n);
+        int64_t* c = hc.data() + size_t(t) * size_t(T);
         for (int64_t e = nets * t / T; e < nets * (t + 1) / T; ++e) {
             const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
             if (k < 2) continue;
@@ -363,13 +393,32 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
             const int32_t* pe = h.pins.data() + p0;
             for (int64_t j = 0; j + 1 < k; ++j)
                 for (int64_t q = j + 1; q < k; ++q) {
-                    const int32_t a = std::min(pe[j], pe[q]), b = std::max(pe[j], pe[q]);
-                    const int64_t at = cnt[size_t(a)] + c[a]++;
-                    pk[size_t(at)] = uint32_t(b);
-                    pw[size_t(at)] = weight;
+                    const uint32_t a = uint32_t(std::min(pe[j], pe[q])), b = uint32_t(std::max(pe[j], pe[q]));
+                    const int64_t at = c[owner(a)]++;
+                    tr[size_t(at)] = a;
+                    tk[size_t(at)] = b;
+                    tw[size_t(at)] = weight;
                 }
         }
     });
+    dvec<int64_t> cnt(static_cast<size_t>(n) + 1);
+    dvec<uint32_t> pk(static_cast<size_t>(npairs));
+    dvec<float> pw(static_cast<size_t>(npairs));
+    run_threads(T, [&](int u) {  // owner u: its bucket counting-sorted by row (stable)
+        const int64_t r0 = lo[size_t(u)], r1 = lo[size_t(u) + 1], s0 = base[size_t(u)], s1 = base[size_t(u) + 1];
+        std::vector<int64_t> cur(size_t(r1 - r0) + 1, 0);
+        for (int64_t x = s0; x < s1; ++x) ++cur[size_t(tr[size_t(x)] - r0) + 1];
+        cur[0] = s0;
+        for (int64_t r = r0; r < r1; ++r) cur[size_t(r - r0) + 1] += cur[size_t(r - r0)];
+        for (int64_t r = r0; r <= r1; ++r)
+            if (r < r1 || u == T - 1) cnt[size_t(r)] = cur[size_t(r - r0)];
+        for (int64_t x = s0; x < s1; ++x) {
+            const int64_t at = cur[size_t(tr[size_t(x)] - r0)]++;
+            pk[size_t(at)] = tk[size_t(x)];
+            pw[size_t(at)] = tw[size_t(x)];
+        }
+    });
+    if (n == 0) cnt[0] = 0;
     pt.mark("pairs");
     // B. rows: forward lists in map order, per thread, rows in order
     struct Part {
@@ -380,16 +429,16 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     std::vector<Part> parts(static_cast<size_t>(T));
     dvec<int32_t> fcnt(static_cast<size_t>(n));
     std::atomic<bool> too_big{false};
+    std::fill(hc.begin(), hc.end(), 0);  // now: thread t's backward entries by their node's owner
     run_threads(T, [&](int t) {
-        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        const int64_t r0 = lo[size_t(t)], r1 = lo[size_t(t) + 1];
         Part& P = parts[size_t(t)];
-        P.off.assign(size_t(hi - lo) + 1, 0);
+        P.off.assign(size_t(r1 - r0) + 1, 0);
         P.key.clear();
         P.w.clear();
-        P.key.reserve(size_t(cnt[size_t(hi)] - cnt[size_t(lo)]));
-        P.w.reserve(size_t(cnt[size_t(hi)] - cnt[size_t(lo)]));
-        zero_loc(t);  // (now: this thread's backward counts per node)
-        int32_t* bc = loc.data() + size_t(t) * size_t(n);
+        P.key.reserve(size_t(cnt[size_t(r1)] - cnt[size_t(r0)]));
+        P.w.reserve(size_t(cnt[size_t(r1)] - cnt[size_t(r0)]));
+        int64_t* bc = hc.data() + size_t(t) * size_t(T);
         std::vector<int64_t> idx;
         std::vector<int32_t> scratch, bk0, bk1;
         std::vector<std::pair<int64_t, std::pair<uint32_t, float>>> first;  // (first pair, (key, sum))
@@ -397,10 +446,10 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
         std::vector<std::pair<uint32_t, float>> bykey;
         std::vector<float> dsum;
         std::vector<int32_t> oidx;
-        for (int64_t a = lo; a < hi; ++a) {
+        for (int64_t a = r0; a < r1; ++a) {
             const int64_t b = cnt[size_t(a)], e = cnt[size_t(a) + 1];
             if (b == e) {
-                P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
+                P.off[size_t(a - r0) + 1] = int64_t(P.key.size());
                 fcnt[size_t(a)] = 0;
                 continue;
             }
@@ -432,27 +481,15 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
                     const uint32_t key = keys[size_t(p)];
                     P.key.push_back(key);
                     P.w.push_back(dsum[size_t(p)]);
-                    if (int64_t(key) != a) ++bc[key];
+                    if (int64_t(key) != a) ++bc[owner(key)];
                 }
                 fcnt[size_t(a)] = int32_t(oidx.size());
-                P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
+                P.off[size_t(a - r0) + 1] = int64_t(P.key.size());
                 continue;
             }
             idx.resize(size_t(e - b));
             std::iota(idx.begin(), idx.end(), b);
-            // (std::stable_sort allocates a merge buffer per call: small rows
-            // take a stable insertion sort instead)
-            if (idx.size() <= 48) {
-                for (size_t u = 1; u < idx.size(); ++u) {
-                    const int64_t x = idx[u];
-                    const uint32_t kx = pk[size_t(x)];
-                    size_t v = u;
-                    for (; v > 0 && pk[size_t(idx[v - 1])] > kx; --v) idx[v] = idx[v - 1];
-                    idx[v] = x;
-                }
-            } else {
-                std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return pk[size_t(x)] < pk[size_t(y)]; });
-            }
+            std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return pk[size_t(x)] < pk[size_t(y)]; });
             first.clear();
             bykey.clear();
             for (size_t u = 0; u < idx.size();) {
@@ -477,60 +514,71 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
                 const auto it = std::lower_bound(bykey.begin(), bykey.end(), std::make_pair(key, -INFINITY));
                 P.key.push_back(key);
                 P.w.push_back(it->second);
-                if (int64_t(key) != a) ++bc[key];
+                if (int64_t(key) != a) ++bc[owner(key)];
             }
             fcnt[size_t(a)] = int32_t(order.size());
-            P.off[size_t(a - lo) + 1] = int64_t(P.key.size());
+            P.off[size_t(a - r0) + 1] = int64_t(P.key.size());
         }
     });
     if (too_big) fail(EK_EINVAL, "hash-order emulation: a row exceeds the bucket table");
     pt.mark("rows + map order");
-    // C. assemble
-    dvec<int64_t> bcnt(static_cast<size_t>(n));
-    run_threads(T, [&](int t) {  // per node: backward total, each thread's slot base relative to its list
-        for (int64_t r = n * t / T; r < n * (t + 1) / T; ++r) {
-            int64_t run = 0;
-            for (int u = 0; u < T; ++u) {
-                int32_t& x = loc[size_t(u) * size_t(n) + size_t(r)];
-                const int64_t v = x;
-                x = int32_t(run);
-                run += v;
+    // C. assemble: backward entries bucketed by their node's owner, rows ascending
+    bucket_bases();
+    run_threads(T, [&](int t) {  // (reuses the pair buckets: backward entries <= pairs)
+        const int64_t r0 = lo[size_t(t)], r1 = lo[size_t(t) + 1];
+        const Part& P = parts[size_t(t)];
+        int64_t* c = hc.data() + size_t(t) * size_t(T);
+        for (int64_t r = r0; r < r1; ++r)
+            for (int64_t q = P.off[size_t(r - r0)]; q < P.off[size_t(r - r0) + 1]; ++q) {
+                const uint32_t k = P.key[size_t(q)];
+                if (int64_t(k) == r) continue;
+                const int64_t at = c[owner(k)]++;
+                tk[size_t(at)] = k;
+                tr[size_t(at)] = uint32_t(r);
+                tw[size_t(at)] = P.w[size_t(q)];
             }
-            bcnt[size_t(r)] = run;
-        }
     });
+    std::vector<int64_t> rsum(size_t(T) + 1, 0);  // per owner: its rows' lengths, then their offsets
+    std::vector<std::vector<int32_t>> bcur(static_cast<size_t>(T));
+    run_threads(T, [&](int u) {
+        const int64_t r0 = lo[size_t(u)], r1 = lo[size_t(u) + 1];
+        std::vector<int32_t>& bk = bcur[size_t(u)];
+        bk.assign(size_t(r1 - r0), 0);
+        for (int64_t x = base[size_t(u)]; x < base[size_t(u) + 1]; ++x) ++bk[size_t(tk[size_t(x)] - r0)];
+        int64_t s = 0;
+        for (int64_t r = r0; r < r1; ++r) s += int64_t(fcnt[size_t(r)]) + bk[size_t(r - r0)];
+        rsum[size_t(u) + 1] = s;
+    });
+    for (int u = 0; u < T; ++u) rsum[size_t(u) + 1] += rsum[size_t(u)];
+    if (rsum[size_t(T)] > INT32_MAX) fail(EK_EINVAL, "KL graph nnz exceeds int32");
     G.nrows = n;
     G.value_bytes = 4;
     G.rowptr.resize(size_t(n) + 1);
     G.nfwd.resize(size_t(n));
     G.rowptr[0] = 0;
-    for (int64_t r = 0; r < n; ++r) {
-        const int64_t len = int64_t(fcnt[size_t(r)]) + bcnt[size_t(r)];
-        if (int64_t(G.rowptr[size_t(r)]) + len > INT32_MAX) fail(EK_EINVAL, "KL graph nnz exceeds int32");
-        G.rowptr[size_t(r) + 1] = G.rowptr[size_t(r)] + int32_t(len);
-    }
-    G.col.resize(size_t(G.rowptr[size_t(n)]));
-    G.val32.resize(size_t(G.rowptr[size_t(n)]));
-    run_threads(T, [&](int t) {
-        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
-        const Part& P = parts[size_t(t)];
-        int32_t* bs = loc.data() + size_t(t) * size_t(n);
-        for (int64_t r = lo; r < hi; ++r) {  // forward part
+    G.col.resize(size_t(rsum[size_t(T)]));
+    G.val32.resize(size_t(rsum[size_t(T)]));
+    run_threads(T, [&](int u) {
+        const int64_t r0 = lo[size_t(u)], r1 = lo[size_t(u) + 1];
+        const Part& P = parts[size_t(u)];
+        std::vector<int32_t>& bk = bcur[size_t(u)];
+        int64_t p = rsum[size_t(u)];
+        for (int64_t r = r0; r < r1; ++r) {  // rowptr; forward part; bk becomes the backward cursor
             G.nfwd[size_t(r)] = fcnt[size_t(r)];
-            int64_t p = G.rowptr[size_t(r)];
-            for (int64_t q = P.off[size_t(r - lo)]; q < P.off[size_t(r - lo) + 1]; ++q) {
+            for (int64_t q = P.off[size_t(r - r0)]; q < P.off[size_t(r - r0) + 1]; ++q) {
                 G.col[size_t(p)] = int32_t(P.key[size_t(q)]);
                 G.val32[size_t(p++)] = P.w[size_t(q)];
             }
+            const int32_t nb = bk[size_t(r - r0)];
+            bk[size_t(r - r0)] = int32_t(p);
+            p += nb;
+            G.rowptr[size_t(r) + 1] = int32_t(p);
         }
-        for (int64_t r = lo; r < hi; ++r)  // backward parts: this thread's slots, rows ascending
-            for (int64_t q = P.off[size_t(r - lo)]; q < P.off[size_t(r - lo) + 1]; ++q) {
-                const int64_t k = P.key[size_t(q)];
-                if (k == r) continue;
-                const int64_t pos = G.rowptr[size_t(k)] + fcnt[size_t(k)] + bs[k]++;
-                G.col[size_t(pos)] = int32_t(r);
-                G.val32[size_t(pos)] = P.w[size_t(q)];
-            }
+        for (int64_t x = base[size_t(u)]; x < base[size_t(u) + 1]; ++x) {  // backward parts, rows ascending
+            const int32_t at = bk[size_t(tk[size_t(x)] - r0)]++;
+            G.col[size_t(at)] = int32_t(tr[size_t(x)]);
+            G.val32[size_t(at)] = tw[size_t(x)];
+        }
     });
     pt.mark("assemble");
 }
