@@ -35,14 +35,18 @@ void chk(int rc) {
 // The KL adjacency (cKL.cpp:84-149, hash-order emulation) built on host
 // threads, then uploaded with the nets (the device-side inline segments and
 // weight codes included) on the context's KL stream: all of it while the GPU
-// runs the Lanczos solve on the main stream.  The host copy is freed here
-// too, off the solve's path (freeing ~10 MB that several threads touched
-// cost the solve's thread ~2.5 ms at the end of a step).
+// runs the Lanczos solve on the main stream.  A small host copy is freed
+// here too, off the solve's path (freeing ~10 MB that several threads
+// touched cost the solve's thread ~2.5 ms at the end of a step).  A large
+// one goes back to the caller, which frees it on another thread while the
+// KL loop runs: the 10x graph's ~100 MB took ~20 ms to unmap, and this
+// thread's end is on the path between Lanczos and KL there.
 // Its errors come back as {status, message}: the message was written to this
 // thread's ek_last_error(), which the caller's thread cannot see.
 struct ThreadStatus {
     int code = EK_OK;
     std::string msg;
+    std::unique_ptr<ek_csr> host_copy;  // (large graphs) for the caller to free off the path
 };
 // The host build needs no context: in a fresh process it runs while the HIP
 // runtime starts (get_ctx waits for that only before the uploads).
@@ -51,14 +55,15 @@ ThreadStatus kl_graph_host(const std::function<ek_ctx*()>* get_ctx, const ek_hgr
     try {
         PhaseTimer pt("kl_thread");
         ThreadCap cap(threads);
-        ek_csr G;
-        build_kl_graph(*h, G);
+        auto G = std::make_unique<ek_csr>();
+        build_kl_graph(*h, *G);
         pt.mark("graph built");
         ek_ctx* ctx = (*get_ctx)();
-        chk(ek_kl_graph_setup(ctx, h->nodes, G.rowptr.data(), G.col.data(), G.val32.data()));
+        chk(ek_kl_graph_setup(ctx, h->nodes, G->rowptr.data(), G->col.data(), G->val32.data()));
         pt.mark("graph set up");
         chk(ek_kl_nets_setup(ctx, h->nets, h->net_ptr.data(), h->pins.data()));
         pt.mark("nets set up");
+        if (G->col.size() >= (size_t(1) << 22)) st.host_copy = std::move(G);  // (>= 32 MB of col + val)
     } catch (...) {
         st.code = guard_exceptions();
         st.msg = ek_last_error();
@@ -212,7 +217,17 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     auto t = clk::now();
     // graph and nets set up on the context (KL stream, synchronised); a
     // failure there is re-raised here with its message
-    if (const ThreadStatus st = kg.get(); st.code != EK_OK) fail(st.code, "KL graph setup: %s", st.msg.c_str());
+    std::future<void> host_copy_freed;  // (joined when solve returns, long after it is done)
+    {
+        ThreadStatus st = kg.get();
+        if (st.code != EK_OK) fail(st.code, "KL graph setup: %s", st.msg.c_str());
+        if (st.host_copy)
+            host_copy_freed = std::async(std::launch::async, [p = std::move(st.host_copy)]() mutable {
+                PhaseTimer pt("kl_host_copy");
+                p.reset();
+                pt.mark("freed");
+            });
+    }
     r.t_kl_graph_wait = since(t);
     t = clk::now();
     int64_t n0 = int64_t(order0.size()), n1 = int64_t(order1.size());
