@@ -97,6 +97,38 @@ def test_kl_graph_repeated_pins(ek, oracle, tmp_path):
     assert np.array_equal(G.val.view(np.uint32), w.view(np.uint32))
 
 
+_KL_HASH_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from conftest import load_package
+G = load_package().Hypergraph.read(sys.argv[2]).kl_graph()
+m = hashlib.md5()
+for a in (G.rowptr, G.col, G.nfwd, G.val.view(np.uint32)):
+    m.update(np.ascontiguousarray(a).tobytes())
+print(m.hexdigest())
+"""
+
+
+def test_kl_graph_thread_count_invariant(ek, oracle, tmp_path):
+    """The adjacency build splits nets and rows over T host threads (row owners
+    by multiply-shift, graph_build.cpp build_kl_graph): the CSR must be the same
+    bits for every T, including T that do not divide n, and equal the oracle's."""
+    path = str(tmp_path / "g.hgr")
+    ek.Hypergraph.generate(0.3, 5).write(path)  # 60,576 nodes: up to 14 threads
+    G = ek.Hypergraph.read(path).kl_graph()
+    rp, col, w, nf = oracle.Graph.read(path).kl_csr()
+    assert np.array_equal(G.rowptr, rp) and np.array_equal(G.col, col) and np.array_equal(G.nfwd, nf)
+    assert np.array_equal(G.val.view(np.uint32), w.view(np.uint32))
+    digests = set()
+    for t in (1, 3, 7, 16):
+        env = dict(os.environ, EK_THREADS=str(t))
+        out = subprocess.run(["python3", "-c", _KL_HASH_SCRIPT, os.path.join(REPO, "tests"), path], env=env,
+                             check=True, capture_output=True, text=True, timeout=300).stdout
+        digests.add(out.strip().splitlines()[-1])
+    assert len(digests) == 1, digests
+
+
 @pytest.mark.parametrize("name", ["fract", "ibm01", "industry2"])
 def test_laplacian_matches_oracle(ek, oracle, name):
     L = ek.Hypergraph.read(circuit_path(name)).laplacian()
