@@ -19,6 +19,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <system_error>
 
 #include "ek_internal.hpp"
 
@@ -221,12 +222,17 @@ void solve(const std::function<ek_ctx*()>& get_ctx, int rank, int nranks, const 
     {
         ThreadStatus st = kg.get();
         if (st.code != EK_OK) fail(st.code, "KL graph setup: %s", st.msg.c_str());
-        if (st.host_copy)
-            host_copy_freed = std::async(std::launch::async, [p = std::move(st.host_copy)]() mutable {
-                PhaseTimer pt("kl_host_copy");
-                p.reset();
-                pt.mark("freed");
-            });
+        if (st.host_copy) {
+            try {
+                host_copy_freed = std::async(std::launch::async, [p = std::move(st.host_copy)]() mutable {
+                    PhaseTimer pt("kl_host_copy");
+                    p.reset();
+                    pt.mark("freed");
+                });
+            } catch (const std::system_error&) {
+                // no thread to spare: the copy was freed here, with the lambda
+            }
+        }
     }
     r.t_kl_graph_wait = since(t);
     t = clk::now();
