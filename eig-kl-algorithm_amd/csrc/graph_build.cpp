@@ -245,8 +245,10 @@ void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& L) {
     std::vector<int32_t> rlen(size_t(nr), 0);
     auto work = [&](int t) {
         const int64_t lo = nr * t / T, hi = nr * (t + 1) / T;
-        auto& oc = tcol[size_t(t)];
-        auto& ov = tval[size_t(t)];
+        // (built in locals and moved out at the end: the threads' vectors sit
+        // side by side in tcol / tval, and push_back writes their ends)
+        std::vector<int32_t> oc;
+        std::vector<double> ov;
         oc.reserve(size_t(ip[size_t(hi)] - ip[size_t(lo)]) * 4 + 16);
         ov.reserve(oc.capacity());
         std::vector<std::pair<int32_t, double>> row;
@@ -299,6 +301,8 @@ void build_laplacian_rows(const ek_hgr& h, int64_t r0, int64_t r1, ek_csr& L) {
             }
             rlen[size_t(i)] = int32_t(oc.size() - base);
         }
+        tcol[size_t(t)] = std::move(oc);
+        tval[size_t(t)] = std::move(ov);
     };
     run_threads(T, work);
     pt.mark("rows");
@@ -355,14 +359,18 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
         lo[size_t(u)] = r;
     }
     // per (thread, owner) counts -> slot bases: bucket u holds threads 0..T-1 in order
-    std::vector<int64_t> hc(size_t(T) * size_t(T));
+    // (rows HS int64 apart, HS a whole number of 64-B lines plus one: no two
+    // threads' counters share a cache line — the counts are incremented per
+    // pair, and a shared line cost the rows phase most of its thread scaling)
+    const size_t HS = (size_t(T) + 7) / 8 * 8 + 8;
+    std::vector<int64_t> hc(size_t(T) * HS);
     std::vector<int64_t> base(size_t(T) + 1);
     auto bucket_bases = [&]() {
         int64_t run = 0;
         for (int u = 0; u < T; ++u) {
             base[size_t(u)] = run;
             for (int t = 0; t < T; ++t) {
-                int64_t& x = hc[size_t(t) * size_t(T) + size_t(u)];
+                int64_t& x = hc[size_t(t) * HS + size_t(u)];
                 const int64_t v = x;
                 x = run;
                 run += v;
@@ -372,7 +380,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     };
     // A. pairs by smaller endpoint
     run_threads(T, [&](int t) {
-        int64_t* c = hc.data() + size_t(t) * size_t(T);
+        int64_t* c = hc.data() + size_t(t) * HS;
         for (int64_t e = nets * t / T; e < nets * (t + 1) / T; ++e) {
             const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
             const int32_t* pe = h.pins.data() + p0;
@@ -385,7 +393,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     dvec<uint32_t> tr(static_cast<size_t>(npairs)), tk(static_cast<size_t>(npairs));  // bucketed (row, key)
     dvec<float> tw(static_cast<size_t>(npairs));
     run_threads(T, [&](int t) {
-        int64_t* c = hc.data() + size_t(t) * size_t(T);
+        int64_t* c = hc.data() + size_t(t) * HS;
         for (int64_t e = nets * t / T; e < nets * (t + 1) / T; ++e) {
             const int64_t p0 = h.net_ptr[size_t(e)], k = h.net_ptr[size_t(e) + 1] - p0;
             if (k < 2) continue;
@@ -421,7 +429,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     if (n == 0) cnt[0] = 0;
     pt.mark("pairs");
     // B. rows: forward lists in map order, per thread, rows in order
-    struct Part {
+    struct alignas(64) Part {  // (own cache lines: push_back writes the vectors' ends)
         std::vector<uint32_t> key;
         std::vector<float> w;
         std::vector<int64_t> off;  // row r's entries at [off[r - lo], off[r - lo + 1])
@@ -438,7 +446,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
         P.w.clear();
         P.key.reserve(size_t(cnt[size_t(r1)] - cnt[size_t(r0)]));
         P.w.reserve(size_t(cnt[size_t(r1)] - cnt[size_t(r0)]));
-        int64_t* bc = hc.data() + size_t(t) * size_t(T);
+        int64_t* bc = hc.data() + size_t(t) * HS;
         std::vector<int64_t> idx;
         std::vector<int32_t> scratch, bk0, bk1;
         std::vector<std::pair<int64_t, std::pair<uint32_t, float>>> first;  // (first pair, (key, sum))
@@ -527,7 +535,7 @@ void build_kl_graph(const ek_hgr& h, ek_csr& G) {
     run_threads(T, [&](int t) {  // (reuses the pair buckets: backward entries <= pairs)
         const int64_t r0 = lo[size_t(t)], r1 = lo[size_t(t) + 1];
         const Part& P = parts[size_t(t)];
-        int64_t* c = hc.data() + size_t(t) * size_t(T);
+        int64_t* c = hc.data() + size_t(t) * HS;
         for (int64_t r = r0; r < r1; ++r)
             for (int64_t q = P.off[size_t(r - r0)]; q < P.off[size_t(r - r0) + 1]; ++q) {
                 const uint32_t k = P.key[size_t(q)];
