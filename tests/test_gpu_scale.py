@@ -78,11 +78,14 @@ def test_full_scale_solve_kl_swap_log_matches_oracle(ek, oracle, ctx, mult, seed
     assert res["iterations"] > 5000
 
 
-def test_solve_file_equals_resident_path(ek, ctx, tmp_path):
+@pytest.mark.parametrize("mult,seed", [(1.0, 1), (4.0, 4)])
+def test_solve_file_equals_resident_path(ek, ctx, tmp_path, mult, seed):
     """ek_solve_file (parse -> ... -> results file, bench.py's step) gives the
     resident path's Lanczos bits and swap log, and a results file in cKL's
-    format (cKL.cpp:315, 380)."""
-    h = ek.Hypergraph.generate(1.0, 1)
+    format (cKL.cpp:315, 380).  The 4x graph's KL adjacency (> 4 M entries)
+    takes the path whose host copy is freed on another thread during the KL
+    loop (solve.cpp)."""
+    h = ek.Hypergraph.generate(mult, seed)
     p = str(tmp_path / "syn1.hgr")
     h.write(p)
     lam, v, st, bits = _fiedler_bits(ek, ctx, h)
