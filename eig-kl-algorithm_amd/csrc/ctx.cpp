@@ -90,7 +90,7 @@ struct Uploader {
 };
 
 namespace {
-inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::dev::KL_CHUNK), ek::dev::KL_CHUNK); }
+inline int64_t chunk_pad(int64_t n) { return std::max<int64_t>(round_up(n, ek::dev::KL_CHUNK_PAD), ek::dev::KL_CHUNK_PAD); }
 
 }  // namespace
 

@@ -576,6 +576,16 @@ constexpr int KL_LOOP_THREADS = EK_KL_THREADS;  // 8 waves: 256 VGPRs per lane, 
 #define EK_KL_CHUNK 2048  // (A/B builds: EXTRA_DEFS=-DEK_KL_CHUNK=1024)
 #endif
 constexpr int KL_CHUNK = EK_KL_CHUNK;  // positions per chunk key (a few keys per lane: barrier-free selection)
+// the off-chip-bitmap loop's chunks (k_kl_swap_loop<.., GB>, graphs past the
+// LDS budget): 4096 positions, 3.11 -> 2.90 us a swap at 10x and equal at
+// 3x / 5x (profiles/r06/kl/kl_chunk_big_2048_4096.txt)
+#ifndef EK_KL_CHUNK_GB
+#define EK_KL_CHUNK_GB 4096
+#endif
+constexpr int KL_CHUNK_GB = EK_KL_CHUNK_GB;
+// positions the gain / descriptor arrays are padded to: whole chunks of either size
+constexpr int KL_CHUNK_PAD = KL_CHUNK > KL_CHUNK_GB ? KL_CHUNK : KL_CHUNK_GB;
+static_assert(KL_CHUNK_PAD % KL_CHUNK == 0 && KL_CHUNK_PAD % KL_CHUNK_GB == 0, "chunk sizes must nest");
 struct alignas(16) KLInfo {
     int32_t a, b, c, d;
 };

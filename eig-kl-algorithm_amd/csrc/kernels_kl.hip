@@ -16,7 +16,7 @@
 //   * k_gain_scan   : one lane per row (the sequential fp32 order forbids
 //                     splitting a row), all n rows; also fp64 per-block
 //                     partials of the initial cut.
-//   * k_chunk_init  : one wave64 per KL_CHUNK-position chunk of each remain[]
+//   * k_chunk_init  : one wave64 per chunk (KL_CHUNK positions; KL_CHUNK_GB for the off-chip-bitmap loop) of each remain[]
 //                     list; the chunk's best (gain, first position) packed in
 //                     a 64-bit key whose unsigned max IS the cKL selection
 //                     rule, so a wave64 shuffle max is an exact argmax.
@@ -193,14 +193,15 @@ __device__ __forceinline__ float row_gain(const int32_t* __restrict__ rowptr, co
 // best key of KL_CHUNK consecutive positions of one remain[] list (gains by
 // position).  The gain arrays are padded with NaN (invalid key) to a whole
 // number of chunks, so every load is unconditional and all are in flight at once.
+template <int CH = KL_CHUNK>
 __device__ __forceinline__ u64 chunk_key(const float* __restrict__ gp, int s, int c, int lane) {
-    float g[KL_CHUNK / 64];
+    float g[CH / 64];
 #pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) g[q] = gp[c * KL_CHUNK + q * 64 + lane];
+    for (int q = 0; q < CH / 64; ++q) g[q] = gp[c * CH + q * 64 + lane];
     u64 k = 0ull;
 #pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) {
-        const int p = c * KL_CHUNK + q * 64 + lane;
+    for (int q = 0; q < CH / 64; ++q) {
+        const int p = c * CH + q * 64 + lane;
         const u64 kk = s ? key_min(g[q], p) : key_max(g[q], p);
         k = kk > k ? kk : k;
     }
@@ -267,25 +268,32 @@ __device__ __forceinline__ u64 lane_best(const float* g, int s, int p0, int lane
 // descriptors are both read by position, so the winner needs no dependent
 // load.  Returns the key in every lane; the winner lane (or lane 0 for an
 // all-invalid chunk) has *mine = true and its descriptor in *info.
+// (in blocks of 32 positions a lane: a 4096-position chunk's 64 gains and
+// descriptors would not fit the registers at once; the keys carry their
+// position, so the running max over blocks is the same winner)
+template <int CH = KL_CHUNK>
 __device__ __forceinline__ u64 chunk_best(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
                                           int c, int lane, KLInfo* info, bool* mine) {
-    float g[KL_CHUNK / 64];
-    int4 pi[KL_CHUNK / 64];
-#pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) {  // padded arrays: unconditional, all in flight
-        const int p = c * KL_CHUNK + q * 64 + lane;
-        g[q] = gp[p];
-        pi[q] = *reinterpret_cast<const int4*>(pinfo + p);
-    }
+    constexpr int NB = CH / 64 < 32 ? CH / 64 : 32;
     u64 k = 0ull;
     int4 bi = make_int4(0, 0, 0, 0);
+    for (int q0 = 0; q0 < CH / 64; q0 += NB) {
+        float g[NB];
+        int4 pi[NB];
 #pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) {
-        const int p = c * KL_CHUNK + q * 64 + lane;
-        const u64 kk = s ? key_min(g[q], p) : key_max(g[q], p);
-        if (kk > k) {
-            k = kk;
-            bi = pi[q];
+        for (int q = 0; q < NB; ++q) {  // padded arrays: unconditional, all in flight
+            const int p = c * CH + (q0 + q) * 64 + lane;
+            g[q] = gp[p];
+            pi[q] = *reinterpret_cast<const int4*>(pinfo + p);
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int p = c * CH + (q0 + q) * 64 + lane;
+            const u64 kk = s ? key_min(g[q], p) : key_max(g[q], p);
+            if (kk > k) {
+                k = kk;
+                bi = pi[q];
+            }
         }
     }
     const u64 m = wave_max_u64(k);
@@ -298,6 +306,7 @@ __device__ __forceinline__ u64 chunk_best(const float* __restrict__ gp, const KL
     return m;
 }
 
+template <int CH>
 __global__ __launch_bounds__(256) void k_chunk_init(KLDev d) {
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wv >= d.nck0 + d.nck1) return;
@@ -305,14 +314,14 @@ __global__ __launch_bounds__(256) void k_chunk_init(KLDev d) {
     if (d.pinfo0) {
         KLInfo info;
         bool mine;
-        const u64 k = s ? chunk_best(d.gp1, d.pinfo1, 1, c, lane, &info, &mine)
-                        : chunk_best(d.gp0, d.pinfo0, 0, c, lane, &info, &mine);
+        const u64 k = s ? chunk_best<CH>(d.gp1, d.pinfo1, 1, c, lane, &info, &mine)
+                        : chunk_best<CH>(d.gp0, d.pinfo0, 0, c, lane, &info, &mine);
         if (mine) {
             (s ? d.ckey1 : d.ckey0)[c] = k;
             (s ? d.cinfo1 : d.cinfo0)[c] = info;
         }
     } else {
-        const u64 k = s ? chunk_key(d.gp1, 1, c, lane) : chunk_key(d.gp0, 0, c, lane);
+        const u64 k = s ? chunk_key<CH>(d.gp1, 1, c, lane) : chunk_key<CH>(d.gp0, 0, c, lane);
         if (lane == 0) (s ? d.ckey1 : d.ckey0)[c] = k;
     }
 }
@@ -362,14 +371,15 @@ size_t kl_loop_lds_bytes(const KLDev& d, bool bitmaps, bool fixed) {
 // unconditional and all in flight at once).  Every lane gets the key; the
 // winner lane (lane 0 for an all-invalid chunk) has *mine set and loads the
 // winner's row descriptor into *info.
+template <int CH = KL_CHUNK>
 __device__ __forceinline__ u64 chunk_rescan(const float* __restrict__ gp, const KLInfo* __restrict__ pinfo, int s,
                                             int c, int skip, int lane, KLInfo* info, bool* mine) {
-    float g[KL_CHUNK / 64];
+    float g[CH / 64];
 #pragma unroll
-    for (int q = 0; q < KL_CHUNK / 64; ++q) g[q] = gp[c * KL_CHUNK + q * 64 + lane];
+    for (int q = 0; q < CH / 64; ++q) g[q] = gp[c * CH + q * 64 + lane];
     int bq;
-    const u64 k = lane_best<KL_CHUNK / 64>(g, s, c * KL_CHUNK, lane, skip, &bq);
-    const int bp = c * KL_CHUNK + (bq < 0 ? 0 : bq) * 64 + lane;
+    const u64 k = lane_best<CH / 64>(g, s, c * CH, lane, skip, &bq);
+    const int bp = c * CH + (bq < 0 ? 0 : bq) * 64 + lane;
     const u64 m = wave_max_u64(k);
     const u64 bal = __ballot(m != 0ull && k == m);  // keys carry the position: one lane at most
     *mine = bal ? (lane == __ffsll((long long)bal) - 1) : (lane == 0);
@@ -487,10 +497,13 @@ template <bool PROF, bool SEGC, bool GB = false, bool FIX = false>
 __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int limit, ek_swap* __restrict__ log,
                                                                   long long cap, KLOut* __restrict__ out) {
     constexpr int NW = KL_LOOP_THREADS / 64;
+    // positions per chunk key: larger chunks for the off-chip-bitmap form (fewer
+    // keys for the selection to reduce; kl_loop_form)
+    constexpr int CH = GB ? KL_CHUNK_GB : KL_CHUNK;
     // roles: W_W the pair gain; E_PARTS waves per chunk rescan node1's chunk
     // (waves W_EA, W_EA-1, ...) and E_PARTS node2's (W_EB, W_EB-1, ...);
     // waves 0 .. NG-1 run the gain updates
-    constexpr int E_PARTS = KL_E_PARTS, NQ_E = KL_CHUNK / 64 / E_PARTS;
+    constexpr int E_PARTS = KL_E_PARTS, NQ_E = CH / 64 / E_PARTS;
     constexpr int W_W = NW - 1, W_EA = NW - 2, W_EB = W_EA - E_PARTS, NG = W_EB - E_PARTS + 1;
     constexpr int W_PF = W_W;  // also runs P, the prefetch of the provisional next pair
     constexpr int W_FLIP = W_EA - 1;  // flips the side / lock bitmaps after barrier 1 (an early-rescan wave)
@@ -673,7 +686,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
         }
         if (k0 == 0ull || k1 == 0ull) break;  // cKL.cpp:357,387-388 (identical in every wave)
         const int posA = int(~uint32_t(k0 & 0xffffffffull)), posB = int(~uint32_t(k1 & 0xffffffffull));
-        const int cA = posA / KL_CHUNK, cB = posB / KL_CHUNK;
+        const int cA = posA / CH, cB = posB / CH;
         if (sel) {
             dA = *reinterpret_cast<const v4i*>(ci0 + cA);
             dB = *reinterpret_cast<const v4i*>(ci1 + cB);
@@ -745,7 +758,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             // E. early rescan of the chunk node1 (node2) leaves, E_PARTS waves
             // each taking a contiguous part of it
             const int s = wv <= W_EB ? 1 : 0, part = (s ? W_EB : W_EA) - wv;
-            const int p0 = (s ? cB : cA) * KL_CHUNK + part * NQ_E * 64;
+            const int p0 = (s ? cB : cA) * CH + part * NQ_E * 64;
             // (with both trips' 2 KB a wave instead of 10 KB, the gain-update
             // waves' row loads no longer need a head start: EK_E_SLEEP 0)
             if constexpr (EK_E_SLEEP > 0) __builtin_amdgcn_s_sleep(EK_E_SLEEP);
@@ -861,7 +874,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 // the row's list, position, chunk and that chunk's current key
                 // depend on the descriptor only: read ahead of the sums
                 const uint32_t pl = uint32_t(a.w);
-                const int ls = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / KL_CHUNK;
+                const int ls = int(pl >> 31), pp = int(pl & 0x7fffffffu), c = pp / CH;
                 const bool ab = ls ? c == cB : c == cA;  // node1's / node2's chunk: resolved in G2
                 const u64 K = (ls ? ck1 : ck0)[c];       // stable until the barrier
                 stamp(6);
@@ -1029,8 +1042,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                 if (!(q ? stB : stA)) continue;
                 KLInfo info;
                 bool mine;
-                const u64 kk = q ? chunk_rescan(d.gp1, d.pinfo1, 1, cB, -1, lane, &info, &mine)
-                                 : chunk_rescan(d.gp0, d.pinfo0, 0, cA, -1, lane, &info, &mine);
+                const u64 kk = q ? chunk_rescan<CH>(d.gp1, d.pinfo1, 1, cB, -1, lane, &info, &mine)
+                                 : chunk_rescan<CH>(d.gp0, d.pinfo0, 0, cA, -1, lane, &info, &mine);
                 if (mine) {
                     (q ? ck1 : ck0)[q ? cB : cA] = kk;
                     (q ? ckn1 : ckn0)[q ? cB : cA] = kk;
@@ -1140,7 +1153,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
                     if (s) desc = t;
                 }
                 if (!mS && k != R && k != 0ull)  // an unchanged chunk's winner
-                    desc = *reinterpret_cast<const v4i*>((s ? ci1 : ci0) + int(~uint32_t(k & 0xffffffffull)) / KL_CHUNK);
+                    desc = *reinterpret_cast<const v4i*>((s ? ci1 : ci0) + int(~uint32_t(k & 0xffffffffull)) / CH);
                 if (hl == 0) {
                     nx_key[s] = k;
                     *reinterpret_cast<v4i*>(nx_info + s) = desc;
@@ -1210,7 +1223,7 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             else {  // beyond the LDS item list (hubs): rederive
                 const int u = i < la ? d.col[pa + i] : d.col[pb + i - la];
                 cs = locked_now(u) ? -1 : int((uint32_t(d.nd[u].c) & 0x80000000u) |
-                                                                     ((uint32_t(d.nd[u].c) & 0x7fffffffu) / KL_CHUNK));
+                                                                     ((uint32_t(d.nd[u].c) & 0x7fffffffu) / CH));
             }
             if (cs == -1) continue;
             const int s = int(uint32_t(cs) >> 31), c = cs & 0x7fffffff;
@@ -1223,8 +1236,8 @@ __global__ __launch_bounds__(KL_LOOP_THREADS) void k_kl_swap_loop(KLDev d, int l
             }
             KLInfo info;
             bool mine;
-            const u64 kk = s ? chunk_rescan(d.gp1, d.pinfo1, 1, c, -1, lane, &info, &mine)
-                             : chunk_rescan(d.gp0, d.pinfo0, 0, c, -1, lane, &info, &mine);
+            const u64 kk = s ? chunk_rescan<CH>(d.gp1, d.pinfo1, 1, c, -1, lane, &info, &mine)
+                             : chunk_rescan<CH>(d.gp0, d.pinfo0, 0, c, -1, lane, &info, &mine);
             if (mine) {
                 (s ? ck1 : ck0)[c] = kk;
                 (s ? ckn1 : ckn0)[c] = kk;
@@ -2440,12 +2453,40 @@ void kl_build_desc(hipStream_t s, int n, int n0, int n1, int pad0, int pad1, con
                        plist, rowptr, p0, p1, nd);
 }
 
-void kl_prepare(hipStream_t s, const KLDev& d) {
+namespace {
+KLDev with_chunk(KLDev d, int ch) {
+    d.nck0 = (d.n0 + ch - 1) / ch;
+    d.nck1 = (d.n1 + ch - 1) / ch;
+    return d;
+}
+// Which swap loop runs, decided on the KL_CHUNK chunk counts: LDS bytes of
+// the on-chip form (0: does not fit / not taken), of the off-chip-bitmap form,
+// and the chunk size the chosen form and its chunk keys use.  kl_prepare and
+// kl_loop both ask, so the keys are built for the loop that reads them.
+struct LoopForm {
+    size_t lds, lds_gb;
+    int ch;
+};
+LoopForm loop_form(const KLDev& d_in) {
+    const KLDev d = with_chunk(d_in, KL_CHUNK);
+    const bool force_gb = std::getenv("EK_KL_GBITS") && std::getenv("EK_KL_GBITS")[0] == '1';
+    const size_t lds = force_gb ? 0 : kl_loop_lds_bytes(d);
+    const size_t lds_gb = d.locked && !std::getenv("EK_KL_GLOBAL_STATE") ? kl_loop_lds_bytes(d, false) : 0;
+    if (!lds && lds_gb) return {0, kl_loop_lds_bytes(with_chunk(d, KL_CHUNK_GB), false), KL_CHUNK_GB};
+    return {lds, lds_gb, KL_CHUNK};
+}
+}  // namespace
+
+void kl_prepare(hipStream_t s, const KLDev& d_in) {
+    const KLDev d = with_chunk(d_in, loop_form(d_in).ch);
     const int nb = (d.n + 255) / 256;
     hipLaunchKernelGGL(k_gain_scan, dim3(nb), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_cut_final, dim3(1), dim3(256), 0, s, d, nb);
     const int waves = d.nck0 + d.nck1;
-    hipLaunchKernelGGL(k_chunk_init, dim3((waves + 3) / 4), dim3(256), 0, s, d);
+    if (loop_form(d_in).ch == KL_CHUNK_GB)
+        hipLaunchKernelGGL(k_chunk_init<KL_CHUNK_GB>, dim3((waves + 3) / 4), dim3(256), 0, s, d);
+    else
+        hipLaunchKernelGGL(k_chunk_init<KL_CHUNK>, dim3((waves + 3) / 4), dim3(256), 0, s, d);
 }
 
 // Streams `n16` 16-B pieces through the caches (nothing kept): after it the
@@ -2456,13 +2497,13 @@ __global__ __launch_bounds__(256) void k_touch(const int4* __restrict__ p, long 
     if (acc == 0x7fffabcd) sink[0] = acc;
 }
 
-void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long cap, KLOut* out) {
+void kl_loop(hipStream_t s, const KLDev& d_in, int limit, ek_swap* log, long long cap, KLOut* out) {
     // the on-chip loop with its bitmaps in LDS; else (a larger graph) with
     // them in global memory while the rest fits (EK_KL_GBITS=1 forces that
-    // form: tests); else the global-state loop
-    const bool force_gb = std::getenv("EK_KL_GBITS") && std::getenv("EK_KL_GBITS")[0] == '1';
-    const size_t lds = force_gb ? 0 : kl_loop_lds_bytes(d);
-    const size_t lds_gb = d.locked && !std::getenv("EK_KL_GLOBAL_STATE") ? kl_loop_lds_bytes(d, false) : 0;
+    // form: tests), over KL_CHUNK_GB-position chunks; else the global-state loop
+    const LoopForm form = loop_form(d_in);
+    const KLDev d = with_chunk(d_in, form.ch);
+    const size_t lds = form.lds, lds_gb = form.lds_gb;
     // Warm the Infinity Cache with the per-entry arrays the swap loop reads at
     // random (inline segments, then descriptors, so the descriptors are the
     // most recent): most of its one dependent round trip per swap then hits
@@ -2497,7 +2538,10 @@ void kl_loop(hipStream_t s, const KLDev& d, int limit, ek_swap* log, long long c
     }
     const bool global_state = std::getenv("EK_KL_GLOBAL_STATE") != nullptr;  // A/B: force the global-state loop
     if (!lds && lds_gb) {
-        if (d.segc)
+        if (prof && d.segc)  // (phase stamps of the off-chip-bitmap form: diagnostic)
+            hipLaunchKernelGGL((k_kl_swap_loop<true, true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_gb, s, d, limit,
+                               log, cap, out);
+        else if (d.segc)
             hipLaunchKernelGGL((k_kl_swap_loop<false, true, true>), dim3(1), dim3(KL_LOOP_THREADS), lds_gb, s, d, limit,
                                log, cap, out);
         else
