@@ -107,8 +107,9 @@ void fiedler_vector(ek_ctx* ctx, int rank, int nranks, const ek_hgr& h, const ek
     (void)nranks;
     auto t = clk::now();
     // the KL adjacency's host thread starts first: the Laplacian rows are
-    // assembled on the GPU, and the adjacency (~25 ms on 12 threads) must
-    // finish within the Lanczos solve (~28 ms) not to stall the KL phase
+    // assembled on the GPU, and the adjacency (~3 ms on 12 threads at the
+    // headline, ~37 ms at 10x) must finish within the Lanczos solve (~17 ms,
+    // ~76 ms) not to stall the KL phase
     if (after_laplacian) after_laplacian();
     // this rank's rows, assembled on the GPU from the pins into the SpMV's
     // coded form (the host build only as ek_spmv_setup_pins' fallback)
