@@ -456,13 +456,16 @@ int ek_init(int device, ek_ctx** out) {
     if (device < 0 || device >= cnt) ek::fail(EK_EINVAL, "device %d out of range [0,%d)", device, cnt);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
+    ek::cold_stamp("hip_props");
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         ek::fail(EK_EHIP, "device %d is %s; this build targets gfx950 (MI355X)", device, prop.gcnArchName);
     auto c = std::make_unique<ek_ctx>();
     c->device = device;
     c->num_cu = std::max(1, prop.multiProcessorCount);
     HIPCHK(hipSetDevice(device));
+    ek::cold_stamp("hip_set_device");
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    ek::cold_stamp("hip_stream0");
     HIPCHK(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
     ek::cold_stamp("hip_streams");
     *out = c.release();

@@ -5,7 +5,8 @@ Runs `gKL2 <hgr> -EIG --quiet` REPS times from a fresh process each and
 reports, per start-up event, the median offset (s) from the launch
 (time.time() before the spawn; the library stamps CLOCK_REALTIME):
 lib_loaded (exec + dynamic loading + static init), main, read_done,
-hip_first_call / hip_device_count / hip_streams (ek_init on its thread),
+hip_first_call / hip_device_count / hip_props / hip_set_device / hip_stream0 /
+hip_streams (ek_init on its thread),
 laplacian_start/done, lanczos_done, kl_start/done, solve_done,
 ctx_destroy_start/done, atexit, and `exit` (the child reaped).
 
